@@ -1,0 +1,365 @@
+// Multi-head self-attention of timm ViT-B/16 (vision_transformer.py Attention with
+// F.scaled_dot_product_attention; N = 197 tokens, 12 heads, head dim 64, scale 1/8).
+//
+// One workgroup (4 waves) per (batch, head).  The whole key/value (or query/dO) sequence is
+// resident in LDS (N padded to a multiple of 32, <= 256), so the softmax is exact over the
+// full row — no online rescaling.  All products are v_mfma_f32_16x16x32_bf16:
+//   forward  S^T = K Q^T (lane owns one query), P in registers, O^T = V^T P^T;
+//   dQ pass  recompute S, P; dP^T = V dO^T; dS = P (dP - delta); dQ^T = K^T dS^T;
+//   dK/dV    key-owned: S = Q K^T, dP = dO V^T; dV^T += dO^T P; dK^T += Q^T dS.
+// Products that contract over the token index use a k-slot permutation (slot 8g+j <-> token
+// 32u + 4g + j for j < 4, 32u + 16 + 4g + j - 4 otherwise) so that accumulator registers
+// feed the next MFMA directly; the matching operand is read with ds_read_b64_tr_b16.
+#include "common.h"
+
+namespace {
+
+// [rows][64] bf16 image, 128-B rows; 16-B chunk index XOR ((row >> 1) & 3) << 1 makes both
+// the ds_read_b128 row reads and the tr_b16 column reads conflict-free.
+DFU_DEV int r128_off(int row, int chunk) { return row * 128 + ((chunk ^ (((row >> 1) & 3) << 1)) << 4); }
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+DFU_DEV bf16x8 row_frag(const char* lds, int rb, int ks, int lane) {
+  return *(const bf16x8*)(lds + r128_off(rb + (lane & 15), ks * 4 + (lane >> 4)));
+}
+// Transposed fragment over token chunk u (32 tokens, slot-permuted), feature tile d0.
+DFU_DEV bf16x8 tr_frag(const char* lds, int u, int d0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = d0 + 4 * p;
+  const int chunk = col >> 3, half = (col >> 2) & 1;
+  const int r0 = 32 * u + 4 * g + q;
+  const char* a0 = lds + r128_off(r0, chunk) + half * 8;
+  const char* a1 = lds + r128_off(r0 + 16, chunk) + half * 8;
+  bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+  bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+  return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+DFU_DEV bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
+  u32x4 w;
+  w[0] = pack2(a[0], a[1]);
+  w[1] = pack2(a[2], a[3]);
+  w[2] = pack2(b[0], b[1]);
+  w[3] = pack2(b[2], b[3]);
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+// Copy rows [0, NPAD) of one (b, h) slice of qkv (which = 0 q, 1 k, 2 v) or of a [B*N][H][64]
+// tensor into an r128 LDS image; rows >= N are zero.
+DFU_DEV void stage_rows(char* lds, const bf16_t* base, int64_t row_stride, int N, int NPAD,
+                        int tid) {
+  for (int idx = tid; idx < NPAD * 8; idx += 256) {
+    const int row = idx >> 3, chunk = idx & 7;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (row < N) v = *(const u32x4*)(base + (int64_t)row * row_stride + chunk * 8);
+    *(u32x4*)(lds + r128_off(row, chunk)) = v;
+  }
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+template <int KT>
+__global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ qkv, int N, int H,
+                                                  float scale, bf16_t* __restrict__ o,
+                                                  float* __restrict__ lse) {
+  constexpr int NPAD = KT * 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NPAD * 128];
+  char* Ks = smem;
+  char* Vs = smem + NPAD * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int64_t tok_stride = (int64_t)3 * H * 64;
+  const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
+  stage_rows(Ks, qbase + H * 64, tok_stride, N, NPAD, tid);
+  stage_rows(Vs, qbase + 2 * H * 64, tok_stride, N, NPAD, tid);
+  __syncthreads();
+  const float c = scale * LOG2E;
+  const int QT = (N + 15) / 16;
+  for (int qt = wave; qt < QT; qt += 4) {
+    const int q = qt * 16 + (lane & 15);
+    bf16x8 qf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (q < N) v = *(const u32x4*)(qbase + (int64_t)q * tok_stride + 32 * ks + 8 * g);
+      qf[ks] = __builtin_bit_cast(bf16x8, v);
+    }
+    f32x4 s[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * t, ks, lane), qf[ks], s[t], 0, 0, 0);
+    }
+    // lane holds S[q][key = 16t + 4g + r]
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * t + 4 * g + r;
+        if (key >= N) s[t][r] = -INFINITY;
+        mx = fmaxf(mx, s[t][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = exp2f((s[t][r] - mx) * c);
+        s[t][r] = pv;
+        l += pv;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 acc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < KT / 2; ++u) {
+      const bf16x8 pb = pack_frag(s[2 * u], s[2 * u + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Vs, u, 16 * dt, lane), pb, acc[dt], 0, 0, 0);
+    }
+    if (q < N) {
+      const float inv = 1.0f / l;
+      bf16_t* orow = o + ((int64_t)b * N + q) * H * 64 + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *(u32x2*)(orow + 16 * dt) = (u32x2){pack2(acc[dt][0] * inv, acc[dt][1] * inv),
+                                            pack2(acc[dt][2] * inv, acc[dt][3] * inv)};
+      if (g == 0) lse[(int64_t)bh * NPAD + q] = mx * scale + logf(l);
+    }
+  }
+}
+
+// dQ (and delta = rowsum(dO * O)), query-owned.
+template <int KT>
+__global__ __launch_bounds__(256) void k_attn_bwd_dq(const bf16_t* __restrict__ qkv,
+                                                     const bf16_t* __restrict__ o,
+                                                     const bf16_t* __restrict__ dout,
+                                                     const float* __restrict__ lse, int N, int H,
+                                                     float scale, float* __restrict__ delta,
+                                                     bf16_t* __restrict__ dqkv) {
+  constexpr int NPAD = KT * 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NPAD * 128];
+  char* Ks = smem;
+  char* Vs = smem + NPAD * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int64_t tok_stride = (int64_t)3 * H * 64;
+  const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
+  const int64_t o_stride = (int64_t)H * 64;
+  const bf16_t* obase = o + (int64_t)b * N * o_stride + h * 64;
+  const bf16_t* dobase = dout + (int64_t)b * N * o_stride + h * 64;
+  stage_rows(Ks, qbase + H * 64, tok_stride, N, NPAD, tid);
+  stage_rows(Vs, qbase + 2 * H * 64, tok_stride, N, NPAD, tid);
+  __syncthreads();
+  const float c = scale * LOG2E;
+  const int QT = (N + 15) / 16;
+  for (int qt = wave; qt < QT; qt += 4) {
+    const int q = qt * 16 + (lane & 15);
+    const bool qv = q < N;
+    bf16x8 qf[2], df[2];
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 vq = {0u, 0u, 0u, 0u}, vd = {0u, 0u, 0u, 0u}, vo = {0u, 0u, 0u, 0u};
+      if (qv) {
+        vq = *(const u32x4*)(qbase + (int64_t)q * tok_stride + 32 * ks + 8 * g);
+        vd = *(const u32x4*)(dobase + (int64_t)q * o_stride + 32 * ks + 8 * g);
+        vo = *(const u32x4*)(obase + (int64_t)q * o_stride + 32 * ks + 8 * g);
+      }
+      qf[ks] = __builtin_bit_cast(bf16x8, vq);
+      df[ks] = __builtin_bit_cast(bf16x8, vd);
+      float fd[8], fo[8];
+      unpack8(vd, fd);
+      unpack8(vo, fo);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum += fd[e] * fo[e];
+    }
+    dsum += __shfl_xor(dsum, 16, 64);
+    dsum += __shfl_xor(dsum, 32, 64);
+    if (g == 0) delta[(int64_t)bh * NPAD + q] = qv ? dsum : 0.f;
+    const float lq = qv ? lse[(int64_t)bh * NPAD + q] * LOG2E : 0.f;
+    f32x4 s[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * t, ks, lane), qf[ks], st, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Vs, 16 * t, ks, lane), df[ks], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * t + 4 * g + r;
+        const float pv = (qv && key < N) ? exp2f(st[r] * c - lq) : 0.f;
+        st[r] = pv * (dp[r] - dsum);
+      }
+      s[t] = st;
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < KT / 2; ++u) {
+      const bf16x8 dsb = pack_frag(s[2 * u], s[2 * u + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ks, u, 16 * dt, lane), dsb, acc[dt], 0, 0, 0);
+    }
+    if (qv) {
+      bf16_t* dst = dqkv + ((int64_t)b * N + q) * tok_stride + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *(u32x2*)(dst + 16 * dt) = (u32x2){pack2(acc[dt][0] * scale, acc[dt][1] * scale),
+                                           pack2(acc[dt][2] * scale, acc[dt][3] * scale)};
+    }
+  }
+}
+
+// dK, dV, key-owned.
+template <int KT>
+__global__ __launch_bounds__(256) void k_attn_bwd_dkv(const bf16_t* __restrict__ qkv,
+                                                      const bf16_t* __restrict__ dout,
+                                                      const float* __restrict__ lse,
+                                                      const float* __restrict__ delta, int N,
+                                                      int H, float scale,
+                                                      bf16_t* __restrict__ dqkv) {
+  constexpr int NPAD = KT * 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NPAD * 128 + 2 * NPAD * 4];
+  char* Qs = smem;
+  char* Ds = smem + NPAD * 128;
+  float* Ls = (float*)(smem + 2 * NPAD * 128);
+  float* Es = Ls + NPAD;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int64_t tok_stride = (int64_t)3 * H * 64;
+  const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
+  const int64_t o_stride = (int64_t)H * 64;
+  stage_rows(Qs, qbase, tok_stride, N, NPAD, tid);
+  stage_rows(Ds, dout + (int64_t)b * N * o_stride + h * 64, o_stride, N, NPAD, tid);
+  for (int i = tid; i < NPAD; i += 256) {
+    Ls[i] = i < N ? lse[(int64_t)bh * NPAD + i] * LOG2E : 0.f;
+    Es[i] = i < N ? delta[(int64_t)bh * NPAD + i] : 0.f;
+  }
+  __syncthreads();
+  const float c = scale * LOG2E;
+  const int KTc = (N + 15) / 16;
+  for (int kt = wave; kt < KTc; kt += 4) {
+    const int key = kt * 16 + (lane & 15);
+    const bool kv = key < N;
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 a = {0u, 0u, 0u, 0u}, v = {0u, 0u, 0u, 0u};
+      if (kv) {
+        a = *(const u32x4*)(qbase + (int64_t)key * tok_stride + H * 64 + 32 * ks + 8 * g);
+        v = *(const u32x4*)(qbase + (int64_t)key * tok_stride + 2 * H * 64 + 32 * ks + 8 * g);
+      }
+      kf[ks] = __builtin_bit_cast(bf16x8, a);
+      vf[ks] = __builtin_bit_cast(bf16x8, v);
+    }
+    f32x4 dv[4], dk[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll 1
+    for (int u = 0; u < KT / 2; ++u) {
+      f32x4 ph[2], dsh[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int qt = 2 * u + hh;
+        f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * qt, ks, lane), kf[ks], st, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * qt, ks, lane), vf[ks], dp, 0, 0, 0);
+        }
+        // lane holds S[q = 16qt + 4g + r][key]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 16 * qt + 4 * g + r;
+          const float pv = (kv && q < N) ? exp2f(st[r] * c - Ls[q]) : 0.f;
+          ph[hh][r] = pv;
+          dsh[hh][r] = pv * (dp[r] - Es[q]);
+        }
+      }
+      const bf16x8 pb = pack_frag(ph[0], ph[1]);
+      const bf16x8 db = pack_frag(dsh[0], dsh[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ds, u, 16 * dt, lane), pb, dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Qs, u, 16 * dt, lane), db, dk[dt], 0, 0, 0);
+      }
+    }
+    if (kv) {
+      bf16_t* dst = dqkv + ((int64_t)b * N + key) * tok_stride + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        *(u32x2*)(dst + H * 64 + 16 * dt) = (u32x2){pack2(dk[dt][0] * scale, dk[dt][1] * scale),
+                                                    pack2(dk[dt][2] * scale, dk[dt][3] * scale)};
+        *(u32x2*)(dst + 2 * H * 64 + 16 * dt) = (u32x2){pack2(dv[dt][0], dv[dt][1]),
+                                                        pack2(dv[dt][2], dv[dt][3])};
+      }
+    }
+  }
+}
+
+#define DISPATCH_KT(KTV, CALL) \
+  switch (KTV) {               \
+    case 2: CALL(2); break;    \
+    case 4: CALL(4); break;    \
+    case 6: CALL(6); break;    \
+    case 8: CALL(8); break;    \
+    case 10: CALL(10); break;  \
+    case 12: CALL(12); break;  \
+    case 14: CALL(14); break;  \
+    case 16: CALL(16); break;  \
+    default: break;            \
+  }
+
+}  // namespace
+
+extern "C" int dfu_attention_npad(int32_t N) { return ((N + 31) / 32) * 32; }
+
+extern "C" int dfu_attention_fwd(const void* qkv, int32_t B, int32_t N, int32_t H, int32_t dh,
+                                 float scale, void* o, float* lse, void* stream) {
+  DFU_CHECK_ARG(qkv && o && lse && B > 0 && H > 0, "dfu_attention_fwd: bad args");
+  DFU_CHECK_ARG(dh == 64, "dfu_attention_fwd: head dim %d unsupported (64 only)", dh);
+  DFU_CHECK_ARG(N > 0 && N <= 256, "dfu_attention_fwd: N=%d unsupported (<= 256)", N);
+  const int KT = dfu_attention_npad(N) / 16;
+  hipStream_t s = (hipStream_t)stream;
+#define CALL(K) hipLaunchKernelGGL(k_attn_fwd<K>, dim3(B * H), dim3(256), 0, s, (const bf16_t*)qkv, N, H, scale, (bf16_t*)o, lse)
+  DISPATCH_KT(KT, CALL)
+#undef CALL
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_attention_bwd(const void* qkv, const void* o, const void* dout,
+                                 const float* lse, int32_t B, int32_t N, int32_t H, int32_t dh,
+                                 float scale, float* delta, void* dqkv, void* stream) {
+  DFU_CHECK_ARG(qkv && o && dout && lse && delta && dqkv && B > 0 && H > 0,
+                "dfu_attention_bwd: bad args");
+  DFU_CHECK_ARG(dh == 64, "dfu_attention_bwd: head dim %d unsupported (64 only)", dh);
+  DFU_CHECK_ARG(N > 0 && N <= 256, "dfu_attention_bwd: N=%d unsupported (<= 256)", N);
+  const int KT = dfu_attention_npad(N) / 16;
+  hipStream_t s = (hipStream_t)stream;
+#define CALL(K) hipLaunchKernelGGL(k_attn_bwd_dq<K>, dim3(B * H), dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse, N, H, scale, delta, (bf16_t*)dqkv)
+  DISPATCH_KT(KT, CALL)
+#undef CALL
+  DFU_LAUNCH_CHECK();
+#define CALL(K) hipLaunchKernelGGL(k_attn_bwd_dkv<K>, dim3(B * H), dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, N, H, scale, (bf16_t*)dqkv)
+  DISPATCH_KT(KT, CALL)
+#undef CALL
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}

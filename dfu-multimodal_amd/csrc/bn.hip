@@ -1,0 +1,303 @@
+// Training-mode BatchNorm2d over NHWC bf16 activations (torchvision resnet.py: every conv is
+// followed by BatchNorm2d(eps=1e-5, momentum=0.1); train_multimodal_fusion.py:375 runs them
+// in train mode).  Forward statistics come from the producing GEMM's epilogue slab
+// (DFU_EPI_BF16_STATS: per 128-row tile, per channel (sum, M2)); this file combines them,
+// applies the normalisation (+ residual, + ReLU), and implements the backward.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- forward finalize
+// Block = 64 tile-lanes x 4 channels; Chan-merge of (count, mean, M2) in fp64.
+__global__ void k_bn_finalize(const float* __restrict__ stats, int tiles, int M, int C,
+                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                              float eps, float momentum, float* __restrict__ rmean,
+                              float* __restrict__ rvar, int64_t* __restrict__ nbt,
+                              float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                              float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  __shared__ double sh_n[4][64], sh_mean[4][64], sh_m2[4][64];
+  const int tl = threadIdx.x & 63, cl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 4 + cl;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  if (c < C) {
+    for (int t = tl; t < tiles; t += 64) {
+      const double nb = (double)min(128, M - t * 128);
+      const double sb = stats[((int64_t)t * 2 + 0) * C + c];
+      const double qb = stats[((int64_t)t * 2 + 1) * C + c];
+      const double mb = sb / nb;
+      const double nt = n + nb;
+      const double d = mb - mean;
+      mean += d * nb / nt;
+      m2 += qb + d * d * n * nb / nt;
+      n = nt;
+    }
+  }
+  sh_n[cl][tl] = n;
+  sh_mean[cl][tl] = mean;
+  sh_m2[cl][tl] = m2;
+  __syncthreads();
+  for (int s = 32; s > 0; s >>= 1) {
+    if (tl < s) {
+      const double na = sh_n[cl][tl], nb = sh_n[cl][tl + s];
+      const double nt = na + nb;
+      if (nb > 0.0) {
+        const double d = sh_mean[cl][tl + s] - sh_mean[cl][tl];
+        sh_mean[cl][tl] += d * nb / nt;
+        sh_m2[cl][tl] += sh_m2[cl][tl + s] + d * d * na * nb / nt;
+        sh_n[cl][tl] = nt;
+      }
+    }
+    __syncthreads();
+  }
+  if (tl == 0 && c < C) {
+    const double nn = sh_n[cl][0];
+    const double mu = sh_mean[cl][0];
+    const double var = sh_m2[cl][0] / nn;  // biased, used to normalise
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f;
+    const float b = beta ? beta[c] : 0.f;
+    mean_out[c] = (float)mu;
+    invstd_out[c] = invstd;
+    scale_out[c] = g * invstd;
+    shift_out[c] = b - (float)mu * g * invstd;
+    if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
+    if (rvar) {
+      const double unb = nn > 1.0 ? sh_m2[cl][0] / (nn - 1.0) : var;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+  }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+}
+
+__global__ void k_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm,
+                                 const float* rv, float eps, int C, float* scale, float* shift) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const float inv = 1.0f / sqrtf(rv[c] + eps);
+    const float g = gamma ? gamma[c] : 1.f;
+    scale[c] = g * inv;
+    shift[c] = (beta ? beta[c] : 0.f) - rm[c] * g * inv;
+  }
+}
+
+// ---------------------------------------------------------------- forward apply
+__global__ void k_bn_apply(const bf16_t* __restrict__ y, const float* __restrict__ scale,
+                           const float* __restrict__ shift, const bf16_t* __restrict__ res,
+                           int relu, bf16_t* __restrict__ out, int64_t M, int C) {
+  const int cv = C / 8;
+  const int64_t n = M * cv;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * 8;
+    float f[8];
+    unpack8(*(const u32x4*)(y + i * 8), f);
+    float r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (res) unpack8(*(const u32x4*)(res + i * 8), r);
+    const f32x4 s0 = *(const f32x4*)(scale + c0), s1 = *(const f32x4*)(scale + c0 + 4);
+    const f32x4 h0 = *(const f32x4*)(shift + c0), h1 = *(const f32x4*)(shift + c0 + 4);
+    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    const float sf[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = fmaf(f[e], sc[e], sf[e]) + r[e];
+      f[e] = relu ? fmaxf(v, 0.f) : v;
+    }
+    *(u32x4*)(out + i * 8) = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// Block of 256 threads = CT column-threads (8 channels each) x (256/CT) row-lanes.
+inline int bwd_rows_per_block(int64_t M) { return M >= 65536 ? 512 : 64; }
+
+__global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ y,
+                                const bf16_t* __restrict__ out, int relu,
+                                const float* __restrict__ mean, const float* __restrict__ invstd,
+                                int64_t M, int C, int rows_per_block, float* __restrict__ partial) {
+  __shared__ float red[2][256][8];
+  const int cv = C / 8;
+  const int ct_n = min(cv, 64);
+  const int rl_n = 256 / ct_n;
+  const int ct = threadIdx.x % ct_n, rl = threadIdx.x / ct_n;
+  const int c8 = blockIdx.x * ct_n + ct;
+  const int c0 = c8 * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], is[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e]; }
+  for (int64_t r = r0 + rl; r < r1; r += rl_n) {
+    const int64_t o = r * C + c0;
+    float g[8], yy[8];
+    unpack8(*(const u32x4*)(dout + o), g);
+    unpack8(*(const u32x4*)(y + o), yy);
+    if (relu) {
+      float oo[8];
+      unpack8(*(const u32x4*)(out + o), oo);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = oo[e] > 0.f ? g[e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sg[e] += g[e];
+      sgx[e] += g[e] * (yy[e] - mu[e]) * is[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][threadIdx.x][e] = sg[e]; red[1][threadIdx.x][e] = sgx[e]; }
+  __syncthreads();
+  if (rl == 0) {
+    for (int l = 1; l < rl_n; ++l) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sg[e] += red[0][l * ct_n + ct][e];
+        sgx[e] += red[1][l * ct_n + ct][e];
+      }
+    }
+    float* p0 = partial + ((int64_t)blockIdx.y * 2 + 0) * C + c0;
+    float* p1 = partial + ((int64_t)blockIdx.y * 2 + 1) * C + c0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { p0[e] = sg[e]; p1[e] = sgx[e]; }
+  }
+}
+
+__global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int blocks, int64_t M, int C,
+                                  const float* __restrict__ gamma,
+                                  const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                  float* __restrict__ dbeta, float* __restrict__ coef) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    double sg = 0.0, sgx = 0.0;
+    for (int b = 0; b < blocks; ++b) {
+      sg += partial[((int64_t)b * 2 + 0) * C + c];
+      sgx += partial[((int64_t)b * 2 + 1) * C + c];
+    }
+    if (dbeta) dbeta[c] += (float)sg;
+    if (dgamma) dgamma[c] += (float)sgx;
+    const float g = gamma ? gamma[c] : 1.f;
+    coef[3 * c + 0] = g * invstd[c];
+    coef[3 * c + 1] = (float)(sg / (double)M);
+    coef[3 * c + 2] = (float)(sgx / (double)M);
+  }
+}
+
+__global__ void k_bn_bwd_apply(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ y,
+                               const bf16_t* __restrict__ out, int relu,
+                               const float* __restrict__ mean, const float* __restrict__ invstd,
+                               const float* __restrict__ coef, int64_t M, int C,
+                               bf16_t* __restrict__ dy, bf16_t* __restrict__ dres) {
+  const int cv = C / 8;
+  const int64_t n = M * cv;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * 8;
+    float g[8], yy[8];
+    unpack8(*(const u32x4*)(dout + i * 8), g);
+    unpack8(*(const u32x4*)(y + i * 8), yy);
+    if (relu) {
+      float oo[8];
+      unpack8(*(const u32x4*)(out + i * 8), oo);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = oo[e] > 0.f ? g[e] : 0.f;
+    }
+    if (dres) *(u32x4*)(dres + i * 8) = pack8(g);
+    float d[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      const float xh = (yy[e] - mean[c]) * invstd[c];
+      d[e] = coef[3 * c] * (g[e] - coef[3 * c + 1] - xh * coef[3 * c + 2]);
+    }
+    *(u32x4*)(dy + i * 8) = pack8(d);
+  }
+}
+
+inline unsigned grid_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 65536) b = 65536;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" int dfu_bn_finalize(const float* stats, int32_t tiles, int32_t M, int32_t C,
+                               const float* gamma, const float* beta, float eps, float momentum,
+                               float* running_mean, float* running_var, int64_t* num_batches,
+                               float* mean_out, float* invstd_out, float* scale_out,
+                               float* shift_out, void* stream) {
+  DFU_CHECK_ARG(stats && tiles == (M + 127) / 128 && C > 0 && mean_out && invstd_out &&
+                    scale_out && shift_out,
+                "dfu_bn_finalize: bad args (tiles=%d M=%d)", tiles, M);
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 3) / 4), dim3(256), 0, (hipStream_t)stream, stats,
+                     tiles, M, C, gamma, beta, eps, momentum, running_mean, running_var,
+                     num_batches, mean_out, invstd_out, scale_out, shift_out);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_bn_eval_coeffs(const float* gamma, const float* beta, const float* running_mean,
+                                  const float* running_var, float eps, int32_t C,
+                                  float* scale_out, float* shift_out, void* stream) {
+  DFU_CHECK_ARG(running_mean && running_var && scale_out && shift_out && C > 0,
+                "dfu_bn_eval_coeffs: bad args");
+  hipLaunchKernelGGL(k_bn_eval_coeffs, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     gamma, beta, running_mean, running_var, eps, C, scale_out, shift_out);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_bn_apply(const void* y, const float* scale, const float* shift,
+                            const void* residual, int32_t relu, void* out, int64_t M, int32_t C,
+                            void* stream) {
+  DFU_CHECK_ARG(y && scale && shift && out && C % 8 == 0 && M > 0, "dfu_bn_apply: bad args");
+  hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)y, scale, shift, (const bf16_t*)residual, relu, (bf16_t*)out,
+                     M, C);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_bn_bwd_blocks(int64_t M) {
+  const int rpb = bwd_rows_per_block(M);
+  return (int)((M + rpb - 1) / rpb);
+}
+
+extern "C" int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* out, int32_t relu,
+                                 const float* mean, const float* invstd, int64_t M, int32_t C,
+                                 float* partial, void* stream) {
+  DFU_CHECK_ARG(dout && y && mean && invstd && partial && C % 8 == 0 && M > 0,
+                "dfu_bn_bwd_reduce: bad args");
+  DFU_CHECK_ARG(!relu || out, "dfu_bn_bwd_reduce: relu needs out");
+  const int cv = C / 8;
+  const int ct_n = cv < 64 ? cv : 64;
+  DFU_CHECK_ARG(256 % ct_n == 0 && cv % ct_n == 0, "dfu_bn_bwd_reduce: C=%d unsupported", C);
+  const int rpb = bwd_rows_per_block(M);
+  dim3 grid(cv / ct_n, dfu_bn_bwd_blocks(M));
+  hipLaunchKernelGGL(k_bn_bwd_reduce, grid, dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, relu, mean, invstd,
+                     M, C, rpb, partial);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t M, int32_t C,
+                                   const float* gamma, const float* invstd, float* dgamma,
+                                   float* dbeta, float* coef, void* stream) {
+  DFU_CHECK_ARG(partial && invstd && coef && blocks > 0 && C > 0, "dfu_bn_bwd_finalize: bad args");
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     partial, blocks, M, C, gamma, invstd, dgamma, dbeta, coef);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t relu,
+                                const float* mean, const float* invstd, const float* coef,
+                                int64_t M, int32_t C, void* dy, void* dres, void* stream) {
+  DFU_CHECK_ARG(dout && y && mean && invstd && coef && dy && C % 8 == 0 && M > 0,
+                "dfu_bn_bwd_apply: bad args");
+  DFU_CHECK_ARG(!relu || out, "dfu_bn_bwd_apply: relu needs out");
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, relu, mean, invstd,
+                     coef, M, C, (bf16_t*)dy, (bf16_t*)dres);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}

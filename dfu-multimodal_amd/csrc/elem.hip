@@ -1,0 +1,679 @@
+// Layout, pooling and elementwise kernels of the DFU training step (HBM-bound; every kernel
+// moves 16-B vectors per lane).  Reference ops replaced are named per entry point in
+// include/dfu_hip.h.
+#include "common.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+inline unsigned nblocks(int64_t n, int per_block = TPB) {
+  int64_t b = (n + per_block - 1) / per_block;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+// ---------------------------------------------------------------- weight packing
+__global__ void k_pack_conv_weight(const float* __restrict__ w, bf16_t* __restrict__ out, int K,
+                                   int C, int R, int S) {
+  const int64_t n = (int64_t)K * R * S * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    // out index i = ((k*R + r)*S + s)*C + c
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int s = (int)(t % S);
+    t /= S;
+    int r = (int)(t % R);
+    int k = (int)(t / R);
+    out[i] = f2bf(w[(((int64_t)k * C + c) * R + r) * S + s]);
+  }
+}
+
+__global__ void k_cast_rows_bf16(const float* __restrict__ in, int64_t ld_in,
+                                 bf16_t* __restrict__ out, int64_t ld_out, int rows, int cols) {
+  const int64_t n = (int64_t)rows * ld_out;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / ld_out;
+    const int c = (int)(i - r * ld_out);
+    out[i] = c < cols ? f2bf(in[r * ld_in + c]) : (bf16_t)0;
+  }
+}
+
+__global__ void k_cast_rows_f32(const bf16_t* __restrict__ in, int64_t ld_in,
+                                float* __restrict__ out, int64_t ld_out, int rows, int cols) {
+  const int64_t n = (int64_t)rows * cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols;
+    const int c = (int)(i - r * cols);
+    out[r * ld_out + c] = bf2f(in[r * ld_in + c]);
+  }
+}
+
+// ---------------------------------------------------------------- stem im2col / patchify
+// out[m][k], m = (b, oh, ow), k = c*R*S + r*S + s; each thread writes one 16-B vector (8 k).
+__global__ void k_im2col_f32(const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh,
+                             int64_t sw, int B, int C, int H, int W, int R, int S, int stride,
+                             int pad, int P, int Q, bf16_t* __restrict__ out, int Kp) {
+  const int vec_per_row = Kp / 8;
+  const int64_t n = (int64_t)B * P * Q * vec_per_row;
+  const int KK = C * R * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / vec_per_row;
+    const int kv = (int)(i - m * vec_per_row);
+    const int b = (int)(m / (P * Q));
+    const int rem = (int)(m - (int64_t)b * P * Q);
+    const int oh = rem / Q, ow = rem - (rem / Q) * Q;
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = kv * 8 + e;
+      float v = 0.f;
+      if (k < KK) {
+        const int c = k / (R * S);
+        const int rs = k - c * R * S;
+        const int r = rs / S, s = rs - (rs / S) * S;
+        const int ih = oh * stride - pad + r, iw = ow * stride - pad + s;
+        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+          v = x[b * sn + c * sc + ih * sh + iw * sw];
+      }
+      f[e] = v;
+    }
+    *(u32x4*)(out + m * Kp + kv * 8) = pack8(f);
+  }
+}
+
+__global__ void k_patchify_f32(const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh,
+                               int64_t sw, int B, int C, int H, int W, int ps,
+                               bf16_t* __restrict__ out) {
+  const int gh = H / ps, gw = W / ps;
+  const int K = C * ps * ps;
+  const int vec_per_row = K / 8;
+  const int64_t n = (int64_t)B * gh * gw * vec_per_row;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / vec_per_row;
+    const int kv = (int)(i - m * vec_per_row);
+    const int b = (int)(m / (gh * gw));
+    const int pidx = (int)(m - (int64_t)b * gh * gw);
+    const int py = pidx / gw, px = pidx - (pidx / gw) * gw;
+    const int k0 = kv * 8;
+    const int c = k0 / (ps * ps);
+    const int rem = k0 - c * ps * ps;
+    const int kh = rem / ps, kw0 = rem - (rem / ps) * ps;  // ps % 8 == 0: 8 consecutive kw
+    const float* src = x + b * sn + c * sc + (py * ps + kh) * sh + (px * ps + kw0) * sw;
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = src[e * sw];
+    *(u32x4*)(out + m * K + k0) = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------- max / avg pooling
+// 3x3 / stride 2 / pad 1 (torchvision resnet maxpool); first max in row-major window order
+// wins, as ATen's max_pool2d_with_indices.
+__global__ void k_maxpool_fwd(const bf16_t* __restrict__ x, int B, int H, int W, int C,
+                              bf16_t* __restrict__ y, uint8_t* __restrict__ am, int P, int Q) {
+  const int cv = C / 8;
+  const int64_t n = (int64_t)B * P * Q * cv;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cv);
+    const int64_t pix = i / cv;
+    const int q = (int)(pix % Q);
+    const int64_t t = pix / Q;
+    const int p = (int)(t % P);
+    const int b = (int)(t / P);
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+    for (int wi = 0; wi < 3; ++wi) {
+      const int ih = 2 * p - 1 + wi;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int wj = 0; wj < 3; ++wj) {
+        const int iw = 2 * q - 1 + wj;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const u32x4 v = *(const u32x4*)(x + (((int64_t)b * H + ih) * W + iw) * C + c8 * 8);
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (f[e] > best[e] || (f[e] != f[e] && best[e] == best[e])) {
+            best[e] = f[e];
+            arg[e] = wi * 3 + wj;
+          }
+      }
+    }
+    *(u32x4*)(y + pix * C + c8 * 8) = pack8(best);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) packed |= (uint64_t)arg[e] << (8 * e);
+    *(uint64_t*)(am + pix * C + c8 * 8) = packed;
+  }
+}
+
+// Gather form (deterministic): every input pixel sums dy of the windows whose argmax it is.
+__global__ void k_maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ am,
+                              int B, int H, int W, int C, int P, int Q, bf16_t* __restrict__ dx) {
+  const int cv = C / 8;
+  const int64_t n = (int64_t)B * H * W * cv;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cv);
+    const int64_t pix = i / cv;
+    const int w = (int)(pix % W);
+    const int64_t t = pix / W;
+    const int h = (int)(t % H);
+    const int b = (int)(t / H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // windows p with 2p-1 <= h <= 2p+1
+    const int p_lo = max(0, h / 2), p_hi = min(P - 1, (h + 1) / 2);
+    const int q_lo = max(0, w / 2), q_hi = min(Q - 1, (w + 1) / 2);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int wi = h - (2 * p - 1);
+      if (wi < 0 || wi > 2) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int wj = w - (2 * q - 1);
+        if (wj < 0 || wj > 2) continue;
+        const int64_t o = (((int64_t)b * P + p) * Q + q) * C + c8 * 8;
+        const uint64_t a = *(const uint64_t*)(am + o);
+        const u32x4 g = *(const u32x4*)(dy + o);
+        float f[8];
+        unpack8(g, f);
+        const int want = wi * 3 + wj;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((int)((a >> (8 * e)) & 0xff) == want) acc[e] += f[e];
+      }
+    }
+    *(u32x4*)(dx + pix * C + c8 * 8) = pack8(acc);
+  }
+}
+
+__global__ void k_avgpool_fwd(const bf16_t* __restrict__ x, int B, int HW, int C,
+                              float* __restrict__ y) {
+  const int cv = C / 8;
+  const int64_t n = (int64_t)B * cv;
+  const float inv = 1.0f / (float)HW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cv);
+    const int b = (int)(i / cv);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16_t* src = x + (int64_t)b * HW * C + c8 * 8;
+    for (int t = 0; t < HW; ++t) {
+      float f[8];
+      unpack8(*(const u32x4*)(src + (int64_t)t * C), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += f[e];
+    }
+    float* dst = y + (int64_t)b * C + c8 * 8;
+    *(f32x4*)dst = (f32x4){acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv};
+    *(f32x4*)(dst + 4) = (f32x4){acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv};
+  }
+}
+
+__global__ void k_avgpool_bwd(const float* __restrict__ dy, int B, int HW, int C,
+                              bf16_t* __restrict__ dx) {
+  const int cv = C / 8;
+  const int64_t n = (int64_t)B * HW * cv;
+  const float inv = 1.0f / (float)HW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cv);
+    const int64_t pix = i / cv;
+    const int b = (int)(pix / HW);
+    const float* g = dy + (int64_t)b * C + c8 * 8;
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = g[e] * inv;
+    *(u32x4*)(dx + pix * C + c8 * 8) = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------- column sums (bias grads)
+// Block = 64 column-threads (8 columns each = 512 columns) x 4 row-lanes; ROWS rows per block.
+constexpr int CS_ROWS = 128;
+template <bool BF>
+__global__ void k_colsum(const void* __restrict__ xv, int64_t ld, int rows, int N,
+                         float* __restrict__ partial) {
+  __shared__ float red[4][512];
+  const int ct = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + ct * 8;
+  const int r0 = blockIdx.y * CS_ROWS;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (col < N) {
+    for (int r = r0 + rl; r < min(rows, r0 + CS_ROWS); r += 4) {
+      if constexpr (BF) {
+        const bf16_t* x = (const bf16_t*)xv + (int64_t)r * ld + col;
+        if (col + 8 <= N) {
+          float f[8];
+          unpack8(*(const u32x4*)x, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += f[e];
+        } else {
+          for (int e = 0; e < 8 && col + e < N; ++e) acc[e] += bf2f(x[e]);
+        }
+      } else {
+        const float* x = (const float*)xv + (int64_t)r * ld + col;
+        for (int e = 0; e < 8 && col + e < N; ++e) acc[e] += x[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][ct * 8 + e] = acc[e];
+  __syncthreads();
+  if (rl == 0 && col < N) {
+    for (int e = 0; e < 8 && col + e < N; ++e) {
+      const float s = red[0][ct * 8 + e] + red[1][ct * 8 + e] + red[2][ct * 8 + e] +
+                      red[3][ct * 8 + e];
+      partial[(int64_t)blockIdx.y * N + col + e] = s;
+    }
+  }
+}
+
+// out_v[d] += sum_b partial[b][v][d]
+__global__ void k_reduce_partials(const float* __restrict__ partial, int blocks, int nvec, int D,
+                                  float* __restrict__ out0, float* __restrict__ out1) {
+  const int64_t n = (int64_t)nvec * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int v = (int)(i / D);
+    const int d = (int)(i - (int64_t)v * D);
+    float s = 0.f;
+    for (int b = 0; b < blocks; ++b) s += partial[((int64_t)b * nvec + v) * D + d];
+    float* o = v == 0 ? out0 : out1;
+    if (o) o[d] += s;
+  }
+}
+
+// ---------------------------------------------------------------- rows gather / scatter
+__global__ void k_gather_rows(const float* __restrict__ in, int64_t ld_in, int stride, int offset,
+                              int rows, int D, float* __restrict__ out, int64_t ld_out) {
+  const int64_t n = (int64_t)rows * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / D);
+    const int d = (int)(i - (int64_t)r * D);
+    out[(int64_t)r * ld_out + d] = in[((int64_t)r * stride + offset) * ld_in + d];
+  }
+}
+__global__ void k_scatter_rows(const float* __restrict__ in, int64_t ld_in, int stride, int offset,
+                               int rows, int D, float* __restrict__ out, int64_t ld_out) {
+  const int64_t n = (int64_t)rows * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / D);
+    const int d = (int)(i - (int64_t)r * D);
+    out[((int64_t)r * stride + offset) * ld_out + d] += in[(int64_t)r * ld_in + d];
+  }
+}
+
+// ---------------------------------------------------------------- relu / dropout
+template <bool BF>
+__global__ void k_relu_fwd(const void* __restrict__ x, void* __restrict__ y, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if constexpr (BF) {
+      const bf16_t v = ((const bf16_t*)x)[i];
+      ((bf16_t*)y)[i] = (v & 0x8000) ? (bf16_t)0 : v;
+    } else {
+      ((float*)y)[i] = fmaxf(((const float*)x)[i], 0.f);
+    }
+  }
+}
+template <bool BF>
+__global__ void k_relu_bwd(const void* __restrict__ dy, const void* __restrict__ y,
+                           void* __restrict__ dx, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if constexpr (BF) {
+      const float yy = bf2f(((const bf16_t*)y)[i]);
+      ((bf16_t*)dx)[i] = yy > 0.f ? ((const bf16_t*)dy)[i] : (bf16_t)0;
+    } else {
+      const float yy = ((const float*)y)[i];
+      ((float*)dx)[i] = yy > 0.f ? ((const float*)dy)[i] : 0.f;
+    }
+  }
+}
+
+DFU_DEV uint32_t hash_u32(uint64_t seed, uint64_t ctr) {
+  // splitmix64 finaliser on (seed ^ counter): counter-based, stateless, graph-replay safe
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+template <bool BF>
+__global__ void k_dropout_fwd(const void* __restrict__ x, void* __restrict__ y,
+                              uint8_t* __restrict__ mask, int64_t n, float p, uint64_t seed,
+                              const int64_t* __restrict__ offset_dev) {
+  const uint64_t base = (uint64_t)(*offset_dev);
+  const float scale = 1.0f / (1.0f - p);
+  const uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bool keep = hash_u32(seed, base + (uint64_t)i) >= thr;
+    mask[i] = keep ? 1 : 0;
+    if constexpr (BF) {
+      ((bf16_t*)y)[i] = f2bf(keep ? bf2f(((const bf16_t*)x)[i]) * scale : 0.f);
+    } else {
+      ((float*)y)[i] = keep ? ((const float*)x)[i] * scale : 0.f;
+    }
+  }
+}
+__global__ void k_advance(int64_t* off, int64_t n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *off += n;
+}
+template <bool BF>
+__global__ void k_dropout_bwd(const void* __restrict__ dy, const uint8_t* __restrict__ mask,
+                              void* __restrict__ dx, int64_t n, float p) {
+  const float scale = 1.0f / (1.0f - p);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bool keep = mask[i] != 0;
+    if constexpr (BF) {
+      ((bf16_t*)dx)[i] = f2bf(keep ? bf2f(((const bf16_t*)dy)[i]) * scale : 0.f);
+    } else {
+      ((float*)dx)[i] = keep ? ((const float*)dy)[i] * scale : 0.f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- concat / split
+__global__ void k_concat2(const void* __restrict__ a, int a_bf, int Na, const void* __restrict__ b,
+                          int b_bf, int Nb, int rows, bf16_t* __restrict__ out) {
+  const int N = Na + Nb;
+  const int64_t n = (int64_t)rows * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / N);
+    const int c = (int)(i - (int64_t)r * N);
+    float v;
+    if (c < Na) v = a_bf ? bf2f(((const bf16_t*)a)[(int64_t)r * Na + c]) : ((const float*)a)[(int64_t)r * Na + c];
+    else v = b_bf ? bf2f(((const bf16_t*)b)[(int64_t)r * Nb + c - Na]) : ((const float*)b)[(int64_t)r * Nb + c - Na];
+    out[i] = f2bf(v);
+  }
+}
+__global__ void k_split2(const void* __restrict__ g, int g_bf, int rows, int Na, int Nb,
+                         float* __restrict__ ga, float* __restrict__ gb) {
+  const int N = Na + Nb;
+  const int64_t n = (int64_t)rows * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / N);
+    const int c = (int)(i - (int64_t)r * N);
+    const float v = g_bf ? bf2f(((const bf16_t*)g)[i]) : ((const float*)g)[i];
+    if (c < Na) { if (ga) ga[(int64_t)r * Na + c] = v; }
+    else if (gb) gb[(int64_t)r * Nb + c - Na] = v;
+  }
+}
+
+// ---------------------------------------------------------------- ViT embedding
+__global__ void k_vit_cls_rows(const float* __restrict__ cls, const float* __restrict__ pos,
+                               float* __restrict__ x, int B, int T, int D) {
+  const int64_t n = (int64_t)B * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / D);
+    const int d = (int)(i - (int64_t)b * D);
+    x[(int64_t)b * T * D + d] = cls[d] + pos[d];
+  }
+}
+// one thread per (t, d): sum over the batch
+__global__ void k_vit_embed_bwd(const float* __restrict__ gx, int B, int T, int D,
+                                float* __restrict__ dcls, float* __restrict__ dpos,
+                                bf16_t* __restrict__ gpatch, float* __restrict__ partial) {
+  const int64_t n = (int64_t)T * D;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i / D);
+    const int d = (int)(i - (int64_t)t * D);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float v = gx[((int64_t)b * T + t) * D + d];
+      s += v;
+      if (t > 0) gpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = f2bf(v);
+    }
+    if (dpos) dpos[i] += s;
+    if (t == 0) {
+      if (dcls) dcls[d] += s;
+      partial[i] = 0.f;
+    } else {
+      partial[i] = s;
+    }
+  }
+}
+__global__ void k_sum_rows_add(const float* __restrict__ partial, int T, int D,
+                               float* __restrict__ out) {
+  for (int d = blockIdx.x * blockDim.x + threadIdx.x; d < D; d += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) s += partial[(int64_t)t * D + d];
+    out[d] += s;
+  }
+}
+
+__global__ void k_argmax_rows(const float* __restrict__ x, int rows, int C,
+                              int64_t* __restrict__ out) {
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += gridDim.x * blockDim.x) {
+    int best = 0;
+    float bv = x[(int64_t)r * C];
+    for (int c = 1; c < C; ++c) {
+      const float v = x[(int64_t)r * C + c];
+      if (v > bv) { bv = v; best = c; }
+    }
+    out[r] = best;
+  }
+}
+
+inline unsigned grid_for(int64_t n) {
+  int64_t b = (n + TPB - 1) / TPB;
+  if (b > 65536) b = 65536;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+#define LAUNCH(kern, n, stream, ...)                                                     \
+  do {                                                                                   \
+    hipLaunchKernelGGL(kern, dim3(grid_for(n)), dim3(TPB), 0, (hipStream_t)(stream),     \
+                       __VA_ARGS__);                                                     \
+    DFU_LAUNCH_CHECK();                                                                  \
+  } while (0)
+
+extern "C" int dfu_pack_conv_weight(const float* w, void* out, int32_t K, int32_t C, int32_t R,
+                                    int32_t S, void* stream) {
+  DFU_CHECK_ARG(w && out && K > 0 && C > 0 && R > 0 && S > 0, "dfu_pack_conv_weight: bad args");
+  LAUNCH(k_pack_conv_weight, (int64_t)K * C * R * S, stream, w, (bf16_t*)out, K, C, R, S);
+  return DFU_OK;
+}
+
+extern "C" int dfu_cast_rows_bf16(const float* in, int64_t ld_in, void* out, int64_t ld_out,
+                                  int32_t rows, int32_t cols, void* stream) {
+  DFU_CHECK_ARG(in && out && rows > 0 && cols > 0 && ld_out >= cols && ld_in >= cols,
+                "dfu_cast_rows_bf16: bad args");
+  LAUNCH(k_cast_rows_bf16, (int64_t)rows * ld_out, stream, in, ld_in, (bf16_t*)out, ld_out, rows,
+         cols);
+  return DFU_OK;
+}
+
+extern "C" int dfu_cast_rows_f32(const void* in, int64_t ld_in, float* out, int64_t ld_out,
+                                 int32_t rows, int32_t cols, void* stream) {
+  DFU_CHECK_ARG(in && out && rows > 0 && cols > 0, "dfu_cast_rows_f32: bad args");
+  LAUNCH(k_cast_rows_f32, (int64_t)rows * cols, stream, (const bf16_t*)in, ld_in, out, ld_out,
+         rows, cols);
+  return DFU_OK;
+}
+
+extern "C" int dfu_im2col_f32(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
+                              int32_t B, int32_t C, int32_t H, int32_t W, int32_t R, int32_t S,
+                              int32_t stride, int32_t pad, int32_t P, int32_t Q, void* out,
+                              int32_t Kp, void* stream) {
+  DFU_CHECK_ARG(x && out && Kp % 8 == 0 && Kp >= C * R * S, "dfu_im2col_f32: bad Kp=%d", Kp);
+  DFU_CHECK_ARG(((uintptr_t)out & 15) == 0, "dfu_im2col_f32: out must be 16-B aligned");
+  LAUNCH(k_im2col_f32, (int64_t)B * P * Q * (Kp / 8), stream, x, sn, sc, sh, sw, B, C, H, W, R,
+         S, stride, pad, P, Q, (bf16_t*)out, Kp);
+  return DFU_OK;
+}
+
+extern "C" int dfu_patchify_f32(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
+                                int32_t B, int32_t C, int32_t H, int32_t W, int32_t ps, void* out,
+                                void* stream) {
+  DFU_CHECK_ARG(x && out && ps % 8 == 0 && H % ps == 0 && W % ps == 0,
+                "dfu_patchify_f32: bad patch size %d for %dx%d", ps, H, W);
+  const int64_t n = (int64_t)B * (H / ps) * (W / ps) * (C * ps * ps / 8);
+  LAUNCH(k_patchify_f32, n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
+  return DFU_OK;
+}
+
+extern "C" int dfu_maxpool_fwd(const void* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y,
+                               uint8_t* argmax, int32_t P, int32_t Q, void* stream) {
+  DFU_CHECK_ARG(x && y && argmax && C % 8 == 0, "dfu_maxpool_fwd: C %% 8 != 0");
+  DFU_CHECK_ARG(P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1, "dfu_maxpool_fwd: bad P/Q");
+  LAUNCH(k_maxpool_fwd, (int64_t)B * P * Q * (C / 8), stream, (const bf16_t*)x, B, H, W, C,
+         (bf16_t*)y, argmax, P, Q);
+  return DFU_OK;
+}
+
+extern "C" int dfu_maxpool_bwd(const void* dy, const uint8_t* argmax, int32_t B, int32_t H,
+                               int32_t W, int32_t C, int32_t P, int32_t Q, void* dx,
+                               void* stream) {
+  DFU_CHECK_ARG(dy && dx && argmax && C % 8 == 0, "dfu_maxpool_bwd: C %% 8 != 0");
+  LAUNCH(k_maxpool_bwd, (int64_t)B * H * W * (C / 8), stream, (const bf16_t*)dy, argmax, B, H, W,
+         C, P, Q, (bf16_t*)dx);
+  return DFU_OK;
+}
+
+extern "C" int dfu_avgpool_fwd(const void* x, int32_t B, int32_t HW, int32_t C, float* y,
+                               void* stream) {
+  DFU_CHECK_ARG(x && y && C % 8 == 0, "dfu_avgpool_fwd: C %% 8 != 0");
+  LAUNCH(k_avgpool_fwd, (int64_t)B * (C / 8), stream, (const bf16_t*)x, B, HW, C, y);
+  return DFU_OK;
+}
+
+extern "C" int dfu_avgpool_bwd(const float* dy, int32_t B, int32_t HW, int32_t C, void* dx,
+                               void* stream) {
+  DFU_CHECK_ARG(dy && dx && C % 8 == 0, "dfu_avgpool_bwd: C %% 8 != 0");
+  LAUNCH(k_avgpool_bwd, (int64_t)B * HW * (C / 8), stream, dy, B, HW, C, (bf16_t*)dx);
+  return DFU_OK;
+}
+
+extern "C" int dfu_colsum_blocks(int32_t rows) { return (rows + CS_ROWS - 1) / CS_ROWS; }
+
+extern "C" int dfu_colsum(const void* x, int32_t is_bf16, int64_t ld, int32_t rows, int32_t N,
+                          float* out, float* partial, void* stream) {
+  DFU_CHECK_ARG(x && out && partial && rows > 0 && N > 0, "dfu_colsum: bad args");
+  if (is_bf16) DFU_CHECK_ARG(ld % 8 == 0 && ((uintptr_t)x & 15) == 0, "dfu_colsum: bf16 needs ld%%8==0");
+  const int blocks = dfu_colsum_blocks(rows);
+  dim3 grid((N + 511) / 512, blocks);
+  if (is_bf16)
+    hipLaunchKernelGGL(k_colsum<true>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, rows, N, partial);
+  else
+    hipLaunchKernelGGL(k_colsum<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, rows, N, partial);
+  DFU_LAUNCH_CHECK();
+  LAUNCH(k_reduce_partials, (int64_t)N, stream, partial, blocks, 1, N, out, (float*)nullptr);
+  return DFU_OK;
+}
+
+extern "C" int dfu_reduce_partials(const float* partial, int32_t blocks, int32_t nvec, int32_t D,
+                                   float* out0, float* out1, void* stream) {
+  DFU_CHECK_ARG(partial && blocks > 0 && nvec >= 1 && nvec <= 2 && D > 0, "dfu_reduce_partials: bad args");
+  LAUNCH(k_reduce_partials, (int64_t)nvec * D, stream, partial, blocks, nvec, D, out0, out1);
+  return DFU_OK;
+}
+
+extern "C" int dfu_gather_rows_f32(const float* in, int64_t ld_in, int32_t stride, int32_t offset,
+                                   int32_t rows, int32_t D, float* out, int64_t ld_out,
+                                   void* stream) {
+  DFU_CHECK_ARG(in && out && rows > 0 && D > 0, "dfu_gather_rows_f32: bad args");
+  LAUNCH(k_gather_rows, (int64_t)rows * D, stream, in, ld_in, stride, offset, rows, D, out, ld_out);
+  return DFU_OK;
+}
+
+extern "C" int dfu_scatter_rows_f32(const float* in, int64_t ld_in, int32_t stride, int32_t offset,
+                                    int32_t rows, int32_t D, float* out, int64_t ld_out,
+                                    void* stream) {
+  DFU_CHECK_ARG(in && out && rows > 0 && D > 0, "dfu_scatter_rows_f32: bad args");
+  LAUNCH(k_scatter_rows, (int64_t)rows * D, stream, in, ld_in, stride, offset, rows, D, out, ld_out);
+  return DFU_OK;
+}
+
+extern "C" int dfu_relu_fwd(const void* x, void* y, int64_t n, int32_t is_bf16, void* stream) {
+  DFU_CHECK_ARG(x && y && n >= 0, "dfu_relu_fwd: bad args");
+  if (n == 0) return DFU_OK;
+  if (is_bf16) LAUNCH(k_relu_fwd<true>, n, stream, x, y, n);
+  else LAUNCH(k_relu_fwd<false>, n, stream, x, y, n);
+  return DFU_OK;
+}
+
+extern "C" int dfu_relu_bwd(const void* dy, const void* y, void* dx, int64_t n, int32_t is_bf16,
+                            void* stream) {
+  DFU_CHECK_ARG(dy && y && dx && n >= 0, "dfu_relu_bwd: bad args");
+  if (n == 0) return DFU_OK;
+  if (is_bf16) LAUNCH(k_relu_bwd<true>, n, stream, dy, y, dx, n);
+  else LAUNCH(k_relu_bwd<false>, n, stream, dy, y, dx, n);
+  return DFU_OK;
+}
+
+extern "C" int dfu_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float p,
+                               uint64_t seed, int64_t* offset_dev, int32_t is_bf16, void* stream) {
+  DFU_CHECK_ARG(x && y && mask && offset_dev && p >= 0.f && p < 1.f, "dfu_dropout_fwd: bad args");
+  if (n == 0) return DFU_OK;
+  if (is_bf16) LAUNCH(k_dropout_fwd<true>, n, stream, x, y, mask, n, p, seed, offset_dev);
+  else LAUNCH(k_dropout_fwd<false>, n, stream, x, y, mask, n, p, seed, offset_dev);
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, offset_dev, n);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float p,
+                               int32_t is_bf16, void* stream) {
+  DFU_CHECK_ARG(dy && mask && dx && p >= 0.f && p < 1.f, "dfu_dropout_bwd: bad args");
+  if (n == 0) return DFU_OK;
+  if (is_bf16) LAUNCH(k_dropout_bwd<true>, n, stream, dy, mask, dx, n, p);
+  else LAUNCH(k_dropout_bwd<false>, n, stream, dy, mask, dx, n, p);
+  return DFU_OK;
+}
+
+extern "C" int dfu_concat2_bf16(const void* a, int32_t a_bf16, int32_t Na, const void* b,
+                                int32_t b_bf16, int32_t Nb, int32_t rows, void* out, void* stream) {
+  DFU_CHECK_ARG(a && b && out && rows > 0, "dfu_concat2_bf16: bad args");
+  LAUNCH(k_concat2, (int64_t)rows * (Na + Nb), stream, a, a_bf16, Na, b, b_bf16, Nb, rows,
+         (bf16_t*)out);
+  return DFU_OK;
+}
+
+extern "C" int dfu_split2_f32(const void* g, int32_t g_bf16, int32_t rows, int32_t Na, int32_t Nb,
+                              float* ga, float* gb, void* stream) {
+  DFU_CHECK_ARG(g && rows > 0, "dfu_split2_f32: bad args");
+  LAUNCH(k_split2, (int64_t)rows * (Na + Nb), stream, g, g_bf16, rows, Na, Nb, ga, gb);
+  return DFU_OK;
+}
+
+extern "C" int dfu_vit_cls_rows(const float* cls, const float* pos, float* x, int32_t B, int32_t T,
+                                int32_t D, void* stream) {
+  DFU_CHECK_ARG(cls && pos && x && B > 0 && T > 0 && D > 0, "dfu_vit_cls_rows: bad args");
+  LAUNCH(k_vit_cls_rows, (int64_t)B * D, stream, cls, pos, x, B, T, D);
+  return DFU_OK;
+}
+
+extern "C" int dfu_vit_embed_bwd(const float* gx, int32_t B, int32_t T, int32_t D, float* dcls,
+                                 float* dpos, float* dbias, void* gpatch, float* partial,
+                                 void* stream) {
+  DFU_CHECK_ARG(gx && gpatch && partial && B > 0 && T > 1 && D > 0, "dfu_vit_embed_bwd: bad args");
+  LAUNCH(k_vit_embed_bwd, (int64_t)T * D, stream, gx, B, T, D, dcls, dpos, (bf16_t*)gpatch, partial);
+  if (dbias) LAUNCH(k_sum_rows_add, (int64_t)D, stream, partial, T, D, dbias);
+  return DFU_OK;
+}
+
+extern "C" int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t* out,
+                               void* stream) {
+  DFU_CHECK_ARG(x && out && rows > 0 && C > 0, "dfu_argmax_rows: bad args");
+  LAUNCH(k_argmax_rows, (int64_t)rows, stream, x, rows, C, out);
+  return DFU_OK;
+}

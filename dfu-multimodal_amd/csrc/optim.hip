@@ -1,0 +1,205 @@
+// Loss and optimizer of the training step:
+//   weighted CrossEntropy (train_multimodal_fusion.py:342-346, 376),
+//   AdamW(lr=1e-4, weight_decay=1e-4, betas (0.9, 0.999), eps 1e-8) (:347, 380),
+// with the step counter kept on the device so a captured graph replays the bias correction.
+#include "common.h"
+
+namespace {
+
+// Single block.  loss = sum_i w[y_i] * (lse_i - z_i[y_i]) / sum_i w[y_i]
+__global__ void k_ce_fwd(const float* __restrict__ z, const int64_t* __restrict__ y,
+                         const float* __restrict__ w, int B, int C, float* __restrict__ loss,
+                         float* __restrict__ dz) {
+  __shared__ float s_num[256], s_den[256];
+  float num = 0.f, den = 0.f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    const int64_t yi = y[i];
+    const float wi = (yi >= 0 && yi < C) ? (w ? w[yi] : 1.f) : 0.f;
+    float mx = -INFINITY;
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, z[(int64_t)i * C + c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += expf(z[(int64_t)i * C + c] - mx);
+    const float lse = mx + logf(se);
+    if (wi != 0.f) num += wi * (lse - z[(int64_t)i * C + yi]);
+    den += wi;
+  }
+  s_num[threadIdx.x] = num;
+  s_den[threadIdx.x] = den;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      s_num[threadIdx.x] += s_num[threadIdx.x + s];
+      s_den[threadIdx.x] += s_den[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  const float D = s_den[0];
+  if (threadIdx.x == 0) loss[0] = s_num[0] / D;
+  if (dz) {
+    for (int i = threadIdx.x; i < B; i += blockDim.x) {
+      const int64_t yi = y[i];
+      const float wi = (yi >= 0 && yi < C) ? (w ? w[yi] : 1.f) : 0.f;
+      float mx = -INFINITY;
+      for (int c = 0; c < C; ++c) mx = fmaxf(mx, z[(int64_t)i * C + c]);
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += expf(z[(int64_t)i * C + c] - mx);
+      for (int c = 0; c < C; ++c) {
+        const float pc = expf(z[(int64_t)i * C + c] - mx) / se;
+        dz[(int64_t)i * C + c] = wi * (pc - (c == yi ? 1.f : 0.f)) / D;
+      }
+    }
+  }
+}
+
+__global__ void k_ce_bwd(const float* __restrict__ saved, const float* __restrict__ g, int n,
+                         float* __restrict__ out) {
+  const float gg = g[0];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    out[i] = saved[i] * gg;
+}
+
+struct AdamCoef {
+  float step_size, bc2_sqrt_inv, decay;
+};
+
+DFU_DEV AdamCoef adam_coef(int64_t step, float lr, float b1, float b2, float wd) {
+  const double t = (double)step;
+  const double bc1 = 1.0 - pow((double)b1, t);
+  const double bc2 = 1.0 - pow((double)b2, t);
+  AdamCoef a;
+  a.step_size = (float)(lr / bc1);
+  a.bc2_sqrt_inv = (float)(1.0 / sqrt(bc2));
+  a.decay = 1.f - lr * wd;
+  return a;
+}
+
+DFU_DEV void adam_update(float& p, float g, float& m, float& v, const AdamCoef& a, float b1,
+                         float b2, float eps) {
+  p *= a.decay;
+  m = m + (1.f - b1) * (g - m);  // lerp_(grad, 1 - beta1)
+  v = v * b2 + (1.f - b2) * g * g;
+  const float denom = sqrtf(v) * a.bc2_sqrt_inv + eps;
+  p -= a.step_size * (m / denom);
+}
+
+__global__ void k_adamw_flat(float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
+                             float b1, float b2, float eps, float wd,
+                             const int64_t* __restrict__ step_dev) {
+  const AdamCoef a = adam_coef(*step_dev, lr, b1, b2, wd);
+  const int64_t n4 = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 pp = ((f32x4*)p)[i], mm = ((f32x4*)m)[i], vv = ((f32x4*)v)[i];
+    const f32x4 gg = ((const f32x4*)g)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pp[e], me = mm[e], ve = vv[e];
+      adam_update(pe, gg[e], me, ve, a, b1, b2, eps);
+      pp[e] = pe; mm[e] = me; vv[e] = ve;
+    }
+    ((f32x4*)p)[i] = pp;
+    ((f32x4*)m)[i] = mm;
+    ((f32x4*)v)[i] = vv;
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float pe = p[i], me = m[i], ve = v[i];
+    adam_update(pe, g[i], me, ve, a, b1, b2, eps);
+    p[i] = pe; m[i] = me; v[i] = ve;
+  }
+}
+
+// Tensor-table form: chunk c covers elements [chunk_offsets[c], chunk_offsets[c+1]) of the
+// virtual concatenation; each block finds its tensor by binary search over tensor starts.
+constexpr int ADAM_CHUNK = 65536;
+__global__ void k_adamw_table(float* const* __restrict__ P, float* const* __restrict__ G,
+                              float* const* __restrict__ M, float* const* __restrict__ V,
+                              const int64_t* __restrict__ numel, int ntensors,
+                              const int64_t* __restrict__ chunk_tensor, int nchunks, float lr,
+                              float b1, float b2, float eps, float wd,
+                              const int64_t* __restrict__ step_dev) {
+  const AdamCoef a = adam_coef(*step_dev, lr, b1, b2, wd);
+  for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    // chunk_tensor[c] packs (tensor index << 32) | chunk index within the tensor
+    const int64_t ct = chunk_tensor[c];
+    const int t = (int)(ct >> 32);
+    const int64_t start = (int64_t)(ct & 0xffffffff) * ADAM_CHUNK;
+    const int64_t end = min(numel[t], start + ADAM_CHUNK);
+    float* p = P[t];
+    float* gp = G[t];
+    float* m = M[t];
+    float* v = V[t];
+    for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+      float pe = p[i], me = m[i], ve = v[i];
+      adam_update(pe, gp ? gp[i] : 0.f, me, ve, a, b1, b2, eps);
+      p[i] = pe; m[i] = me; v[i] = ve;
+    }
+  }
+}
+
+__global__ void k_step_inc(int64_t* s) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *s += 1;
+}
+
+}  // namespace
+
+extern "C" int dfu_ce_weighted_fwd(const float* logits, const int64_t* labels, const float* weight,
+                                   int32_t B, int32_t C, float* loss, float* dlogits,
+                                   void* stream) {
+  DFU_CHECK_ARG(logits && labels && loss && B > 0 && C > 0, "dfu_ce_weighted_fwd: bad args");
+  hipLaunchKernelGGL(k_ce_fwd, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, labels, weight,
+                     B, C, loss, dlogits);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_ce_weighted_bwd(const float* saved, const float* grad_loss, int32_t B,
+                                   int32_t C, float* dlogits, void* stream) {
+  DFU_CHECK_ARG(saved && grad_loss && dlogits, "dfu_ce_weighted_bwd: bad args");
+  const int n = B * C;
+  hipLaunchKernelGGL(k_ce_bwd, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, saved,
+                     grad_loss, n, dlogits);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                              int64_t n, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, const int64_t* step_dev, void* stream) {
+  DFU_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step_dev && n > 0,
+                "dfu_adamw_flat: bad args");
+  DFU_CHECK_ARG(((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 &&
+                    ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0,
+                "dfu_adamw_flat: buffers must be 16-byte aligned");
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_adamw_flat, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param,
+                     grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step_dev);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_adamw(float* const* params, float* const* grads, float* const* exp_avg,
+                         float* const* exp_avg_sq, const int64_t* numels, int32_t ntensors,
+                         const int64_t* chunk_offsets, int32_t nchunks, float lr, float beta1,
+                         float beta2, float eps, float weight_decay, int64_t* step_dev,
+                         void* stream) {
+  DFU_CHECK_ARG(params && exp_avg && exp_avg_sq && numels && chunk_offsets && step_dev &&
+                    ntensors > 0 && nchunks > 0,
+                "dfu_adamw: bad args");
+  const int blocks = nchunks < 8192 ? nchunks : 8192;
+  hipLaunchKernelGGL(k_adamw_table, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params, grads,
+                     exp_avg, exp_avg_sq, numels, ntensors, chunk_offsets, nchunks, lr, beta1,
+                     beta2, eps, weight_decay, step_dev);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_step_increment(int64_t* step_dev, void* stream) {
+  DFU_CHECK_ARG(step_dev, "dfu_step_increment: null counter");
+  hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(64), 0, (hipStream_t)stream, step_dev);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}

@@ -1,0 +1,146 @@
+"""ctypes binding of libdfu_hip.so — the C ABI declared in include/dfu_hip.h.
+
+This is the only place the host touches the native library.  Loading fails loudly: there is
+no CPU or ATen fallback for any op on the hot path (SURVEY.md §7 design stance).
+"""
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdfu_hip.so")
+HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "dfu_hip.h"))
+
+c_int32 = ctypes.c_int32
+c_int64 = ctypes.c_int64
+c_float = ctypes.c_float
+c_uint64 = ctypes.c_uint64
+c_void_p = ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+
+# enum dfu_operand_mode
+OPND_KMAJOR, OPND_MNMAJOR, OPND_CONV_FWD, OPND_CONV_DGRAD, OPND_CONV_DGRAD_W, OPND_CONV_WGRAD_X = range(6)
+# enum dfu_epilogue
+(EPI_BF16, EPI_BF16_RELU, EPI_BF16_GELU, EPI_F32, EPI_F32_RESID, EPI_BF16_DGELU, EPI_BF16_ADD,
+ EPI_F32_ACC, EPI_F32_ACC_CONVW, EPI_BF16_STATS, EPI_PATCH) = range(11)
+
+DFU_E_INVALID = 1001
+DFU_E_UNSUPPORTED = 1002
+
+
+class GemmDesc(ctypes.Structure):
+    """Mirror of `dfu_gemm_desc` (include/dfu_hip.h)."""
+    _fields_ = [
+        ("M", c_int32), ("N", c_int32), ("K", c_int32),
+        ("a_mode", c_int32), ("b_mode", c_int32),
+        ("A", c_void_p), ("lda", c_int64),
+        ("B", c_void_p), ("ldb", c_int64),
+        ("C", c_void_p), ("ldc", c_int64),
+        ("epilogue", c_int32), ("alpha", c_float),
+        ("bias", c_void_p),
+        ("aux", c_void_p), ("ldaux", c_int64),
+        ("aux_out", c_void_p), ("ldaux_out", c_int64),
+        ("stats", c_void_p),
+        ("split_k", c_int32),
+        ("ep_tokens", c_int32),
+        ("conv_n", c_int32), ("conv_h", c_int32), ("conv_w", c_int32), ("conv_c", c_int32),
+        ("conv_k", c_int32), ("conv_r", c_int32), ("conv_s", c_int32),
+        ("conv_stride", c_int32), ("conv_pad", c_int32),
+        ("conv_p", c_int32), ("conv_q", c_int32),
+    ]
+
+
+P = c_void_p
+I32 = c_int32
+I64 = c_int64
+F = c_float
+
+# name -> argtypes (restype is always int32 unless listed in _RESTYPE)
+PROTOTYPES = {
+    "dfu_last_error_string": [],
+    "dfu_version": [],
+    "dfu_zero": [P, I64, P],
+    "dfu_gemm": [ctypes.POINTER(GemmDesc), P],
+    "dfu_gemm_stats_tiles": [I32],
+    "dfu_pack_conv_weight": [P, P, I32, I32, I32, I32, P],
+    "dfu_cast_rows_bf16": [P, I64, P, I64, I32, I32, P],
+    "dfu_cast_rows_f32": [P, I64, P, I64, I32, I32, P],
+    "dfu_im2col_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],
+    "dfu_patchify_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
+    "dfu_bn_finalize": [P, I32, I32, I32, P, P, F, F, P, P, P, P, P, P, P, P],
+    "dfu_bn_eval_coeffs": [P, P, P, P, F, I32, P, P, P],
+    "dfu_bn_apply": [P, P, P, P, I32, P, I64, I32, P],
+    "dfu_bn_bwd_blocks": [I64],
+    "dfu_bn_bwd_reduce": [P, P, P, I32, P, P, I64, I32, P, P],
+    "dfu_bn_bwd_finalize": [P, I32, I64, I32, P, P, P, P, P, P],
+    "dfu_bn_bwd_apply": [P, P, P, I32, P, P, P, I64, I32, P, P, P],
+    "dfu_maxpool_fwd": [P, I32, I32, I32, I32, P, P, I32, I32, P],
+    "dfu_maxpool_bwd": [P, P, I32, I32, I32, I32, I32, I32, P, P],
+    "dfu_avgpool_fwd": [P, I32, I32, I32, P, P],
+    "dfu_avgpool_bwd": [P, I32, I32, I32, P, P],
+    "dfu_layernorm_fwd": [P, I64, I32, I32, P, P, F, P, I64, I32, P, P, P],
+    "dfu_ln_bwd_blocks": [I32],
+    "dfu_layernorm_bwd": [P, I64, I32, P, I64, P, P, P, I32, I32, P, I64, P, P, P],
+    "dfu_reduce_partials": [P, I32, I32, I32, P, P, P],
+    "dfu_attention_fwd": [P, I32, I32, I32, I32, F, P, P, P],
+    "dfu_attention_bwd": [P, P, P, P, I32, I32, I32, I32, F, P, P, P],
+    "dfu_attention_npad": [I32],
+    "dfu_vit_cls_rows": [P, P, P, I32, I32, I32, P],
+    "dfu_vit_embed_bwd": [P, I32, I32, I32, P, P, P, P, P, P],
+    "dfu_colsum": [P, I32, I64, I32, I32, P, P, P],
+    "dfu_colsum_blocks": [I32],
+    "dfu_gather_rows_f32": [P, I64, I32, I32, I32, I32, P, I64, P],
+    "dfu_scatter_rows_f32": [P, I64, I32, I32, I32, I32, P, I64, P],
+    "dfu_relu_fwd": [P, P, I64, I32, P],
+    "dfu_relu_bwd": [P, P, P, I64, I32, P],
+    "dfu_dropout_fwd": [P, P, P, I64, F, c_uint64, P, I32, P],
+    "dfu_dropout_bwd": [P, P, P, I64, F, I32, P],
+    "dfu_concat2_bf16": [P, I32, I32, P, I32, I32, I32, P, P],
+    "dfu_split2_f32": [P, I32, I32, I32, I32, P, P, P],
+    "dfu_ce_weighted_fwd": [P, P, P, I32, I32, P, P, P],
+    "dfu_ce_weighted_bwd": [P, P, I32, I32, P, P],
+    "dfu_adamw": [P, P, P, P, P, I32, P, I32, F, F, F, F, F, P, P],
+    "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P],
+    "dfu_step_increment": [P, P],
+    "dfu_argmax_rows": [P, I32, I32, P, P],
+}
+_RESTYPE = {"dfu_last_error_string": c_char_p}
+
+
+def header_symbols(path=HEADER_PATH):
+    """Every function name declared in include/dfu_hip.h (used by the symbol-export test)."""
+    with open(path) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dfu_\w+)\s*\(", text, re.M)))
+
+
+class DfuError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libdfu_hip.so once; raise if it is missing (never fall back)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DfuError(
+            f"libdfu_hip.so not found at {LIB_PATH}; build it with "
+            f"`make -C dfu-multimodal_amd` (or __graft_entry__.build()). There is no fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in PROTOTYPES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPE.get(name, c_int32)
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().dfu_last_error_string()
+        msg = msg.decode() if msg else ""
+        raise DfuError(f"{what or 'dfu call'} failed (rc={rc}): {msg}")

@@ -1,0 +1,362 @@
+"""Thin, shape-checked wrappers over the libdfu_hip C ABI (include/dfu_hip.h).
+
+Each function takes torch tensors that already live on the GPU, passes raw pointers and the
+current HIP stream, and raises DfuError on any non-zero return code.  Nothing here allocates
+except where an output is documented as returned; nothing synchronises.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+from ._lib import check
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def lib():
+    return L.load()
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _req(t, dtype, name):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: tensor must be on the GPU")
+
+
+# ----------------------------------------------------------------------------------- GEMM
+class ConvGeom:
+    """Implicit-GEMM convolution geometry (NHWC input N,H,W,C; K filters of R x S)."""
+
+    __slots__ = ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "p", "q")
+
+    def __init__(self, n, h, w, c, k, r, s, stride, pad):
+        self.n, self.h, self.w, self.c, self.k = n, h, w, c, k
+        self.r, self.s, self.stride, self.pad = r, s, stride, pad
+        self.p = (h + 2 * pad - r) // stride + 1
+        self.q = (w + 2 * pad - s) // stride + 1
+
+
+def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
+         epilogue=L.EPI_BF16, alpha=1.0, bias=None, aux=None, ldaux=0, aux_out=None,
+         ldaux_out=0, stats=None, split_k=1, ep_tokens=0, conv=None):
+    d = L.GemmDesc()
+    d.M, d.N, d.K = int(M), int(N), int(K)
+    d.a_mode, d.b_mode = int(a_mode), int(b_mode)
+    d.A, d.lda = A.data_ptr(), int(lda)
+    d.B, d.ldb = B.data_ptr(), int(ldb)
+    d.C, d.ldc = C.data_ptr(), int(ldc)
+    d.epilogue, d.alpha = int(epilogue), float(alpha)
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.aux = aux.data_ptr() if aux is not None else None
+    d.ldaux = int(ldaux)
+    d.aux_out = aux_out.data_ptr() if aux_out is not None else None
+    d.ldaux_out = int(ldaux_out)
+    d.stats = stats.data_ptr() if stats is not None else None
+    d.split_k = int(split_k)
+    d.ep_tokens = int(ep_tokens)
+    if conv is not None:
+        d.conv_n, d.conv_h, d.conv_w, d.conv_c = conv.n, conv.h, conv.w, conv.c
+        d.conv_k, d.conv_r, d.conv_s = conv.k, conv.r, conv.s
+        d.conv_stride, d.conv_pad, d.conv_p, d.conv_q = conv.stride, conv.pad, conv.p, conv.q
+    check(lib().dfu_gemm(ctypes.byref(d), stream_ptr()), "dfu_gemm")
+
+
+def stats_tiles(M):
+    return lib().dfu_gemm_stats_tiles(int(M))
+
+
+def choose_split(M, N, K, target_blocks=512, min_k_per_split=256):
+    """split-K for weight-gradient GEMMs whose output tile grid underfills 256 CUs."""
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    ktiles = (K + 63) // 64
+    if tiles >= target_blocks:
+        return 1
+    split = max(1, target_blocks // tiles)
+    split = min(split, max(1, ktiles // (min_k_per_split // 64)))
+    return int(split)
+
+
+# ------------------------------------------------------------------------------- layouts
+def pack_conv_weight(w, out=None):
+    """fp32 OIHW -> bf16 KRSC."""
+    _req(w, F32, "pack_conv_weight")
+    K, C, R, S = w.shape
+    if out is None:
+        out = torch.empty((K, R, S, C), dtype=BF16, device=w.device)
+    check(lib().dfu_pack_conv_weight(ptr(w.contiguous()), ptr(out), K, C, R, S, stream_ptr()),
+          "dfu_pack_conv_weight")
+    return out
+
+
+def cast_rows_bf16(x, ld_out=None, out=None):
+    """fp32 [rows, cols] -> bf16 [rows, ld_out] (zero-padded columns)."""
+    _req(x, F32, "cast_rows_bf16")
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(1) != 1:
+        x2 = x2.contiguous()
+    rows, cols = x2.shape
+    ld_out = cols if ld_out is None else ld_out
+    if out is None:
+        out = torch.empty((rows, ld_out), dtype=BF16, device=x.device)
+    check(lib().dfu_cast_rows_bf16(ptr(x2), x2.stride(0), ptr(out), ld_out, rows, cols,
+                                   stream_ptr()), "dfu_cast_rows_bf16")
+    return out
+
+
+def cast_rows_f32(x, out=None):
+    _req(x, BF16, "cast_rows_f32")
+    x2 = x.reshape(-1, x.shape[-1])
+    rows, cols = x2.shape
+    if out is None:
+        out = torch.empty((rows, cols), dtype=F32, device=x.device)
+    check(lib().dfu_cast_rows_f32(ptr(x2), x2.stride(0), ptr(out), out.stride(0), rows, cols,
+                                  stream_ptr()), "dfu_cast_rows_f32")
+    return out
+
+
+def im2col_f32(x, R, S, stride, pad, Kp):
+    _req(x, F32, "im2col_f32")
+    B, C, H, W = x.shape
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - S) // stride + 1
+    out = torch.empty((B * P * Q, Kp), dtype=BF16, device=x.device)
+    sn, sc, sh, sw = x.stride()
+    check(lib().dfu_im2col_f32(ptr(x), sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q,
+                               ptr(out), Kp, stream_ptr()), "dfu_im2col_f32")
+    return out, P, Q
+
+
+def patchify_f32(x, ps):
+    _req(x, F32, "patchify_f32")
+    B, C, H, W = x.shape
+    out = torch.empty((B * (H // ps) * (W // ps), C * ps * ps), dtype=BF16, device=x.device)
+    sn, sc, sh, sw = x.stride()
+    check(lib().dfu_patchify_f32(ptr(x), sn, sc, sh, sw, B, C, H, W, ps, ptr(out),
+                                 stream_ptr()), "dfu_patchify_f32")
+    return out
+
+
+# ----------------------------------------------------------------------------- BatchNorm
+def bn_finalize(stats, M, C, gamma, beta, eps, momentum, running_mean, running_var, nbt,
+                mean_out, invstd_out, scale_out, shift_out):
+    tiles = stats_tiles(M)
+    check(lib().dfu_bn_finalize(ptr(stats), tiles, M, C, ptr(gamma), ptr(beta), eps, momentum,
+                                ptr(running_mean), ptr(running_var), ptr(nbt), ptr(mean_out),
+                                ptr(invstd_out), ptr(scale_out), ptr(shift_out), stream_ptr()),
+          "dfu_bn_finalize")
+
+
+def bn_eval_coeffs(gamma, beta, rm, rv, eps, scale_out, shift_out):
+    check(lib().dfu_bn_eval_coeffs(ptr(gamma), ptr(beta), ptr(rm), ptr(rv), eps, rm.numel(),
+                                   ptr(scale_out), ptr(shift_out), stream_ptr()),
+          "dfu_bn_eval_coeffs")
+
+
+def bn_apply(y, scale, shift, residual, relu, out, M, C):
+    check(lib().dfu_bn_apply(ptr(y), ptr(scale), ptr(shift), ptr(residual), int(relu), ptr(out),
+                             M, C, stream_ptr()), "dfu_bn_apply")
+
+
+def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta):
+    """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply."""
+    blocks = lib().dfu_bn_bwd_blocks(M)
+    partial = torch.empty((blocks, 2, C), dtype=F32, device=y.device)
+    coef = torch.empty((C, 3), dtype=F32, device=y.device)
+    s = stream_ptr()
+    check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), int(relu), ptr(mean), ptr(invstd),
+                                  M, C, ptr(partial), s), "dfu_bn_bwd_reduce")
+    check(lib().dfu_bn_bwd_finalize(ptr(partial), blocks, M, C, ptr(gamma), ptr(invstd),
+                                    ptr(dgamma), ptr(dbeta), ptr(coef), s), "dfu_bn_bwd_finalize")
+    check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), int(relu), ptr(mean), ptr(invstd),
+                                 ptr(coef), M, C, ptr(dy), ptr(dres), s), "dfu_bn_bwd_apply")
+
+
+# ------------------------------------------------------------------------------- pooling
+def maxpool_fwd(x, B, H, W, C):
+    P = (H - 1) // 2 + 1
+    Q = (W - 1) // 2 + 1
+    y = torch.empty((B, P, Q, C), dtype=BF16, device=x.device)
+    am = torch.empty((B, P, Q, C), dtype=torch.uint8, device=x.device)
+    check(lib().dfu_maxpool_fwd(ptr(x), B, H, W, C, ptr(y), ptr(am), P, Q, stream_ptr()),
+          "dfu_maxpool_fwd")
+    return y, am, P, Q
+
+
+def maxpool_bwd(dy, am, B, H, W, C, P, Q):
+    dx = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
+    check(lib().dfu_maxpool_bwd(ptr(dy), ptr(am), B, H, W, C, P, Q, ptr(dx), stream_ptr()),
+          "dfu_maxpool_bwd")
+    return dx
+
+
+def avgpool_fwd(x, B, HW, C):
+    y = torch.empty((B, C), dtype=F32, device=x.device)
+    check(lib().dfu_avgpool_fwd(ptr(x), B, HW, C, ptr(y), stream_ptr()), "dfu_avgpool_fwd")
+    return y
+
+
+def avgpool_bwd(dy, B, HW, C):
+    dx = torch.empty((B, HW, C), dtype=BF16, device=dy.device)
+    check(lib().dfu_avgpool_bwd(ptr(dy), B, HW, C, ptr(dx), stream_ptr()), "dfu_avgpool_bwd")
+    return dx
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+def layernorm_fwd(x, ldx, rows, D, gamma, beta, eps, out, ldo, out_bf16, mean, rstd):
+    check(lib().dfu_layernorm_fwd(ptr(x), ldx, rows, D, ptr(gamma), ptr(beta), eps, ptr(out),
+                                  ldo, int(out_bf16), ptr(mean), ptr(rstd), stream_ptr()),
+          "dfu_layernorm_fwd")
+
+
+def layernorm_bwd(dy, lddy, dy_bf16, x, ldx, mean, rstd, gamma, rows, D, gx, ldg, gx_bf16,
+                  dgamma, dbeta):
+    blocks = lib().dfu_ln_bwd_blocks(rows)
+    partial = torch.empty((blocks, 2, D), dtype=F32, device=x.device)
+    s = stream_ptr()
+    check(lib().dfu_layernorm_bwd(ptr(dy), lddy, int(dy_bf16), ptr(x), ldx, ptr(mean), ptr(rstd),
+                                  ptr(gamma), rows, D, ptr(gx), ldg, ptr(gx_bf16), ptr(partial),
+                                  s), "dfu_layernorm_bwd")
+    if dgamma is not None or dbeta is not None:
+        check(lib().dfu_reduce_partials(ptr(partial), blocks, 2, D, ptr(dgamma), ptr(dbeta), s),
+              "dfu_reduce_partials")
+
+
+# ----------------------------------------------------------------------------- attention
+def attention_npad(N):
+    return lib().dfu_attention_npad(int(N))
+
+
+def attention_fwd(qkv, B, N, H, dh, scale):
+    o = torch.empty((B * N, H * dh), dtype=BF16, device=qkv.device)
+    lse = torch.empty((B * H, attention_npad(N)), dtype=F32, device=qkv.device)
+    check(lib().dfu_attention_fwd(ptr(qkv), B, N, H, dh, scale, ptr(o), ptr(lse), stream_ptr()),
+          "dfu_attention_fwd")
+    return o, lse
+
+
+def attention_bwd(qkv, o, dout, lse, B, N, H, dh, scale, dqkv=None):
+    delta = torch.empty((B * H, attention_npad(N)), dtype=F32, device=qkv.device)
+    if dqkv is None:
+        dqkv = torch.empty_like(qkv)
+    check(lib().dfu_attention_bwd(ptr(qkv), ptr(o), ptr(dout), ptr(lse), B, N, H, dh, scale,
+                                  ptr(delta), ptr(dqkv), stream_ptr()), "dfu_attention_bwd")
+    return dqkv
+
+
+# ----------------------------------------------------------------------------- misc
+def colsum_add(x, out, is_bf16=None):
+    """out[n] += sum over rows of x[rows, N]."""
+    x2 = x.reshape(-1, x.shape[-1])
+    rows, N = x2.shape
+    bf = (x.dtype == BF16) if is_bf16 is None else is_bf16
+    blocks = lib().dfu_colsum_blocks(rows)
+    partial = torch.empty((blocks, N), dtype=F32, device=x.device)
+    check(lib().dfu_colsum(ptr(x2), int(bf), x2.stride(0), rows, N, ptr(out), ptr(partial),
+                           stream_ptr()), "dfu_colsum")
+
+
+def zero_(t):
+    check(lib().dfu_zero(ptr(t), t.numel() * t.element_size(), stream_ptr()), "dfu_zero")
+    return t
+
+
+def relu_fwd(x):
+    y = torch.empty_like(x)
+    check(lib().dfu_relu_fwd(ptr(x), ptr(y), x.numel(), int(x.dtype == BF16), stream_ptr()),
+          "dfu_relu_fwd")
+    return y
+
+
+def relu_bwd(dy, y):
+    dx = torch.empty_like(y)
+    check(lib().dfu_relu_bwd(ptr(dy), ptr(y), ptr(dx), y.numel(), int(y.dtype == BF16),
+                             stream_ptr()), "dfu_relu_bwd")
+    return dx
+
+
+def dropout_fwd(x, p, seed, offset_dev):
+    y = torch.empty_like(x)
+    mask = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    check(lib().dfu_dropout_fwd(ptr(x), ptr(y), ptr(mask), x.numel(), float(p),
+                                ctypes.c_uint64(int(seed)), ptr(offset_dev), int(x.dtype == BF16),
+                                stream_ptr()), "dfu_dropout_fwd")
+    return y, mask
+
+
+def dropout_bwd(dy, mask, p):
+    dx = torch.empty_like(dy)
+    check(lib().dfu_dropout_bwd(ptr(dy), ptr(mask), ptr(dx), dy.numel(), float(p),
+                                int(dy.dtype == BF16), stream_ptr()), "dfu_dropout_bwd")
+    return dx
+
+
+def concat2_bf16(a, b):
+    rows = a.shape[0]
+    out = torch.empty((rows, a.shape[1] + b.shape[1]), dtype=BF16, device=a.device)
+    check(lib().dfu_concat2_bf16(ptr(a.contiguous()), int(a.dtype == BF16), a.shape[1],
+                                 ptr(b.contiguous()), int(b.dtype == BF16), b.shape[1], rows,
+                                 ptr(out), stream_ptr()), "dfu_concat2_bf16")
+    return out
+
+
+def split2_f32(g, Na, Nb):
+    rows = g.shape[0]
+    ga = torch.empty((rows, Na), dtype=F32, device=g.device)
+    gb = torch.empty((rows, Nb), dtype=F32, device=g.device)
+    check(lib().dfu_split2_f32(ptr(g.contiguous()), int(g.dtype == BF16), rows, Na, Nb, ptr(ga),
+                               ptr(gb), stream_ptr()), "dfu_split2_f32")
+    return ga, gb
+
+
+def vit_cls_rows(cls, pos, x, B, T, D):
+    check(lib().dfu_vit_cls_rows(ptr(cls), ptr(pos), ptr(x), B, T, D, stream_ptr()),
+          "dfu_vit_cls_rows")
+
+
+def vit_embed_bwd(gx, B, T, D, dcls, dpos, dbias):
+    gpatch = torch.empty((B * (T - 1), D), dtype=BF16, device=gx.device)
+    partial = torch.empty((T, D), dtype=F32, device=gx.device)
+    check(lib().dfu_vit_embed_bwd(ptr(gx), B, T, D, ptr(dcls), ptr(dpos), ptr(dbias),
+                                  ptr(gpatch), ptr(partial), stream_ptr()), "dfu_vit_embed_bwd")
+    return gpatch
+
+
+def ce_weighted_fwd(logits, labels, weight, loss, dlogits):
+    B, C = logits.shape
+    check(lib().dfu_ce_weighted_fwd(ptr(logits), ptr(labels), ptr(weight), B, C, ptr(loss),
+                                    ptr(dlogits), stream_ptr()), "dfu_ce_weighted_fwd")
+
+
+def ce_weighted_bwd(saved, grad_loss):
+    B, C = saved.shape
+    out = torch.empty_like(saved)
+    check(lib().dfu_ce_weighted_bwd(ptr(saved), ptr(grad_loss), B, C, ptr(out), stream_ptr()),
+          "dfu_ce_weighted_bwd")
+    return out
+
+
+def adamw_flat(p, g, m, v, lr, b1, b2, eps, wd, step_dev):
+    check(lib().dfu_adamw_flat(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd,
+                               ptr(step_dev), stream_ptr()), "dfu_adamw_flat")
+
+
+def step_increment(step_dev):
+    check(lib().dfu_step_increment(ptr(step_dev), stream_ptr()), "dfu_step_increment")
+
+
+def argmax_rows(x):
+    out = torch.empty((x.shape[0],), dtype=torch.int64, device=x.device)
+    check(lib().dfu_argmax_rows(ptr(x), x.shape[0], x.shape[1], ptr(out), stream_ptr()),
+          "dfu_argmax_rows")
+    return out

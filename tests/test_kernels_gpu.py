@@ -1,0 +1,340 @@
+"""Per-kernel numerics on the GPU: every libdfu_hip entry point against a plain PyTorch fp32
+reference of the same op on the same (bf16-representable) inputs."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dfu_hip import _lib as L
+from dfu_hip import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rnd(*shape, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype).to(DEV)
+
+
+def close(a, b, atol, rtol=0.0, what=""):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol)
+    assert not bad.any(), f"{what}: max err {err.max().item():.3e} (n_bad={bad.sum().item()})"
+
+
+# ------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K", [(300, 200, 136), (128, 128, 64), (1000, 2304, 768), (64, 2, 512),
+                                   (12608, 768, 768)])
+def test_gemm_nt_f32(M, N, K):
+    A = rnd(M, K, seed=1)
+    B = rnd(N, K, seed=2)
+    C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_F32)
+    ref = A.float() @ B.float().t()
+    close(C, ref, atol=2e-3 * math.sqrt(K), what="nt_f32")
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 136), (777, 768, 3072)])
+def test_gemm_nn_f32(M, N, K):
+    A = rnd(M, K, seed=3)
+    Bkn = rnd(K, N, seed=4)
+    C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops.gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32)
+    close(C, A.float() @ Bkn.float(), atol=2e-3 * math.sqrt(K), what="nn_f32")
+
+
+@pytest.mark.parametrize("M,N,K,split", [(200, 136, 300, 1), (768, 2304, 12608, 4), (64, 147, 5000, 7)])
+def test_gemm_tn_acc(M, N, K, split):
+    Akm = rnd(K, M, seed=5)
+    Bkn = rnd(K, (N + 7) // 8 * 8, seed=6)
+    C = rnd(M, N, dtype=torch.float32, seed=7)
+    ref = C + Akm.float().t() @ Bkn.float()[:, :N]
+    ops.gemm(M, N, K, Akm, M, Bkn, Bkn.shape[1], C, N, a_mode=L.OPND_MNMAJOR,
+             b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC, split_k=split)
+    close(C, ref, atol=3e-3 * math.sqrt(K), what="tn_acc")
+
+
+def test_gemm_epilogues():
+    M, N, K = 333, 256, 192
+    A = rnd(M, K, seed=8)
+    B = rnd(N, K, seed=9)
+    bias = rnd(N, dtype=torch.float32, seed=10)
+    acc = A.float() @ B.float().t()
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16, bias=bias, alpha=0.5)
+    close(C, acc * 0.5 + bias, atol=3e-2, rtol=1e-2, what="bf16 bias alpha")
+    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_RELU, bias=bias)
+    close(C, torch.relu(acc + bias), atol=3e-2, rtol=1e-2, what="relu")
+    pre = torch.empty_like(C)
+    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_GELU, bias=bias, aux_out=pre, ldaux_out=N)
+    close(pre, acc + bias, atol=3e-2, rtol=1e-2, what="gelu pre")
+    close(C, F.gelu(acc + bias), atol=3e-2, rtol=1e-2, what="gelu")
+    res = rnd(M, N, dtype=torch.float32, seed=11)
+    Cf = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops.gemm(M, N, K, A, K, B, K, Cf, N, epilogue=L.EPI_F32_RESID, bias=bias, aux=res, ldaux=N)
+    close(Cf, res + acc + bias, atol=2e-3 * math.sqrt(K), what="resid")
+    # dgrad-style epilogues (B as [K][N])
+    Bkn = rnd(K, N, seed=12)
+    acc2 = A.float() @ Bkn.float()
+    h = rnd(M, N, seed=13)
+    ops.gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N)
+    x = h.float()
+    dg = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+    close(C, acc2 * dg, atol=5e-2, rtol=1e-2, what="dgelu")
+    ops.gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16_ADD, aux=h, ldaux=N)
+    close(C, acc2 + h.float(), atol=5e-2, rtol=1e-2, what="add")
+
+
+def test_gemm_stats():
+    M, N, K = 1000, 192, 128
+    A = rnd(M, K, seed=14)
+    B = rnd(N, K, seed=15)
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    tiles = ops.stats_tiles(M)
+    stats = torch.empty(tiles, 2, N, dtype=torch.float32, device=DEV)
+    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_STATS, stats=stats)
+    ref = A.float() @ B.float().t()
+    close(C, ref, atol=5e-2, rtol=1e-2, what="stats store")
+    Cf = C.float()
+    for t in range(tiles):
+        blk = Cf[t * 128:(t + 1) * 128]
+        close(stats[t, 0], blk.sum(0), atol=1e-2, rtol=1e-4, what="tile sum")
+        close(stats[t, 1], ((blk - blk.mean(0)) ** 2).sum(0), atol=1e-2, rtol=1e-3, what="tile M2")
+
+
+def test_gemm_patch():
+    Bsz, T, D = 3, 196, 768
+    M, K = Bsz * T, 768
+    A = rnd(M, K, seed=16)
+    W = rnd(D, K, seed=17, scale=0.05)
+    bias = rnd(D, dtype=torch.float32, seed=18)
+    pos = rnd(T + 1, D, dtype=torch.float32, seed=19)
+    X = torch.zeros(Bsz, T + 1, D, dtype=torch.float32, device=DEV)
+    ops.gemm(M, D, K, A, K, W, K, X, D, epilogue=L.EPI_PATCH, bias=bias, aux=pos, ldaux=D, ep_tokens=T)
+    ref = (A.float() @ W.float().t() + bias).view(Bsz, T, D) + pos[1:]
+    close(X[:, 1:], ref, atol=1e-2, what="patch")
+    assert X[:, 0].abs().max().item() == 0.0
+
+
+# ------------------------------------------------------------------------------ implicit conv
+CONV_CASES = [
+    # N, H, W, C, K, R, S, stride, pad
+    (2, 14, 14, 64, 128, 3, 3, 1, 1),
+    (2, 15, 15, 64, 64, 3, 3, 2, 1),
+    (3, 14, 14, 128, 256, 1, 1, 2, 0),
+    (2, 7, 7, 512, 512, 3, 3, 1, 1),
+]
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    N, H, W, C, K, R, S, st, pad = case
+    g = ops.ConvGeom(N, H, W, C, K, R, S, st, pad)
+    x = rnd(N, C, H, W, seed=20)
+    w = rnd(K, C, R, S, seed=21, scale=0.1)
+    xf = x.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    y_ref = F.conv2d(xf, wf, stride=st, padding=pad)
+    dy = rnd(*y_ref.shape, seed=22)
+    y_ref.backward(dy.float())
+    x_nhwc = _nhwc(x)
+    w_krsc = ops.pack_conv_weight(w.float())
+    M = N * g.p * g.q
+    Y = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+    stats = torch.empty(ops.stats_tiles(M), 2, K, dtype=torch.float32, device=DEV)
+    if R == 1 and S == 1 and st == 1:
+        ops.gemm(M, K, C, x_nhwc, C, w_krsc, C, Y, K, epilogue=L.EPI_BF16_STATS, stats=stats)
+    else:
+        ops.gemm(M, K, R * S * C, x_nhwc, 0, w_krsc, R * S * C, Y, K, a_mode=L.OPND_CONV_FWD,
+                 epilogue=L.EPI_BF16_STATS, stats=stats, conv=g)
+    close(Y.view(N, g.p, g.q, K), _nhwc(y_ref.detach()), atol=5e-2, rtol=1e-2, what="conv fwd")
+    # dgrad
+    dy_nhwc = _nhwc(dy)
+    dX = torch.empty(N * H * W, C, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(N * H * W, C, R * S * K, dy_nhwc, 0, w_krsc, R * S * C, dX, C,
+             a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=L.EPI_BF16, conv=g)
+    close(dX.view(N, H, W, C), _nhwc(xf.grad), atol=5e-2, rtol=1e-2, what="conv dgrad")
+    # wgrad (OIHW fp32 accumulate)
+    dW = torch.zeros(K, C, R, S, dtype=torch.float32, device=DEV)
+    split = ops.choose_split(K, R * S * C, M)
+    ops.gemm(K, R * S * C, M, dy_nhwc, K, x_nhwc, 0, dW, C * R * S, a_mode=L.OPND_MNMAJOR,
+             b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC_CONVW, split_k=split, conv=g)
+    close(dW, wf.grad, atol=2e-2 * math.sqrt(M / 100), rtol=1e-2, what="conv wgrad")
+
+
+# ------------------------------------------------------------------------------ attention
+@pytest.mark.parametrize("B,N,H", [(2, 197, 12), (1, 40, 2), (3, 256, 1)])
+def test_attention(B, N, H):
+    dh = 64
+    qkv = rnd(B * N, 3 * H * dh, seed=30)
+    scale = dh ** -0.5
+    o, lse = ops.attention_fwd(qkv, B, N, H, dh, scale)
+    q, k, v = qkv.float().view(B, N, 3, H, dh).permute(2, 0, 3, 1, 4).unbind(0)
+    q.requires_grad_(True); k.requires_grad_(True); v.requires_grad_(True)
+    ref = F.scaled_dot_product_attention(q, k, v)
+    ref_o = ref.permute(0, 2, 1, 3).reshape(B * N, H * dh)
+    close(o, ref_o, atol=2e-2, what="attn fwd")
+    s = (q @ k.transpose(-1, -2)) * scale
+    close(lse.view(B, H, -1)[:, :, :N], torch.logsumexp(s, -1), atol=1e-3, what="lse")
+    do = rnd(B * N, H * dh, seed=31)
+    ref_o.backward(do.float())
+    dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, H, dh, scale)
+    dq, dk, dv = dqkv.float().view(B, N, 3, H, dh).permute(2, 0, 3, 1, 4).unbind(0)
+    close(dq, q.grad, atol=3e-2, what="dq")
+    close(dk, k.grad, atol=3e-2, what="dk")
+    close(dv, v.grad, atol=3e-2, what="dv")
+
+
+# ------------------------------------------------------------------------------ norms
+def test_batchnorm_train_fwd_bwd():
+    M, C = 5000, 128
+    y = rnd(M, C, seed=40, scale=2.0) + 0.5
+    A = torch.eye(C, dtype=torch.bfloat16, device=DEV)
+    # produce stats through the GEMM epilogue: y @ I
+    Y = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    stats = torch.empty(ops.stats_tiles(M), 2, C, dtype=torch.float32, device=DEV)
+    ops.gemm(M, C, C, y, C, A, C, Y, C, epilogue=L.EPI_BF16_STATS, stats=stats)
+    gamma = rnd(C, dtype=torch.float32, seed=41) * 0.5 + 1
+    beta = rnd(C, dtype=torch.float32, seed=42)
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+    mean, invstd, scale, shift = (torch.empty(C, device=DEV) for _ in range(4))
+    ops.bn_finalize(stats, M, C, gamma, beta, 1e-5, 0.1, rm, rv, nbt, mean, invstd, scale, shift)
+    res = rnd(M, C, seed=43)
+    out = torch.empty_like(Y)
+    ops.bn_apply(Y, scale, shift, res, True, out, M, C)
+    yf = Y.float().requires_grad_(True)
+    gf = gamma.clone().requires_grad_(True)
+    bf = beta.clone().requires_grad_(True)
+    rm2 = torch.zeros(C, device=DEV)
+    rv2 = torch.ones(C, device=DEV)
+    ref = torch.relu(F.batch_norm(yf, rm2, rv2, gf, bf, training=True, momentum=0.1, eps=1e-5) + res.float())
+    close(out, ref, atol=3e-2, rtol=1e-2, what="bn fwd")
+    close(rm, rm2, atol=1e-4, what="running mean")
+    close(rv, rv2, atol=1e-3, rtol=1e-3, what="running var")
+    assert nbt.item() == 1
+    dout = rnd(M, C, seed=44)
+    ref.backward(dout.float())
+    dy = torch.empty_like(Y)
+    dres = torch.empty_like(Y)
+    dgamma = torch.zeros(C, device=DEV)
+    dbeta = torch.zeros(C, device=DEV)
+    ops.bn_bwd(dout, Y, out, True, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta)
+    close(dy, yf.grad, atol=2e-2, rtol=2e-2, what="bn dx")
+    close(dgamma, gf.grad, atol=0.5, rtol=1e-2, what="dgamma")
+    close(dbeta, bf.grad, atol=0.5, rtol=1e-2, what="dbeta")
+
+
+def test_layernorm_fwd_bwd():
+    rows, D = 1000, 768
+    x = (torch.randn(rows, D, device=DEV) * 3 + 1).float()
+    gamma = torch.randn(D, device=DEV)
+    beta = torch.randn(D, device=DEV)
+    out = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(x, D, rows, D, gamma, beta, 1e-6, out, D, True, mean, rstd)
+    xr = x.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (D,), gr, br, 1e-6)
+    close(out, ref, atol=3e-2, rtol=1e-2, what="ln fwd")
+    dy = rnd(rows, D, seed=50)
+    ref.backward(dy.float())
+    gx = torch.randn(rows, D, device=DEV)
+    gx0 = gx.clone()
+    gxb = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
+    dgam = torch.zeros(D, device=DEV)
+    dbet = torch.zeros(D, device=DEV)
+    ops.layernorm_bwd(dy, D, True, x, D, mean, rstd, gamma, rows, D, gx, D, gxb, dgam, dbet)
+    close(gx, gx0 + xr.grad, atol=1e-3, rtol=1e-3, what="ln dx")
+    close(gxb, gx, atol=2e-2, rtol=1e-2, what="ln dx bf16")
+    close(dgam, gr.grad, atol=1e-2, rtol=1e-3, what="ln dgamma")
+    close(dbet, br.grad, atol=1e-2, rtol=1e-3, what="ln dbeta")
+
+
+# ------------------------------------------------------------------------------ misc
+def test_pooling_and_layout():
+    B, C, H, W = 2, 64, 112, 112
+    x = rnd(B, C, H, W, seed=60)
+    xn = _nhwc(x)
+    y, am, P, Q = ops.maxpool_fwd(xn, B, H, W, C)
+    xr = x.float().requires_grad_(True)
+    ref = F.max_pool2d(xr, 3, 2, 1)
+    close(y, _nhwc(ref.detach()), atol=0, what="maxpool fwd")
+    dy = rnd(B, C, P, Q, seed=61)
+    ref.backward(dy.float())
+    dx = ops.maxpool_bwd(_nhwc(dy), am, B, H, W, C, P, Q)
+    close(dx, _nhwc(xr.grad), atol=2e-2, rtol=1e-2, what="maxpool bwd")
+    # avgpool
+    x4 = rnd(B, 7, 7, 2048, seed=62)
+    yf = ops.avgpool_fwd(x4, B, 49, 2048)
+    close(yf, x4.float().mean((1, 2)), atol=1e-4, what="avgpool")
+    g = torch.randn(B, 2048, device=DEV)
+    dx4 = ops.avgpool_bwd(g, B, 49, 2048)
+    close(dx4, (g / 49)[:, None, :].expand(B, 49, 2048), atol=1e-3, rtol=1e-2, what="avgpool bwd")
+    # stem im2col and patchify vs unfold
+    xi = torch.randn(2, 3, 224, 224, device=DEV)
+    col, P, Q = ops.im2col_f32(xi, 7, 7, 2, 3, 160)
+    ref = F.unfold(xi, 7, padding=3, stride=2).transpose(1, 2).reshape(-1, 147)
+    close(col[:, :147], ref, atol=2e-2, rtol=1e-2, what="im2col")
+    assert col[:, 147:].abs().max().item() == 0
+    pt = ops.patchify_f32(xi, 16)
+    ref = F.unfold(xi, 16, stride=16).transpose(1, 2).reshape(-1, 768)
+    close(pt, ref, atol=2e-2, rtol=1e-2, what="patchify")
+    # weight packing
+    w = torch.randn(64, 32, 3, 3, device=DEV)
+    close(ops.pack_conv_weight(w), w.permute(0, 2, 3, 1), atol=2e-2, rtol=1e-2, what="pack")
+
+
+def test_colsum_ce_adamw_dropout():
+    x = rnd(12608, 768, seed=70)
+    out = torch.ones(768, device=DEV)
+    ops.colsum_add(x, out)
+    close(out, 1 + x.float().sum(0), atol=1e-2, rtol=1e-4, what="colsum")
+    logits = torch.randn(64, 2, device=DEV)
+    labels = torch.randint(0, 2, (64,), device=DEV)
+    w = torch.tensor([2.0, 3.0], device=DEV)
+    loss = torch.empty(1, device=DEV)
+    dl = torch.empty_like(logits)
+    ops.ce_weighted_fwd(logits, labels, w, loss, dl)
+    lr = logits.clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels, weight=w)
+    ref.backward()
+    close(loss, ref.detach().view(1), atol=1e-5, what="ce")
+    close(dl, lr.grad, atol=1e-6, what="ce grad")
+    # AdamW vs torch.optim.AdamW over 3 steps
+    n = 10007
+    p = torch.randn(n, device=DEV)
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pr], lr=1e-3, weight_decay=1e-2)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    step = torch.zeros((), dtype=torch.int64, device=DEV)
+    for i in range(3):
+        g = torch.randn(n, device=DEV)
+        pr.grad = g.clone()
+        opt.step()
+        ops.step_increment(step)
+        ops.adamw_flat(p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 1e-2, step)
+    close(p, pr.detach(), atol=1e-6, rtol=1e-5, what="adamw")
+    # dropout statistics and backward consistency
+    xd = torch.ones(1 << 20, device=DEV)
+    off = torch.zeros((), dtype=torch.int64, device=DEV)
+    yd, mask = ops.dropout_fwd(xd, 0.7, 1234, off)
+    keep = mask.float().mean().item()
+    assert abs(keep - 0.3) < 0.01
+    close(yd, mask.float() / 0.3, atol=1e-5, what="dropout scale")
+    assert off.item() == xd.numel()
+    dx = ops.dropout_bwd(torch.ones_like(xd), mask, 0.7)
+    close(dx, yd, atol=1e-6, what="dropout bwd")
