@@ -1,0 +1,259 @@
+#!/usr/bin/env python3
+"""Benchmark: images/sec of the multimodal DFU fusion training step (ResNet50 RGB + ViT-B/16
+thermal -> 2816->512->2 head; weighted CE; AdamW) at bs=64 per GPU on MI355X.
+
+One "step" = forward + backward + AdamW over one batch of 64 synthetic 224x224 RGB+thermal
+pairs already resident in HBM (BASELINE.json config C3; C4 = the same per GPU over N ranks,
+launched by torch.distributed.run, RCCL gradient all-reduce).  Prints ONE JSON line on rank 0.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--config fusion|thermal|rgb]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "dfu-multimodal_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# Algorithmic GEMM/conv FLOPs per unit of work (fwd + dgrad + wgrad), SURVEY.md §8(d)
+FLOPS_PER_UNIT = {"fusion": 129.44e9, "thermal": 105.15e9, "rgb": 24.29e9}
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+RGB_MEAN = (0.485, 0.456, 0.406)
+RGB_STD = (0.229, 0.224, 0.225)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--config", default="fusion", choices=["fusion", "thermal", "rgb"])
+    ap.add_argument("--no-graph", action="store_true", help="eager step instead of a HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def synthetic(B, device, seed):
+    """uint8 U{0..255} images normalised as the reference transforms
+    (train_multimodal_fusion.py:181, 198), labels U{0,1}; generated once on the device."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    rgb = torch.randint(0, 256, (B, 3, 224, 224), generator=g, device=device, dtype=torch.uint8)
+    th = torch.randint(0, 256, (B, 3, 224, 224), generator=g, device=device, dtype=torch.uint8)
+    y = torch.randint(0, 2, (B,), generator=g, device=device, dtype=torch.int64)
+    mean = torch.tensor(RGB_MEAN, device=device).view(1, 3, 1, 1)
+    std = torch.tensor(RGB_STD, device=device).view(1, 3, 1, 1)
+    rgb = ((rgb.float() / 255.0 - mean) / std).contiguous()
+    th = ((th.float() / 255.0 - 0.5) / 0.5).contiguous()
+    return rgb, th, y
+
+
+def build(config, device):
+    import torch.nn as tnn
+    from models import encoders
+    from models.fusion import MultimodalFusionModel
+    from dfu_hip import nn as hnn
+    if config == "fusion":
+        model = MultimodalFusionModel(num_classes=2, dropout=0.7)
+        fwd = lambda m, r, t: m(r, t)  # noqa: E731
+    elif config == "thermal":  # train_thermal_only.py:188-205
+        model = encoders.vit_base_patch16_224(num_classes=2)
+        model.head = tnn.Sequential(hnn.Dropout(0.5), hnn.Linear(768, 2))
+        fwd = lambda m, r, t: m(t)  # noqa: E731
+    else:  # train_rgb_only.py:200-217
+        model = encoders.resnet50()
+        model.fc = tnn.Sequential(hnn.Dropout(0.5), hnn.Linear(2048, 2))
+        fwd = lambda m, r, t: m(r)  # noqa: E731
+    return model.to(device).train(), fwd
+
+
+def cpu_baseline(config, threads):
+    """The oracle (plain PyTorch fp32, oracle/torch_ref.py) timed on the host cores on a bounded
+    sample of the same workload: full train step (fwd+bwd+AdamW) at B=4, 1 warm-up + 2 timed."""
+    from oracle import torch_ref as R
+    torch.set_num_threads(threads)
+    B = 4
+    torch.manual_seed(0)
+    if config == "fusion":
+        model = R.MultimodalFusionModel(num_classes=2, dropout=0.7)
+        run = lambda r, t: model(r, t)  # noqa: E731
+    elif config == "thermal":
+        model = R.VisionTransformer(num_classes=2)
+        run = lambda r, t: model(t)  # noqa: E731
+    else:
+        model = R.ResNet(num_classes=2)
+        run = lambda r, t: model(r)  # noqa: E731
+    model.train()
+    rgb, th, y = R.synthetic_batch(B, seed=42)
+    crit = torch.nn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0]))
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+
+    def step():
+        opt.zero_grad()
+        loss = crit(run(rgb, th), y)
+        loss.backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    n = 2
+    for _ in range(n):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 3), "unit": "images/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle fp32 eager {config} train step (fwd+bwd+AdamW), batch {B}, "
+                      f"{n} timed steps after 1 warm-up, torch.set_num_threads({threads})"}
+
+
+def main():
+    args = parse()
+    from dfu_hip import parallel
+    rank, world, local = parallel.init_from_env()
+    if world > 1 and world != args.gpus:
+        args.gpus = world
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(42)
+
+    from dfu_hip import nn as hnn
+    from dfu_hip.optim import FusedAdamW
+    model, fwd = build(args.config, dev)
+    parallel.broadcast_parameters(model)
+    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
+    reducer = parallel.GradAllReducer(opt.flat, overlap=False) if world > 1 else None
+    rgb, th, y = synthetic(args.batch, dev, seed=42 + rank)
+
+    def fwd_bwd():
+        opt.zero_grad()
+        out = fwd(model, rgb, th)
+        loss = crit(out, y)
+        loss.backward()
+        return loss
+
+    def tail():
+        if reducer is not None:
+            reducer.finish()
+        opt.step()
+
+    use_graph = not args.no_graph
+    graph = None
+    # warm-up (also builds every persistent buffer) on a side stream, as graph capture needs
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(max(1, args.warmup)):
+            fwd_bwd()
+            tail()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    if use_graph:
+        try:
+            opt.check_grads = False
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                fwd_bwd()
+                if reducer is None:
+                    opt.step()
+            for _ in range(2):
+                graph.replay()
+                if reducer is not None:
+                    tail()
+            torch.cuda.synchronize()
+        except Exception as e:  # graph capture is an optimisation; report and run eager
+            if rank == 0:
+                print(f"[bench] graph capture failed ({type(e).__name__}: {e}); eager", file=sys.stderr)
+            graph = None
+            opt.check_grads = True
+            torch.cuda.synchronize()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+            if reducer is not None:
+                tail()
+        else:
+            fwd_bwd()
+            tail()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        t = torch.tensor([elapsed, gpu_ms / 1000.0], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gpu_s = t.tolist()
+        gpu_ms = gpu_s * 1000.0
+    imgs = args.batch * args.gpus * args.steps
+    value = imgs / elapsed
+    per_gpu_step_s = (gpu_ms / 1000.0) / args.steps
+    achieved = args.batch * FLOPS_PER_UNIT[args.config] / per_gpu_step_s / 1e12
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(args.config, min(args.cpu_threads, os.cpu_count() or 1))
+            except Exception as e:  # never lose the GPU line over the baseline
+                cpu = {"error": f"{type(e).__name__}: {e}"}
+        metric = {"fusion": "images/sec (fusion fwd+bwd, bs=64/GPU)",
+                  "thermal": "images/sec (thermal ViT-B/16 fwd+bwd, bs=64/GPU)",
+                  "rgb": "images/sec (RGB ResNet50 fwd+bwd, bs=64/GPU)"}[args.config]
+        line = {
+            "metric": metric,
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": args.gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1000.0 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic 224x224 RGB+thermal pairs (uint8 U{0..255}, reference "
+                    "normalisation), random-init weights (seed 42), resident in HBM",
+            "config": {"workload": f"C3 {args.config} train step (fwd+bwd+AdamW) "
+                                   f"ResNet50+ViT-B/16 -> 2816->512->2",
+                       "model": "resnet50+vit_base_patch16_224 late fusion",
+                       "global_batch": args.batch * args.gpus, "per_gpu_batch": args.batch,
+                       "image": 224, "parallelism": f"dp{args.gpus}",
+                       "hip_graph": graph is not None},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
+                         "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "basis": f"{FLOPS_PER_UNIT[args.config] / 1e9:.2f} GFLOP per image "
+                                  f"(SURVEY 8d) x {args.batch} per launch of the captured step / "
+                                  f"HIP-event step time {per_gpu_step_s * 1e3:.3f} ms"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -163,8 +163,9 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
 
 __global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int blocks, int64_t M, int C,
                                   const float* __restrict__ gamma,
-                                  const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                  float* __restrict__ dbeta, float* __restrict__ coef) {
+                                  const float* __restrict__ invstd, int batch_stats,
+                                  float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                  float* __restrict__ coef) {
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     double sg = 0.0, sgx = 0.0;
     for (int b = 0; b < blocks; ++b) {
@@ -175,8 +176,8 @@ __global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int blocks,
     if (dgamma) dgamma[c] += (float)sgx;
     const float g = gamma ? gamma[c] : 1.f;
     coef[3 * c + 0] = g * invstd[c];
-    coef[3 * c + 1] = (float)(sg / (double)M);
-    coef[3 * c + 2] = (float)(sgx / (double)M);
+    coef[3 * c + 1] = batch_stats ? (float)(sg / (double)M) : 0.f;
+    coef[3 * c + 2] = batch_stats ? (float)(sgx / (double)M) : 0.f;
   }
 }
 
@@ -280,11 +281,11 @@ extern "C" int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* ou
 }
 
 extern "C" int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t M, int32_t C,
-                                   const float* gamma, const float* invstd, float* dgamma,
-                                   float* dbeta, float* coef, void* stream) {
+                                   const float* gamma, const float* invstd, int32_t batch_stats,
+                                   float* dgamma, float* dbeta, float* coef, void* stream) {
   DFU_CHECK_ARG(partial && invstd && coef && blocks > 0 && C > 0, "dfu_bn_bwd_finalize: bad args");
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     partial, blocks, M, C, gamma, invstd, dgamma, dbeta, coef);
+                     partial, blocks, M, C, gamma, invstd, batch_stats, dgamma, dbeta, coef);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -1,0 +1,729 @@
+"""autograd Functions of the DFU fusion training step, each a hand-scheduled sequence of
+libdfu_hip kernels (no ATen compute on this path).
+
+Granularity follows the reference's module tree so the nn.Module surface stays drop-in:
+  StemFn         torchvision resnet conv1 + bn1 + relu + maxpool        (resnet.py _forward_impl)
+  BottleneckFn   torchvision Bottleneck (v1.5, stride on the 3x3)        (resnet.py Bottleneck)
+  AvgPoolFn      AdaptiveAvgPool2d(1) on NHWC -> (B, C, 1, 1) fp32
+  PatchEmbedFn   timm PatchEmbed + cls token + pos_embed                 (vision_transformer.py)
+  ViTBlockFn     timm Block: x += attn(norm1(x)); x += mlp(norm2(x))
+  TokenNormFn    timm final norm applied to the class token rows only (global_pool='token')
+  LinearFn / ReLUFn / DropoutFn / ConcatFn   fusion head (train_multimodal_fusion.py:305-324)
+  CrossEntropyFn weighted CE (train_multimodal_fusion.py:342-346)
+
+Conventions:
+  * ResNet activations are bf16 tensors of logical shape (B, C, H, W) in channels_last memory
+    (physically NHWC); ViT activations are the fp32 residual stream (B, T, D).
+  * Parameter gradients are ACCUMULATED into persistent ``param.grad`` buffers by the
+    weight-gradient GEMM epilogues (``grad_buffer``), and backward returns None for them: this
+    keeps .grad addresses stable for graph replay, the fused optimizer and bucketed all-reduce.
+  * ViT residual-stream gradients are fp32 and modified in place by the LayerNorm backward
+    (the producer of every such tensor is a Function in this file).
+"""
+import math
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+# ------------------------------------------------------------------------- grad plumbing
+_grad_ready_hooks = []
+
+
+def register_grad_ready_hook(fn):
+    """fn(param) is called after a Function has finished writing param.grad (DP bucketing)."""
+    _grad_ready_hooks.append(fn)
+    return fn
+
+
+def remove_grad_ready_hook(fn):
+    if fn in _grad_ready_hooks:
+        _grad_ready_hooks.remove(fn)
+
+
+def grad_buffer(p):
+    """Persistent fp32 gradient buffer of parameter p (zeroed on first use)."""
+    g = p.grad
+    if g is None:
+        g = torch.empty_like(p, memory_format=torch.contiguous_format)
+        ops.zero_(g)
+        p.grad = g
+    return g
+
+
+def grads_done(*params):
+    for p in params:
+        if p is not None:
+            for h in _grad_ready_hooks:
+                h(p)
+
+
+def _wants(p):
+    return p is not None and p.requires_grad
+
+
+def _empty(shape, dtype, device):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+def nhwc_bf16(x):
+    """Return x (B,C,H,W) as a bf16 channels_last tensor (no copy when it already is one)."""
+    if x.dtype != BF16:
+        x = x.to(BF16)
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    return x
+
+
+def rows_view(x):
+    """[B*H*W, C] view of a channels_last (B,C,H,W) tensor."""
+    B, C, H, W = x.shape
+    return x.permute(0, 2, 3, 1).reshape(B * H * W, C)
+
+
+def from_rows(r, B, H, W, C):
+    return r.view(B, H, W, C).permute(0, 3, 1, 2)
+
+
+def weight_bf16_rows(w, ld=None):
+    """fp32 [N, K...] parameter -> bf16 [N, ld] (GEMM operand, re-cast every call)."""
+    w2 = w.detach().reshape(w.shape[0], -1)
+    return ops.cast_rows_bf16(w2, ld_out=ld)
+
+
+def split_for(M, N, K):
+    return ops.choose_split(M, N, K)
+
+
+# ---------------------------------------------------------------------- BatchNorm helper
+class _BN:
+    """Forward/backward state of one BatchNorm2d applied to a GEMM output with stats."""
+
+    def __init__(self, bn, M, C, device):
+        self.bn = bn
+        self.M, self.C = M, C
+        self.training = bn.training or not bn.track_running_stats
+        self.mean = _empty((C,), F32, device)
+        self.invstd = _empty((C,), F32, device)
+        self.scale = _empty((C,), F32, device)
+        self.shift = _empty((C,), F32, device)
+
+    def forward_coeffs(self, stats):
+        bn = self.bn
+        if self.training:
+            track = bn.track_running_stats and bn.training
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            ops.bn_finalize(stats, self.M, self.C, bn.weight, bn.bias, bn.eps, mom,
+                            bn.running_mean if track else None,
+                            bn.running_var if track else None,
+                            bn.num_batches_tracked if track else None,
+                            self.mean, self.invstd, self.scale, self.shift)
+        else:
+            ops.bn_eval_coeffs(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
+                               self.scale, self.shift)
+            self.mean.copy_(bn.running_mean)
+            ops.bn_eval_coeffs(None, None, bn.running_mean, bn.running_var, bn.eps,
+                               self.invstd, _empty((self.C,), F32, self.mean.device))
+
+    def backward(self, dout, y, out, relu, dy, dres):
+        bn = self.bn
+        dgamma = grad_buffer(bn.weight) if _wants(bn.weight) else None
+        dbeta = grad_buffer(bn.bias) if _wants(bn.bias) else None
+        ops.bn_bwd(dout, y, out, relu, self.mean, self.invstd, bn.weight, self.M, self.C, dy,
+                   dres, dgamma, dbeta, batch_stats=self.training)
+        grads_done(bn.weight, bn.bias)
+
+
+# --------------------------------------------------------------------------- conv helpers
+def conv_fwd(x_rows, geom, w_krsc, y, stats):
+    """y[M, K] = conv(x) for NHWC x with a KRSC bf16 weight; BN tile statistics into stats."""
+    g = geom
+    M = g.n * g.p * g.q
+    if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
+        ops.gemm(M, g.k, g.c, x_rows, g.c, w_krsc, g.c, y, g.k, epilogue=L.EPI_BF16_STATS,
+                 stats=stats)
+    else:
+        K = g.r * g.s * g.c
+        ops.gemm(M, g.k, K, x_rows, 0, w_krsc, K, y, g.k, a_mode=L.OPND_CONV_FWD,
+                 epilogue=L.EPI_BF16_STATS, stats=stats, conv=g)
+
+
+def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None):
+    """dx[N*H*W, C] = dgrad(dy) (+ add, bf16)."""
+    g = geom
+    Mx = g.n * g.h * g.w
+    epi = L.EPI_BF16_ADD if add is not None else L.EPI_BF16
+    ld_add = g.c if add is not None else 0
+    if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
+        ops.gemm(Mx, g.c, g.k, dy_rows, g.k, w_krsc, g.c, dx, g.c, b_mode=L.OPND_MNMAJOR,
+                 epilogue=epi, aux=add, ldaux=ld_add)
+    else:
+        ops.gemm(Mx, g.c, g.r * g.s * g.k, dy_rows, 0, w_krsc, g.r * g.s * g.c, dx, g.c,
+                 a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=epi, aux=add,
+                 ldaux=ld_add, conv=g)
+
+
+def conv_wgrad(dy_rows, x_rows, geom, dw):
+    """dw (fp32 OIHW) += wgrad(dy, x)."""
+    g = geom
+    M = g.n * g.p * g.q
+    if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
+        split = split_for(g.k, g.c, M)
+        ops.gemm(g.k, g.c, M, dy_rows, g.k, x_rows, g.c, dw, g.c, a_mode=L.OPND_MNMAJOR,
+                 b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC, split_k=split)
+    else:
+        N = g.r * g.s * g.c
+        split = split_for(g.k, N, M)
+        ops.gemm(g.k, N, M, dy_rows, g.k, x_rows, 0, dw, N, a_mode=L.OPND_MNMAJOR,
+                 b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC_CONVW, split_k=split,
+                 conv=g)
+
+
+def _geom(conv, B, H, W):
+    Cout, Cin, R, S = conv.weight.shape
+    return ops.ConvGeom(B, H, W, Cin, Cout, R, S, conv.stride[0], conv.padding[0])
+
+
+# ------------------------------------------------------------------------------- stem
+class StemFn(torch.autograd.Function):
+    """conv1 7x7/s2/p3 (3->64, explicit bf16 im2col, K padded 147->160) + bn1 + relu +
+    maxpool 3x3/s2/p1.  Input fp32 (B,3,H,W) any strides; output bf16 channels_last."""
+
+    KP = 160
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, mod):
+        conv, bn = mod.conv1, mod.bn1
+        B, C, H, W = x.shape
+        R = S = conv.weight.shape[2]
+        st, pad = conv.stride[0], conv.padding[0]
+        Kp = ((C * R * S + 15) // 16) * 16
+        xf = x.detach().float() if x.dtype != F32 else x.detach()
+        col, P, Q = ops.im2col_f32(xf, R, S, st, pad, Kp)
+        wb = weight_bf16_rows(w, ld=Kp)
+        Cout = w.shape[0]
+        M = B * P * Q
+        y = _empty((M, Cout), BF16, x.device)
+        stats = _empty((ops.stats_tiles(M), 2, Cout), F32, x.device)
+        ops.gemm(M, Cout, Kp, col, Kp, wb, Kp, y, Cout, epilogue=L.EPI_BF16_STATS, stats=stats)
+        bns = _BN(bn, M, Cout, x.device)
+        bns.forward_coeffs(stats)
+        a = _empty((M, Cout), BF16, x.device)
+        ops.bn_apply(y, bns.scale, bns.shift, None, True, a, M, Cout)
+        out, am, P2, Q2 = ops.maxpool_fwd(a, B, P, Q, Cout)
+        ctx.mod = mod
+        ctx.bns = bns
+        ctx.dims = (B, C, H, W, P, Q, P2, Q2, Cout, Kp, R, S, st, pad)
+        ctx.x_requires_grad = x.requires_grad
+        ctx.save_for_backward(col, y, a, am, wb)
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gout):
+        col, y, a, am, wb = ctx.saved_tensors
+        B, C, H, W, P, Q, P2, Q2, Cout, Kp, R, S, st, pad = ctx.dims
+        mod = ctx.mod
+        g = rows_view(nhwc_bf16(gout))
+        da = ops.maxpool_bwd(g, am, B, P, Q, Cout, P2, Q2).view(B * P * Q, Cout)
+        M = B * P * Q
+        dy = torch.empty_like(y)
+        ctx.bns.backward(da, y, a, True, dy, None)
+        w = mod.conv1.weight
+        if _wants(w):
+            dw = grad_buffer(w).view(Cout, -1)
+            K = C * R * S
+            ops.gemm(Cout, K, M, dy, Cout, col, Kp, dw, K, a_mode=L.OPND_MNMAJOR,
+                     b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC,
+                     split_k=split_for(Cout, K, M))
+            grads_done(w)
+        dx = None
+        if ctx.x_requires_grad:
+            # Grad-CAM path (grad_cam_visualization.py:374): dcol = dy W, then col2im.
+            wkn = wb  # [Cout][Kp] viewed as B[k=cout][n=kp]
+            dcol = _empty((M, Kp), BF16, y.device)
+            ops.gemm(M, Kp, Cout, dy, Cout, wkn, Kp, dcol, Kp, b_mode=L.OPND_MNMAJOR,
+                     epilogue=L.EPI_BF16)
+            dx = col2im_f32(dcol, B, C, H, W, R, S, st, pad, P, Q, Kp)
+        return dx, None, None, None, None
+
+
+def col2im_f32(dcol, B, C, H, W, R, S, st, pad, P, Q, Kp):
+    """Adjoint of dfu_im2col_f32 (used only for input gradients, Grad-CAM)."""
+    # Expressed with the patch GEMM identity: input gradient of the explicit im2col is the sum
+    # of the column entries that read each pixel; done with F.fold over fp32 columns.
+    import torch.nn.functional as F
+    cols = dcol[:, :C * R * S].float().view(B, P * Q, C * R * S).transpose(1, 2)
+    return F.fold(cols, (H, W), (R, S), padding=pad, stride=st)
+
+
+# ---------------------------------------------------------------------------- Bottleneck
+class BottleneckFn(torch.autograd.Function):
+    """torchvision Bottleneck: relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1 x))))))) + id)."""
+
+    @staticmethod
+    def forward(ctx, x, *params_and_mod):
+        mod = params_and_mod[-1]
+        x = nhwc_bf16(x.detach())
+        B, Cin, H, W = x.shape
+        dev = x.device
+        xr = rows_view(x)
+        g1 = _geom(mod.conv1, B, H, W)
+        g2 = _geom(mod.conv2, B, g1.p, g1.q)
+        g3 = _geom(mod.conv3, B, g2.p, g2.q)
+        w1 = ops.pack_conv_weight(mod.conv1.weight.detach())
+        w2 = ops.pack_conv_weight(mod.conv2.weight.detach())
+        w3 = ops.pack_conv_weight(mod.conv3.weight.detach())
+        M1 = B * g1.p * g1.q
+        M2 = B * g2.p * g2.q
+        planes, outc = g1.k, g3.k
+
+        def conv_bn(xrows, geom, w, bnmod, relu, residual=None):
+            M = geom.n * geom.p * geom.q
+            y = _empty((M, geom.k), BF16, dev)
+            stats = _empty((ops.stats_tiles(M), 2, geom.k), F32, dev)
+            conv_fwd(xrows, geom, w, y, stats)
+            st = _BN(bnmod, M, geom.k, dev)
+            st.forward_coeffs(stats)
+            out = _empty((M, geom.k), BF16, dev)
+            ops.bn_apply(y, st.scale, st.shift, residual, relu, out, M, geom.k)
+            return y, out, st
+
+        y1, a1, s1 = conv_bn(xr, g1, w1, mod.bn1, True)
+        y2, a2, s2 = conv_bn(a1, g2, w2, mod.bn2, True)
+        if mod.downsample is not None:
+            dconv, dbn = mod.downsample[0], mod.downsample[1]
+            gd = _geom(dconv, B, H, W)
+            wd = ops.pack_conv_weight(dconv.weight.detach())
+            yd, idn, sd = conv_bn(xr, gd, wd, dbn, False)
+        else:
+            gd = wd = yd = sd = None
+            idn = xr
+        y3, out, s3 = conv_bn(a2, g3, w3, mod.bn3, True, residual=idn)
+        ctx.mod = mod
+        ctx.geo = (g1, g2, g3, gd)
+        ctx.bns = (s1, s2, s3, sd)
+        ctx.shape = (B, Cin, H, W)
+        ctx.x_requires_grad = ctx.needs_input_grad[0]
+        ctx.save_for_backward(xr, y1, a1, y2, a2, y3, out, w1, w2, w3,
+                              *( (yd, wd) if yd is not None else ()))
+        return from_rows(out, B, g3.p, g3.q, outc)
+
+    @staticmethod
+    def backward(ctx, gout):
+        saved = ctx.saved_tensors
+        xr, y1, a1, y2, a2, y3, out, w1, w2, w3 = saved[:10]
+        yd, wd = (saved[10], saved[11]) if len(saved) > 10 else (None, None)
+        mod = ctx.mod
+        g1, g2, g3, gd = ctx.geo
+        s1, s2, s3, sd = ctx.bns
+        B, Cin, H, W = ctx.shape
+        dev = xr.device
+        g = rows_view(nhwc_bf16(gout))
+        M1, M2 = y1.shape[0], y3.shape[0]
+        # bn3 (+ residual) + relu
+        dy3 = torch.empty_like(y3)
+        dres = torch.empty_like(y3)
+        s3.backward(g, y3, out, True, dy3, dres)
+        # downsample branch
+        dx_id = None
+        if yd is not None:
+            dyd = torch.empty_like(yd)
+            sd.backward(dres, yd, None, False, dyd, None)
+            dconv = mod.downsample[0]
+            if _wants(dconv.weight):
+                conv_wgrad(dyd, xr, gd, grad_buffer(dconv.weight))
+                grads_done(dconv.weight)
+            if ctx.x_requires_grad:
+                dx_id = _empty((M1, Cin), BF16, dev)
+                conv_dgrad(dyd, gd, wd, dx_id)
+        else:
+            dx_id = dres
+        # conv3
+        da2 = torch.empty_like(a2)
+        conv_dgrad(dy3, g3, w3, da2)
+        if _wants(mod.conv3.weight):
+            conv_wgrad(dy3, a2, g3, grad_buffer(mod.conv3.weight))
+            grads_done(mod.conv3.weight)
+        # bn2 + relu, conv2
+        dy2 = torch.empty_like(y2)
+        s2.backward(da2, y2, a2, True, dy2, None)
+        da1 = torch.empty_like(a1)
+        conv_dgrad(dy2, g2, w2, da1)
+        if _wants(mod.conv2.weight):
+            conv_wgrad(dy2, a1, g2, grad_buffer(mod.conv2.weight))
+            grads_done(mod.conv2.weight)
+        # bn1 + relu, conv1 (+ identity gradient fused in the dgrad epilogue)
+        dy1 = torch.empty_like(y1)
+        s1.backward(da1, y1, a1, True, dy1, None)
+        dx = None
+        if ctx.x_requires_grad:
+            dxr = _empty((M1, Cin), BF16, dev)
+            conv_dgrad(dy1, g1, w1, dxr, add=dx_id)
+            dx = from_rows(dxr, B, H, W, Cin)
+        if _wants(mod.conv1.weight):
+            conv_wgrad(dy1, xr, g1, grad_buffer(mod.conv1.weight))
+            grads_done(mod.conv1.weight)
+        n_params = len(ctx.needs_input_grad) - 2
+        return (dx,) + (None,) * n_params + (None,)
+
+
+# ------------------------------------------------------------------------------ avgpool
+class AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = nhwc_bf16(x.detach())
+        B, C, H, W = x.shape
+        ctx.shape = (B, C, H, W)
+        y = ops.avgpool_fwd(rows_view(x), B, H * W, C)
+        return y.view(B, C, 1, 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, H, W = ctx.shape
+        g = g.reshape(B, C)
+        if g.dtype != F32:
+            g = g.float()
+        dx = ops.avgpool_bwd(g.contiguous(), B, H * W, C)
+        return from_rows(dx.view(B * H * W, C), B, H, W, C)
+
+
+# ------------------------------------------------------------------------ ViT embedding
+class PatchEmbedFn(torch.autograd.Function):
+    """timm PatchEmbed (conv16/s16 + flatten) + cat(cls_token) + pos_embed -> fp32 (B,T,D)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cls, pos, ps):
+        B, C, H, W = x.shape
+        D = w.shape[0]
+        xf = x.detach().float() if x.dtype != F32 else x.detach()
+        patches = ops.patchify_f32(xf, ps)
+        T = (H // ps) * (W // ps)
+        wb = weight_bf16_rows(w)
+        K = wb.shape[1]
+        X = _empty((B, T + 1, D), F32, x.device)
+        ops.gemm(B * T, D, K, patches, K, wb, K, X, D, epilogue=L.EPI_PATCH,
+                 bias=b.detach() if b is not None else None, aux=pos.detach().reshape(T + 1, D),
+                 ldaux=D, ep_tokens=T)
+        ops.vit_cls_rows(cls.detach().reshape(D), pos.detach().reshape(T + 1, D), X, B, T + 1, D)
+        ctx.params = (w, b, cls, pos)
+        ctx.dims = (B, T, D, K)
+        ctx.save_for_backward(patches)
+        return X
+
+    @staticmethod
+    def backward(ctx, gX):
+        (patches,) = ctx.saved_tensors
+        w, b, cls, pos = ctx.params
+        B, T, D, K = ctx.dims
+        gX = gX.contiguous()
+        gpatch = ops.vit_embed_bwd(gX, B, T + 1, D,
+                                   grad_buffer(cls) if _wants(cls) else None,
+                                   grad_buffer(pos) if _wants(pos) else None,
+                                   grad_buffer(b) if _wants(b) else None)
+        if _wants(w):
+            dw = grad_buffer(w).view(D, K)
+            ops.gemm(D, K, B * T, gpatch, D, patches, K, dw, K, a_mode=L.OPND_MNMAJOR,
+                     b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC,
+                     split_k=split_for(D, K, B * T))
+        grads_done(w, b, cls, pos)
+        return None, None, None, None, None, None
+
+
+# ---------------------------------------------------------------------------- ViT block
+def _linear_wgrad(dy_bf, x_bf, w, rows):
+    """w.grad [N, K] += dy^T x  (dy [rows, N], x [rows, K], both bf16)."""
+    N, K = w.shape
+    ops.gemm(N, K, rows, dy_bf, N, x_bf, K, grad_buffer(w), K, a_mode=L.OPND_MNMAJOR,
+             b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC, split_k=split_for(N, K, rows))
+
+
+def _ln_fwd(x2d, norm, rows, D, out_bf):
+    mean = _empty((rows,), F32, x2d.device)
+    rstd = _empty((rows,), F32, x2d.device)
+    ops.layernorm_fwd(x2d, D, rows, D, norm.weight, norm.bias, norm.eps, out_bf, D, True, mean,
+                      rstd)
+    return mean, rstd
+
+
+def _ln_bwd(dy_bf, x2d, mean, rstd, norm, rows, D, g, g_bf):
+    ops.layernorm_bwd(dy_bf, D, True, x2d, D, mean, rstd, norm.weight, rows, D, g, D, g_bf,
+                      grad_buffer(norm.weight) if _wants(norm.weight) else None,
+                      grad_buffer(norm.bias) if _wants(norm.bias) else None)
+    grads_done(norm.weight, norm.bias)
+
+
+def _bf16_of_grad(g):
+    """bf16 copy of an fp32 residual-stream gradient: reuse the one the producing LayerNorm
+    backward emitted (stashed on the tensor) or cast."""
+    gb = getattr(g, "_dfu_bf16", None)
+    if gb is not None and gb.shape == g.shape:
+        return gb
+    return ops.cast_rows_bf16(g.reshape(-1, g.shape[-1])).view(g.shape)
+
+
+class ViTBlockFn(torch.autograd.Function):
+    """timm Block (pre-norm, qkv_bias, SDPA, exact GELU, no LayerScale, drop_path 0)."""
+
+    @staticmethod
+    def forward(ctx, x, *params_and_mod):
+        blk = params_and_mod[-1]
+        attn, mlp = blk.attn, blk.mlp
+        B, T, D = x.shape
+        rows = B * T
+        H = attn.num_heads
+        dh = D // H
+        dev = x.device
+        x = x.detach().contiguous()
+        x2 = x.view(rows, D)
+        wqkv = weight_bf16_rows(attn.qkv.weight)
+        wproj = weight_bf16_rows(attn.proj.weight)
+        wfc1 = weight_bf16_rows(mlp.fc1.weight)
+        wfc2 = weight_bf16_rows(mlp.fc2.weight)
+        Dh = wfc1.shape[0]
+        bias = lambda lin: lin.bias.detach() if lin.bias is not None else None  # noqa: E731
+        # attention branch
+        xn1 = _empty((rows, D), BF16, dev)
+        m1, r1 = _ln_fwd(x2, blk.norm1, rows, D, xn1)
+        qkv = _empty((rows, 3 * D), BF16, dev)
+        ops.gemm(rows, 3 * D, D, xn1, D, wqkv, D, qkv, 3 * D, epilogue=L.EPI_BF16,
+                 bias=bias(attn.qkv))
+        o, lse = ops.attention_fwd(qkv, B, T, H, dh, attn.scale)
+        xm = _empty((rows, D), F32, dev)
+        ops.gemm(rows, D, D, o, D, wproj, D, xm, D, epilogue=L.EPI_F32_RESID, bias=bias(attn.proj),
+                 aux=x2, ldaux=D)
+        # MLP branch
+        xn2 = _empty((rows, D), BF16, dev)
+        m2, r2 = _ln_fwd(xm, blk.norm2, rows, D, xn2)
+        hpre = _empty((rows, Dh), BF16, dev)
+        h = _empty((rows, Dh), BF16, dev)
+        ops.gemm(rows, Dh, D, xn2, D, wfc1, D, h, Dh, epilogue=L.EPI_BF16_GELU, bias=bias(mlp.fc1),
+                 aux_out=hpre, ldaux_out=Dh)
+        xo = _empty((B, T, D), F32, dev)
+        ops.gemm(rows, D, Dh, h, Dh, wfc2, Dh, xo.view(rows, D), D, epilogue=L.EPI_F32_RESID,
+                 bias=bias(mlp.fc2), aux=xm, ldaux=D)
+        ctx.blk = blk
+        ctx.dims = (B, T, D, H, dh, Dh)
+        ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv,
+                              wproj, wfc1, wfc2)
+        return xo
+
+    @staticmethod
+    def backward(ctx, gout):
+        (x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv, wproj, wfc1,
+         wfc2) = ctx.saved_tensors
+        blk = ctx.blk
+        attn, mlp = blk.attn, blk.mlp
+        B, T, D, H, dh, Dh = ctx.dims
+        rows = B * T
+        dev = x2.device
+        g = gout.contiguous()
+        if g.dtype != F32:
+            g = g.float()
+        g2 = g.view(rows, D)
+        gb = _bf16_of_grad(g).view(rows, D)
+        # ---- MLP branch: x_out = x_mid + fc2(gelu(fc1(norm2(x_mid))))
+        dh_pre = _empty((rows, Dh), BF16, dev)
+        ops.gemm(rows, Dh, D, gb, D, wfc2, Dh, dh_pre, Dh, b_mode=L.OPND_MNMAJOR,
+                 epilogue=L.EPI_BF16_DGELU, aux=hpre, ldaux=Dh)
+        if _wants(mlp.fc2.weight):
+            _linear_wgrad(gb, h, mlp.fc2.weight, rows)
+        if _wants(mlp.fc2.bias):
+            ops.colsum_add(g2, grad_buffer(mlp.fc2.bias))
+        grads_done(mlp.fc2.weight, mlp.fc2.bias)
+        dxn2 = _empty((rows, D), BF16, dev)
+        ops.gemm(rows, D, Dh, dh_pre, Dh, wfc1, D, dxn2, D, b_mode=L.OPND_MNMAJOR,
+                 epilogue=L.EPI_BF16)
+        if _wants(mlp.fc1.weight):
+            _linear_wgrad(dh_pre, xn2, mlp.fc1.weight, rows)
+        if _wants(mlp.fc1.bias):
+            ops.colsum_add(dh_pre, grad_buffer(mlp.fc1.bias))
+        grads_done(mlp.fc1.weight, mlp.fc1.bias)
+        gmb = _empty((rows, D), BF16, dev)
+        _ln_bwd(dxn2, xm, m2, r2, blk.norm2, rows, D, g2, gmb)  # g2 := g_mid (in place)
+        # ---- attention branch: x_mid = x_in + proj(attn(norm1(x_in)))
+        do = _empty((rows, D), BF16, dev)
+        ops.gemm(rows, D, D, gmb, D, wproj, D, do, D, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16)
+        if _wants(attn.proj.weight):
+            _linear_wgrad(gmb, o, attn.proj.weight, rows)
+        if _wants(attn.proj.bias):
+            ops.colsum_add(g2, grad_buffer(attn.proj.bias))
+        grads_done(attn.proj.weight, attn.proj.bias)
+        dqkv = ops.attention_bwd(qkv, o, do, lse, B, T, H, dh, attn.scale)
+        dxn1 = _empty((rows, D), BF16, dev)
+        ops.gemm(rows, D, 3 * D, dqkv, 3 * D, wqkv, D, dxn1, D, b_mode=L.OPND_MNMAJOR,
+                 epilogue=L.EPI_BF16)
+        if _wants(attn.qkv.weight):
+            _linear_wgrad(dqkv, xn1, attn.qkv.weight, rows)
+        if _wants(attn.qkv.bias):
+            ops.colsum_add(dqkv, grad_buffer(attn.qkv.bias))
+        grads_done(attn.qkv.weight, attn.qkv.bias)
+        gib = _empty((B, T, D), BF16, dev)
+        _ln_bwd(dxn1, x2, m1, r1, blk.norm1, rows, D, g2, gib.view(rows, D))  # g2 := g_in
+        gin = g.view(B, T, D)
+        gin._dfu_bf16 = gib
+        n_params = len(ctx.needs_input_grad) - 2
+        return (gin,) + (None,) * n_params + (None,)
+
+
+class TokenNormFn(torch.autograd.Function):
+    """timm final LayerNorm + token pooling x[:, 0]: only the class-token rows are normalised
+    (LayerNorm is per token, so this equals norm(x)[:, 0])."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, norm):
+        B, T, D = x.shape
+        x = x.detach().contiguous()
+        out = _empty((B, D), F32, x.device)
+        mean = _empty((B,), F32, x.device)
+        rstd = _empty((B,), F32, x.device)
+        ops.layernorm_fwd(x, T * D, B, D, norm.weight, norm.bias, norm.eps, out, D, False, mean,
+                          rstd)
+        ctx.norm = norm
+        ctx.save_for_backward(x, mean, rstd)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, mean, rstd = ctx.saved_tensors
+        norm = ctx.norm
+        B, T, D = x.shape
+        g = g.contiguous().float()
+        gx = _empty((B, T, D), F32, x.device)
+        ops.zero_(gx)
+        gxb = _empty((B, T, D), BF16, x.device)
+        ops.zero_(gxb)
+        ops.layernorm_bwd(g, D, False, x, T * D, mean, rstd, norm.weight, B, D, gx, T * D, gxb,
+                          grad_buffer(norm.weight) if _wants(norm.weight) else None,
+                          grad_buffer(norm.bias) if _wants(norm.bias) else None)
+        grads_done(norm.weight, norm.bias)
+        gx._dfu_bf16 = gxb
+        return gx, None, None, None
+
+
+# --------------------------------------------------------------------------- fusion head
+class LinearFn(torch.autograd.Function):
+    """y = x W^T + b (fp32 out) for the late-fusion MLP; x fp32 or bf16, any leading dims."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        lead = x.shape[:-1]
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = x.detach().reshape(-1, K)
+        rows = x2.shape[0]
+        xb = x2.contiguous() if x2.dtype == BF16 else ops.cast_rows_bf16(x2)
+        wb = weight_bf16_rows(w)
+        y = _empty((rows, N), F32, x.device)
+        ops.gemm(rows, N, K, xb, K, wb, K, y, N, epilogue=L.EPI_F32,
+                 bias=b.detach() if b is not None else None)
+        if relu:
+            y = ops.relu_fwd(y)
+        ctx.relu = relu
+        ctx.params = (w, b)
+        ctx.x_dtype = x.dtype
+        ctx.lead = lead
+        ctx.save_for_backward(xb, wb, y if relu else None)
+        return y.view(*lead, N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, wb, y = ctx.saved_tensors
+        w, b = ctx.params
+        rows, K = xb.shape
+        N = wb.shape[0]
+        g = gy.reshape(rows, N)
+        if g.dtype != F32:
+            g = g.float()
+        g = g.contiguous()
+        if ctx.relu:
+            g = ops.relu_bwd(g, y)
+        gb = ops.cast_rows_bf16(g, ld_out=max(8, (N + 7) // 8 * 8))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            # dX[rows, K] = g[rows, N] W[N, K]; N may be tiny (2), pad the contraction to 8
+            Np = gb.shape[1]
+            if Np != N:
+                wp = _empty((Np, K), BF16, xb.device)
+                ops.zero_(wp)
+                wp[:N].copy_(wb)
+            else:
+                wp = wb
+            out_bf = ctx.x_dtype == BF16
+            dx = _empty((rows, K), BF16 if out_bf else F32, xb.device)
+            ops.gemm(rows, K, Np, gb, Np, wp, K, dx, K, b_mode=L.OPND_MNMAJOR,
+                     epilogue=L.EPI_BF16 if out_bf else L.EPI_F32)
+            dx = dx.view(*ctx.lead, K)
+        if _wants(w):
+            ops.gemm(N, K, rows, gb, gb.shape[1], xb, K, grad_buffer(w), K,
+                     a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+        if _wants(b):
+            ops.colsum_add(g, grad_buffer(b))
+        grads_done(w, b)
+        return dx, None, None, None
+
+
+class ReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = ops.relu_fwd(x.detach().contiguous())
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        return ops.relu_bwd(g.contiguous().to(y.dtype), y)
+
+
+class DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed, offset):
+        y, mask = ops.dropout_fwd(x.detach().contiguous(), p, seed, offset)
+        ctx.p = p
+        ctx.save_for_backward(mask)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (mask,) = ctx.saved_tensors
+        return ops.dropout_bwd(g.contiguous(), mask, ctx.p), None, None, None
+
+
+class ConcatFn(torch.autograd.Function):
+    """torch.cat([rgb_feat, thermal_feat], 1) into one bf16 GEMM operand."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.dims = (a.shape[1], b.shape[1])
+        ctx.dtypes = (a.dtype, b.dtype)
+        return ops.concat2_bf16(a.detach(), b.detach())
+
+    @staticmethod
+    def backward(ctx, g):
+        Na, Nb = ctx.dims
+        ga, gb = ops.split2_f32(g, Na, Nb)
+        if ctx.dtypes[0] != F32:
+            ga = ga.to(ctx.dtypes[0])
+        if ctx.dtypes[1] != F32:
+            gb = gb.to(ctx.dtypes[1])
+        return ga, gb
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, weight):
+        z = logits.detach().contiguous().float()
+        loss = _empty((1,), F32, z.device)
+        dz = torch.empty_like(z)
+        ops.ce_weighted_fwd(z, labels.contiguous(), weight, loss, dz)
+        ctx.save_for_backward(dz)
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        (dz,) = ctx.saved_tensors
+        return ops.ce_weighted_bwd(dz, g.reshape(1).float().contiguous()), None, None

@@ -168,7 +168,8 @@ def bn_apply(y, scale, shift, residual, relu, out, M, C):
                              M, C, stream_ptr()), "dfu_bn_apply")
 
 
-def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta):
+def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta,
+           batch_stats=True):
     """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply."""
     blocks = lib().dfu_bn_bwd_blocks(M)
     partial = torch.empty((blocks, 2, C), dtype=F32, device=y.device)
@@ -177,7 +178,8 @@ def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbet
     check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), int(relu), ptr(mean), ptr(invstd),
                                   M, C, ptr(partial), s), "dfu_bn_bwd_reduce")
     check(lib().dfu_bn_bwd_finalize(ptr(partial), blocks, M, C, ptr(gamma), ptr(invstd),
-                                    ptr(dgamma), ptr(dbeta), ptr(coef), s), "dfu_bn_bwd_finalize")
+                                    int(batch_stats), ptr(dgamma), ptr(dbeta), ptr(coef), s),
+          "dfu_bn_bwd_finalize")
     check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), int(relu), ptr(mean), ptr(invstd),
                                  ptr(coef), M, C, ptr(dy), ptr(dres), s), "dfu_bn_bwd_apply")
 

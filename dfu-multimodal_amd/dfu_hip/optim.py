@@ -1,0 +1,112 @@
+"""FusedAdamW: torch.optim.AdamW semantics (train_multimodal_fusion.py:347, 380:
+AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4), betas (0.9, 0.999), eps 1e-8) as ONE
+kernel launch over a flat fp32 parameter buffer.
+
+At construction the parameters are moved into one contiguous fp32 buffer (``p.data`` becomes a
+view) and ``p.grad`` into a matching flat gradient buffer, so:
+  * the optimizer step is a single HBM-streaming kernel (5 fp32 passes over 443 MB at B=64);
+  * zero_grad is one hipMemsetAsync;
+  * the weight-gradient GEMM epilogues accumulate straight into the flat buffer, whose
+    contiguous slices are what data-parallel all-reduce buckets send (dfu_hip.parallel);
+  * the step counter lives on the device, so the whole step can be captured in a HIP graph.
+"""
+import torch
+
+from . import ops
+
+_ALIGN = 4  # elements (16 B) so every tensor view starts 16-byte aligned
+
+
+def _aligned(n):
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class FlatParams:
+    """Contiguous fp32 storage for a list of parameters and their gradients."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("FlatParams: no trainable parameters")
+        dev = self.params[0].device
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            if p.dtype != torch.float32:
+                raise TypeError("FusedAdamW: fp32 master parameters expected")
+            self.offsets.append(off)
+            off += _aligned(p.numel())
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, o in zip(self.params, self.offsets):
+                view = self.data[o:o + p.numel()].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                p.grad = self.grad[o:o + p.numel()].view_as(p)
+
+    def grad_view(self, i):
+        p, o = self.params[i], self.offsets[i]
+        return self.grad[o:o + p.numel()].view_as(p)
+
+    def rebind_grads(self):
+        """Re-attach p.grad to the flat buffer if user code replaced or cleared it (eager)."""
+        for i, p in enumerate(self.params):
+            v = self.grad_view(i)
+            g = p.grad
+            if g is None:
+                ops.zero_(v)
+                p.grad = v
+            elif g.data_ptr() != v.data_ptr():
+                v.copy_(g)
+                p.grad = v
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 amsgrad=False, maximize=False):
+        if amsgrad or maximize:
+            raise NotImplementedError("FusedAdamW: amsgrad/maximize not supported")
+        params = list(params)
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        if len(self.param_groups) != 1:
+            raise NotImplementedError("FusedAdamW: a single param group")
+        self.flat = FlatParams(self.param_groups[0]["params"])
+        dev = self.flat.data.device
+        self.exp_avg = torch.zeros_like(self.flat.data)
+        self.exp_avg_sq = torch.zeros_like(self.flat.data)
+        self.step_dev = torch.zeros((), dtype=torch.int64, device=dev)
+        self.check_grads = True  # set False inside captured graphs (pointers are static)
+
+    def zero_grad(self, set_to_none=True):
+        # gradients stay bound to the flat buffer (stable addresses); one memset clears them
+        ops.zero_(self.flat.grad)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        if self.check_grads:
+            self.flat.rebind_grads()
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        ops.step_increment(self.step_dev)
+        ops.adamw_flat(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, g["lr"], b1,
+                       b2, g["eps"], g["weight_decay"], self.step_dev)
+        return loss
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["dfu_flat"] = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                          "step": self.step_dev}
+        return sd
+
+    def load_state_dict(self, state_dict):
+        flat = state_dict.get("dfu_flat")
+        sd = {k: v for k, v in state_dict.items() if k != "dfu_flat"}
+        super().load_state_dict(sd)
+        if flat is not None:
+            self.exp_avg.copy_(flat["exp_avg"])
+            self.exp_avg_sq.copy_(flat["exp_avg_sq"])
+            self.step_dev.copy_(flat["step"])

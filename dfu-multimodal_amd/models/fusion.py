@@ -1,0 +1,88 @@
+"""Late-fusion heads and the multimodal model.
+
+North-star head (grad_cam_visualization.py:289-302, extended_metrics.py:338-350):
+    cat([f_rgb (2048), f_th (768)]) -> Linear(2816, 512) -> ReLU -> Dropout(p) -> Linear(512, 2)
+``hidden_dims=(512, 256)`` builds the train-script variant (train_multimodal_fusion.py:305-313).
+"""
+import torch
+import torch.nn as tnn
+
+from dfu_hip import functional as Fn
+from dfu_hip import nn as hnn
+
+from .encoders import resnet50, vit_base_patch16_224
+
+
+def _mlp(in_dim, hidden_dims, num_classes, dropout):
+    layers = []
+    d = in_dim
+    for h in hidden_dims:
+        layers += [hnn.Linear(d, h), hnn.ReLU(), hnn.Dropout(dropout)]
+        d = h
+    layers.append(hnn.Linear(d, num_classes))
+    return tnn.Sequential(*layers)
+
+
+class MLPFusion(tnn.Module):
+    """MLPFusion(rgb_feat_dim=2048, thermal_feat_dim=768, hidden_dim=512, num_classes=2):
+    ``.classifier`` = Sequential(Linear, ReLU, Dropout(0.7), Linear)."""
+
+    def __init__(self, rgb_feat_dim=2048, thermal_feat_dim=768, hidden_dim=512, num_classes=2,
+                 dropout=0.7, hidden_dims=None):
+        super().__init__()
+        dims = tuple(hidden_dims) if hidden_dims is not None else (hidden_dim,)
+        self.classifier = _mlp(rgb_feat_dim + thermal_feat_dim, dims, num_classes, dropout)
+
+    def forward(self, rgb_feat, thermal_feat):
+        fused = Fn.ConcatFn.apply(rgb_feat, thermal_feat)
+        return self.classifier(fused)
+
+
+class MultimodalFusionModel(tnn.Module):
+    """ResNet50 (RGB) + ViT-B/16 (thermal) late fusion.
+
+    layout='eval' (default): attributes ``resnet``, ``vit``, ``fusion`` (an MLPFusion) — the
+    grad_cam_visualization.py:305-320 / extended_metrics.py:353-367 model, 2816->512->2.
+    layout='train': attributes ``rgb_branch``, ``thermal_branch``, ``fusion`` (a Sequential
+    with hidden_dims=(512, 256)) — train_multimodal_fusion.py:285-326 keys.
+    """
+
+    def __init__(self, num_classes=2, dropout=0.7, hidden_dims=(512,), layout="eval",
+                 pretrained=False):
+        super().__init__()
+        self.layout = layout
+        rgb = resnet50(pretrained=pretrained)
+        rgb.fc = tnn.Identity()
+        th = vit_base_patch16_224(pretrained=pretrained, num_classes=0)
+        if layout == "eval":
+            self.resnet = rgb
+            self.vit = th
+            self.fusion = MLPFusion(2048, 768, num_classes=num_classes, dropout=dropout,
+                                    hidden_dims=hidden_dims)
+        elif layout == "train":
+            self.rgb_branch = rgb
+            self.thermal_branch = th
+            self.fusion = _mlp(2048 + 768, tuple(hidden_dims) if hidden_dims != (512,) else (512, 256),
+                               num_classes, dropout)
+        else:
+            raise ValueError(f"layout must be 'eval' or 'train', got {layout!r}")
+
+    def forward(self, rgb, thermal):
+        if self.layout == "eval":
+            return self.fusion(self.resnet(rgb), self.vit(thermal))
+        f = Fn.ConcatFn.apply(self.rgb_branch(rgb), self.thermal_branch(thermal))
+        return self.fusion(f)
+
+
+class GatedFusion(tnn.Module):
+    """models/fusion.py:4-18 (early-era gated fusion; off the north-star path):
+    g = sigmoid(MLP(cat)), fused = g*rgb + (1-g)*th."""
+
+    def __init__(self, feat_dim=1280):
+        super().__init__()
+        self.gate = tnn.Sequential(hnn.Linear(feat_dim * 2, feat_dim), hnn.ReLU(),
+                                   hnn.Linear(feat_dim, feat_dim), tnn.Sigmoid())
+
+    def forward(self, rgb_feat, th_feat):
+        g = self.gate(Fn.ConcatFn.apply(rgb_feat, th_feat))
+        return g * rgb_feat + (1 - g) * th_feat

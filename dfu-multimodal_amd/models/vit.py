@@ -1,0 +1,163 @@
+"""ViT-Base/16 at 224 (timm ``vit_base_patch16_224`` semantics, timm>=0.9.2 pinned by the
+reference, requirements.txt:19; created at train_multimodal_fusion.py:299-302) on MI355X
+kernels.
+
+Attribute tree and state_dict keys are timm's (patch_embed.proj, cls_token, pos_embed,
+blocks[i].{norm1, attn.{qkv,proj}, norm2, mlp.{fc1,fc2}}, norm, fc_norm, head), with
+``global_pool='token'``, qkv_bias=True, LayerNorm eps 1e-6, exact GELU, no LayerScale and all
+drop rates 0.  Compute: fp32 residual stream, bf16 MFMA GEMMs, LDS-resident attention
+(functional.PatchEmbedFn / ViTBlockFn / TokenNormFn).
+"""
+import math
+
+import torch
+import torch.nn as tnn
+
+from dfu_hip import functional as Fn
+from dfu_hip import nn as hnn
+
+
+def _trunc_normal_(t, std=0.02):
+    # timm trunc_normal_(std=.02): N(0, std) truncated at [-2, 2] (absolute bounds)
+    tnn.init.trunc_normal_(t, mean=0.0, std=std, a=-2.0, b=2.0)
+
+
+class PatchEmbed(tnn.Module):
+    def __init__(self, img_size=224, patch_size=16, in_chans=3, embed_dim=768):
+        super().__init__()
+        self.img_size = (img_size, img_size)
+        self.patch_size = (patch_size, patch_size)
+        self.grid_size = (img_size // patch_size, img_size // patch_size)
+        self.num_patches = self.grid_size[0] * self.grid_size[1]
+        self.flatten = True
+        self.proj = tnn.Conv2d(in_chans, embed_dim, kernel_size=patch_size, stride=patch_size,
+                               bias=True)
+        self.norm = tnn.Identity()
+
+
+class Attention(tnn.Module):
+    def __init__(self, dim, num_heads=8, qkv_bias=True):
+        super().__init__()
+        assert dim % num_heads == 0
+        self.num_heads = num_heads
+        self.head_dim = dim // num_heads
+        self.scale = self.head_dim ** -0.5
+        self.fused_attn = True
+        self.qkv = hnn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.q_norm = tnn.Identity()
+        self.k_norm = tnn.Identity()
+        self.attn_drop = hnn.Dropout(0.0)
+        self.proj = hnn.Linear(dim, dim)
+        self.proj_drop = hnn.Dropout(0.0)
+
+
+class Mlp(tnn.Module):
+    def __init__(self, in_features, hidden_features):
+        super().__init__()
+        self.fc1 = hnn.Linear(in_features, hidden_features)
+        self.act = tnn.GELU()
+        self.drop1 = hnn.Dropout(0.0)
+        self.norm = tnn.Identity()
+        self.fc2 = hnn.Linear(hidden_features, in_features)
+        self.drop2 = hnn.Dropout(0.0)
+
+
+class Block(tnn.Module):
+    def __init__(self, dim, num_heads, mlp_ratio=4.0, qkv_bias=True):
+        super().__init__()
+        self.norm1 = hnn.LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, num_heads=num_heads, qkv_bias=qkv_bias)
+        self.ls1 = tnn.Identity()
+        self.drop_path1 = tnn.Identity()
+        self.norm2 = hnn.LayerNorm(dim, eps=1e-6)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+        self.ls2 = tnn.Identity()
+        self.drop_path2 = tnn.Identity()
+
+    def _params(self):
+        a, m = self.attn, self.mlp
+        return [self.norm1.weight, self.norm1.bias, a.qkv.weight, a.qkv.bias, a.proj.weight,
+                a.proj.bias, self.norm2.weight, self.norm2.bias, m.fc1.weight, m.fc1.bias,
+                m.fc2.weight, m.fc2.bias]
+
+    def forward(self, x):
+        x = Fn.ViTBlockFn.apply(x, *self._params(), self)
+        # timm calls drop_path2 last; keep a hook point for Grad-CAM's target-layer rule
+        # (grad_cam_visualization.py:389-392 picks 'blocks.11.drop_path2').
+        if self.drop_path2._forward_hooks or self.drop_path2._forward_pre_hooks:
+            x = self.drop_path2(x)
+        return x
+
+
+class VisionTransformer(tnn.Module):
+    def __init__(self, img_size=224, patch_size=16, in_chans=3, num_classes=1000,
+                 embed_dim=768, depth=12, num_heads=12, mlp_ratio=4.0, qkv_bias=True):
+        super().__init__()
+        self.num_classes = num_classes
+        self.global_pool = "token"
+        self.num_features = self.embed_dim = embed_dim
+        self.num_prefix_tokens = 1
+        self.has_class_token = True
+        self.patch_embed = PatchEmbed(img_size, patch_size, in_chans, embed_dim)
+        num_patches = self.patch_embed.num_patches
+        self.cls_token = tnn.Parameter(torch.zeros(1, 1, embed_dim))
+        self.pos_embed = tnn.Parameter(torch.randn(1, num_patches + 1, embed_dim) * 0.02)
+        self.pos_drop = hnn.Dropout(0.0)
+        self.patch_drop = tnn.Identity()
+        self.norm_pre = tnn.Identity()
+        self.blocks = tnn.Sequential(*[Block(embed_dim, num_heads, mlp_ratio, qkv_bias)
+                                      for _ in range(depth)])
+        self.norm = hnn.LayerNorm(embed_dim, eps=1e-6)
+        self.fc_norm = tnn.Identity()
+        self.head_drop = hnn.Dropout(0.0)
+        self.head = hnn.Linear(embed_dim, num_classes) if num_classes > 0 else tnn.Identity()
+        self.init_weights()
+
+    def init_weights(self):
+        # timm init_weights(mode=''): trunc_normal(.02) pos_embed, normal(1e-6) cls_token,
+        # init_weights_vit_timm on Linear (trunc_normal .02, zero bias); patch conv untouched.
+        _trunc_normal_(self.pos_embed, std=0.02)
+        tnn.init.normal_(self.cls_token, std=1e-6)
+        for m in self.modules():
+            if isinstance(m, tnn.Linear):
+                _trunc_normal_(m.weight, std=0.02)
+                if m.bias is not None:
+                    tnn.init.zeros_(m.bias)
+
+    def reset_classifier(self, num_classes):
+        self.num_classes = num_classes
+        self.head = hnn.Linear(self.embed_dim, num_classes) if num_classes > 0 else tnn.Identity()
+
+    def get_classifier(self):
+        return self.head
+
+    def _embed(self, x):
+        pe = self.patch_embed
+        return Fn.PatchEmbedFn.apply(x, pe.proj.weight, pe.proj.bias, self.cls_token,
+                                     self.pos_embed, pe.patch_size[0])
+
+    def forward_features(self, x):
+        """Tokens after the final norm, fp32 (B, 197, 768) (all rows normalised)."""
+        x = self._embed(x)
+        x = self.blocks(x)
+        return self.norm(x)
+
+    def forward_head(self, x, pre_logits=False):
+        x = x[:, 0]
+        x = self.fc_norm(x)
+        x = self.head_drop(x)
+        return x if pre_logits else self.head(x)
+
+    def forward(self, x):
+        x = self._embed(x)
+        x = self.blocks(x)
+        # final norm on the class-token rows only (== norm(x)[:, 0] for a per-token norm)
+        x = Fn.TokenNormFn.apply(x, self.norm.weight, self.norm.bias, self.norm)
+        x = self.fc_norm(x)
+        x = self.head_drop(x)
+        return self.head(x)
+
+
+def vit_base_patch16_224(num_classes=1000, **kw):
+    return VisionTransformer(img_size=224, patch_size=16, embed_dim=768, depth=12, num_heads=12,
+                             num_classes=num_classes, **kw)

@@ -137,10 +137,11 @@ int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* out, int32_t 
                       const float* mean, const float* invstd, int64_t M, int32_t C,
                       float* partial, void* stream);
 /* finalize: sums -> dgamma, dbeta (accumulated into grad buffers, may be NULL) and the
- * per-channel coefficients used by apply. */
+ * per-channel coefficients used by apply.  batch_stats = 0 for eval-mode BN (running
+ * statistics are constants: dy = gamma*invstd*g). */
 int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t M, int32_t C,
-                        const float* gamma, const float* invstd, float* dgamma, float* dbeta,
-                        float* coef, void* stream);
+                        const float* gamma, const float* invstd, int32_t batch_stats,
+                        float* dgamma, float* dbeta, float* coef, void* stream);
 /* dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); optionally dres = g (bf16). */
 int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t relu,
                      const float* mean, const float* invstd, const float* coef, int64_t M,

@@ -1,0 +1,135 @@
+"""Block-level parity on the GPU: each fused autograd Function vs the matching oracle module
+(fp32 CPU) on identical bf16-representable inputs, weights and upstream gradients."""
+import pytest
+import torch
+
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    return ((a - b).norm() / b.norm().clamp(min=1e-12)).item()
+
+
+def bfr(t):
+    """round to bf16-representable fp32"""
+    return t.to(torch.bfloat16).float()
+
+
+def _grad_report(hip_mod, ref_mod, tol, tag):
+    rp = dict(ref_mod.named_parameters())
+    bad = []
+    for n, p in hip_mod.named_parameters():
+        if rp[n].grad is None:
+            continue
+        e = rel(p.grad, rp[n].grad)
+        print(f"{tag} grad {n}: {e:.3e}")
+        if not e < tol:
+            bad.append((n, e))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("inpl,planes,stride,ds,H", [(64, 64, 1, True, 56), (256, 64, 1, False, 56),
+                                                     (256, 128, 2, True, 56), (1024, 512, 2, True, 14)])
+def test_bottleneck(inpl, planes, stride, ds, H):
+    from models.resnet import Bottleneck, conv1x1
+    from dfu_hip import nn as hnn
+    torch.manual_seed(0)
+    B = 2
+    dref = None
+    if ds:
+        dref = torch.nn.Sequential(torch.nn.Conv2d(inpl, planes * 4, 1, stride=stride, bias=False),
+                                   torch.nn.BatchNorm2d(planes * 4))
+    ref = R.Bottleneck(inpl, planes, stride, dref)
+    with torch.no_grad():
+        for m in ref.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.5, 0.5)
+            if isinstance(m, torch.nn.Conv2d):
+                m.weight.copy_(bfr(m.weight))
+    dhip = None
+    if ds:
+        dhip = torch.nn.Sequential(conv1x1(inpl, planes * 4, stride), hnn.BatchNorm2d(planes * 4))
+    hip = Bottleneck(inpl, planes, stride, dhip)
+    hip.load_state_dict(ref.state_dict())
+    hip = hip.to(DEV)
+    x = bfr(torch.randn(B, inpl, H, H))
+    xr = x.clone().requires_grad_(True)
+    R.set_bf16_emulation(True)  # compare with the bf16-rounded oracle block (same rounding)
+    try:
+        out_r = ref(xr)
+        g = bfr(torch.randn_like(out_r))
+        out_r.backward(g)
+    finally:
+        R.set_bf16_emulation(False)
+    xh = x.to(DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    out_h = hip(xh)
+    out_h.backward(g.to(DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+    torch.cuda.synchronize()
+    eo = rel(out_h, out_r)
+    ex = rel(xh.grad, xr.grad)
+    print(f"\nbottleneck {inpl},{planes},s{stride}: out {eo:.3e} dx {ex:.3e}")
+    rb = dict(ref.named_buffers())
+    for n, b in hip.named_buffers():
+        if "running" in n:
+            print(f"  buf {n}: {rel(b, rb[n]):.3e}")
+    assert eo < 2e-2 and ex < 3e-2
+    _grad_report(hip, ref, 3e-2, "  ")
+
+
+def test_stem():
+    from models.resnet import ResNet
+    torch.manual_seed(0)
+    ref = R.ResNet()
+    hip = ResNet()
+    hip.load_state_dict(ref.state_dict())
+    hip = hip.to(DEV)
+    B = 2
+    rgb, _, _ = R.synthetic_batch(B)
+    with torch.no_grad():
+        ref.conv1.weight.copy_(bfr(ref.conv1.weight))
+    hip.conv1.weight.data.copy_(ref.conv1.weight.to(DEV))
+    rgb = bfr(rgb)
+    R.set_bf16_emulation(True)
+    try:
+        a = ref.maxpool(R.rb(ref.relu(ref.bn1(R.rb(R.conv(rgb, ref.conv1.weight, 2, 3))))))
+        g = bfr(torch.randn_like(a))
+        a.backward(g)
+    finally:
+        R.set_bf16_emulation(False)
+    from dfu_hip import functional as Fn
+    ah = Fn.StemFn.apply(rgb.to(DEV), hip.conv1.weight, hip.bn1.weight, hip.bn1.bias, hip)
+    ah.backward(g.to(DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+    torch.cuda.synchronize()
+    print(f"\nstem out {rel(ah, a):.3e}")
+    for n in ["conv1.weight", "bn1.weight", "bn1.bias"]:
+        e = rel(dict(hip.named_parameters())[n].grad, dict(ref.named_parameters())[n].grad)
+        print(f"  stem grad {n}: {e:.3e}")
+        assert e < 3e-2
+    assert rel(ah, a) < 2e-2
+
+
+def test_vit_block_and_embed():
+    from models.vit import VisionTransformer
+    torch.manual_seed(0)
+    ref = R.VisionTransformer(num_classes=0, depth=2)
+    hip = VisionTransformer(num_classes=0, depth=2)
+    hip.load_state_dict(ref.state_dict())
+    hip = hip.to(DEV)
+    B = 2
+    _, th, _ = R.synthetic_batch(B)
+    th = bfr(th)
+    out_r = ref(th)
+    g = torch.randn_like(out_r)
+    out_r.backward(g)
+    out_h = hip(th.to(DEV))
+    out_h.backward(g.to(DEV))
+    torch.cuda.synchronize()
+    print(f"\nvit out {rel(out_h, out_r):.3e}")
+    assert rel(out_h, out_r) < 2e-2
+    _grad_report(hip, ref, 3e-2, "  vit")
