@@ -107,7 +107,17 @@ __global__ void k_bn_apply(const bf16_t* __restrict__ y, const float* __restrict
 
 // ---------------------------------------------------------------- backward
 // Block of 256 threads = CT column-threads (8 channels each) x (256/CT) row-lanes.
-inline int bwd_rows_per_block(int64_t M) { return M >= 65536 ? 512 : 64; }
+// Rows per block: each thread walks ~16 rows, and at most ~512 row-blocks exist, so the
+// finalize reduction over blocks stays short.
+inline int bwd_rows_per_block(int64_t M, int C) {
+  const int cv = C / 8;
+  const int ct_n = cv < 64 ? cv : 64;
+  const int rl_n = 256 / ct_n;
+  int64_t rpb = (int64_t)rl_n * 16;
+  const int64_t col_groups = cv / ct_n;
+  while ((M + rpb - 1) / rpb * col_groups > 1024 && rpb < M) rpb *= 2;
+  return (int)rpb;
+}
 
 __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ y,
                                 const bf16_t* __restrict__ out, int relu,
@@ -161,17 +171,27 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
   }
 }
 
+// 32 block-lanes x 8 channels per workgroup; fp64 sums.
 __global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int blocks, int64_t M, int C,
                                   const float* __restrict__ gamma,
                                   const float* __restrict__ invstd, int batch_stats,
                                   float* __restrict__ dgamma, float* __restrict__ dbeta,
                                   float* __restrict__ coef) {
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    double sg = 0.0, sgx = 0.0;
-    for (int b = 0; b < blocks; ++b) {
+  __shared__ double red[2][32][8];
+  const int cl = threadIdx.x & 7, bl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  double sg = 0.0, sgx = 0.0;
+  if (c < C) {
+    for (int b = bl; b < blocks; b += 32) {
       sg += partial[((int64_t)b * 2 + 0) * C + c];
       sgx += partial[((int64_t)b * 2 + 1) * C + c];
     }
+  }
+  red[0][bl][cl] = sg;
+  red[1][bl][cl] = sgx;
+  __syncthreads();
+  if (bl == 0 && c < C) {
+    for (int l = 1; l < 32; ++l) { sg += red[0][l][cl]; sgx += red[1][l][cl]; }
     if (dbeta) dbeta[c] += (float)sg;
     if (dgamma) dgamma[c] += (float)sgx;
     const float g = gamma ? gamma[c] : 1.f;
@@ -257,8 +277,8 @@ extern "C" int dfu_bn_apply(const void* y, const float* scale, const float* shif
   return DFU_OK;
 }
 
-extern "C" int dfu_bn_bwd_blocks(int64_t M) {
-  const int rpb = bwd_rows_per_block(M);
+extern "C" int dfu_bn_bwd_blocks(int64_t M, int32_t C) {
+  const int rpb = bwd_rows_per_block(M, C);
   return (int)((M + rpb - 1) / rpb);
 }
 
@@ -271,8 +291,8 @@ extern "C" int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* ou
   const int cv = C / 8;
   const int ct_n = cv < 64 ? cv : 64;
   DFU_CHECK_ARG(256 % ct_n == 0 && cv % ct_n == 0, "dfu_bn_bwd_reduce: C=%d unsupported", C);
-  const int rpb = bwd_rows_per_block(M);
-  dim3 grid(cv / ct_n, dfu_bn_bwd_blocks(M));
+  const int rpb = bwd_rows_per_block(M, C);
+  dim3 grid(cv / ct_n, dfu_bn_bwd_blocks(M, C));
   hipLaunchKernelGGL(k_bn_bwd_reduce, grid, dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, relu, mean, invstd,
                      M, C, rpb, partial);
@@ -284,7 +304,7 @@ extern "C" int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t
                                    const float* gamma, const float* invstd, int32_t batch_stats,
                                    float* dgamma, float* dbeta, float* coef, void* stream) {
   DFU_CHECK_ARG(partial && invstd && coef && blocks > 0 && C > 0, "dfu_bn_bwd_finalize: bad args");
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 7) / 8), dim3(256), 0, (hipStream_t)stream,
                      partial, blocks, M, C, gamma, invstd, batch_stats, dgamma, dbeta, coef);
   DFU_LAUNCH_CHECK();
   return DFU_OK;

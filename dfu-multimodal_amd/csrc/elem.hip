@@ -29,6 +29,22 @@ __global__ void k_pack_conv_weight(const float* __restrict__ w, bf16_t* __restri
   }
 }
 
+// oihw[k][c][r][s] += krsc[k][r][s][c]; one thread per OIHW element (coalesced writes).
+__global__ void k_conv_grad_krsc_to_oihw(const float* __restrict__ krsc, float* __restrict__ oihw,
+                                         int K, int C, int R, int S) {
+  const int64_t n = (int64_t)K * C * R * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int s = (int)(i % S);
+    int64_t t = i / S;
+    const int r = (int)(t % R);
+    t /= R;
+    const int c = (int)(t % C);
+    const int k = (int)(t / C);
+    oihw[i] += krsc[(((int64_t)k * R + r) * S + s) * C + c];
+  }
+}
+
 __global__ void k_cast_rows_bf16(const float* __restrict__ in, int64_t ld_in,
                                  bf16_t* __restrict__ out, int64_t ld_out, int rows, int cols) {
   const int64_t n = (int64_t)rows * ld_out;
@@ -275,16 +291,22 @@ __global__ void k_colsum(const void* __restrict__ xv, int64_t ld, int rows, int 
   }
 }
 
-// out_v[d] += sum_b partial[b][v][d]
+// out_v[d] += sum_b partial[b][v][d]; 32 block-lanes x 8 columns per workgroup.
 __global__ void k_reduce_partials(const float* __restrict__ partial, int blocks, int nvec, int D,
                                   float* __restrict__ out0, float* __restrict__ out1) {
-  const int64_t n = (int64_t)nvec * D;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  __shared__ float red[32][8];
+  const int cl = threadIdx.x & 7, bl = threadIdx.x >> 3;
+  const int64_t i = (int64_t)blockIdx.x * 8 + cl;  // flattened (v, d)
+  const bool ok = i < (int64_t)nvec * D;
+  float s = 0.f;
+  if (ok)
+    for (int b = bl; b < blocks; b += 32) s += partial[(int64_t)b * nvec * D + i];
+  red[bl][cl] = s;
+  __syncthreads();
+  if (bl == 0 && ok) {
+    for (int l = 1; l < 32; ++l) s += red[l][cl];
     const int v = (int)(i / D);
     const int d = (int)(i - (int64_t)v * D);
-    float s = 0.f;
-    for (int b = 0; b < blocks; ++b) s += partial[((int64_t)b * nvec + v) * D + d];
     float* o = v == 0 ? out0 : out1;
     if (o) o[d] += s;
   }
@@ -493,6 +515,13 @@ extern "C" int dfu_pack_conv_weight(const float* w, void* out, int32_t K, int32_
   return DFU_OK;
 }
 
+extern "C" int dfu_conv_grad_krsc_to_oihw(const float* krsc, float* oihw, int32_t K, int32_t C,
+                                          int32_t R, int32_t S, void* stream) {
+  DFU_CHECK_ARG(krsc && oihw && K > 0 && C > 0 && R > 0 && S > 0, "dfu_conv_grad_krsc_to_oihw: bad args");
+  LAUNCH(k_conv_grad_krsc_to_oihw, (int64_t)K * C * R * S, stream, krsc, oihw, K, C, R, S);
+  return DFU_OK;
+}
+
 extern "C" int dfu_cast_rows_bf16(const float* in, int64_t ld_in, void* out, int64_t ld_out,
                                   int32_t rows, int32_t cols, void* stream) {
   DFU_CHECK_ARG(in && out && rows > 0 && cols > 0 && ld_out >= cols && ld_in >= cols,
@@ -576,14 +605,18 @@ extern "C" int dfu_colsum(const void* x, int32_t is_bf16, int64_t ld, int32_t ro
   else
     hipLaunchKernelGGL(k_colsum<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, rows, N, partial);
   DFU_LAUNCH_CHECK();
-  LAUNCH(k_reduce_partials, (int64_t)N, stream, partial, blocks, 1, N, out, (float*)nullptr);
+  hipLaunchKernelGGL(k_reduce_partials, dim3((N + 7) / 8), dim3(256), 0, (hipStream_t)stream,
+                     partial, blocks, 1, N, out, (float*)nullptr);
+  DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
 
 extern "C" int dfu_reduce_partials(const float* partial, int32_t blocks, int32_t nvec, int32_t D,
                                    float* out0, float* out1, void* stream) {
   DFU_CHECK_ARG(partial && blocks > 0 && nvec >= 1 && nvec <= 2 && D > 0, "dfu_reduce_partials: bad args");
-  LAUNCH(k_reduce_partials, (int64_t)nvec * D, stream, partial, blocks, nvec, D, out0, out1);
+  hipLaunchKernelGGL(k_reduce_partials, dim3((unsigned)(((int64_t)nvec * D + 7) / 8)), dim3(256), 0,
+                     (hipStream_t)stream, partial, blocks, nvec, D, out0, out1);
+  DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
 

@@ -1,54 +1,116 @@
-// Host dispatch for the MFMA GEMM template (include/dfu_hip.h: dfu_gemm).
-// Only the (A mode, B mode, epilogue) combinations the training step uses are instantiated.
-#include "gemm_kernel.h"
+// Host dispatch for the MFMA GEMM template (include/dfu_hip.h: dfu_gemm): picks the tile
+// shape and split-K by a wave-quantisation cost model (one 512-thread workgroup per CU),
+// launches the kernel, and for split-K with a caller workspace reduces the fp32 slabs.
+#include <math.h>
+
+#include "gemm_table.h"
 
 using namespace dfu;
 
 namespace {
 
-typedef void (*gemm_fn)(const GemmArgs);
+constexpr int kCUs = 256;
+constexpr int kTM[NTILES] = {128, 256, 128, 256};
+constexpr int kTN[NTILES] = {128, 128, 256, 256};
+// Relative MFMA throughput per tile area (measured on MI355X, tools/gemm_bench.py).
+constexpr double kEff[NTILES] = {1.0, 1.25, 1.25, 1.45};
+constexpr double kStepUs = 0.55;        // one 128x128x64 K-step at kEff = 1
+constexpr double kRoundOverheadUs = 3.0;  // prologue fill + epilogue per workgroup round
+constexpr double kSlabGBs = 4500.0;      // fp32 slab write + reduce read rate
 
-template <int A, int B, int E>
-constexpr gemm_fn K() {
-  return &gemm_kernel<A, B, E>;
+const Entry* find_entry(int a, int b, int e, int tile) {
+  const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256};
+  const int ns[NTILES] = {kTable128x128N, kTable256x128N, kTable128x256N, kTable256x256N};
+  for (int i = 0; i < ns[tile]; ++i) {
+    const Entry& en = tabs[tile][i];
+    if (en.a == a && en.b == b && en.e == e) return &en;
+  }
+  return nullptr;
 }
 
-struct Entry {
-  int a, b, e;
-  gemm_fn fn;
-};
-
-#define E3(a, b, e) {a, b, e, K<a, b, e>()}
-const Entry kTable[] = {
-    // Linear forward: Y = X W^T (+ epilogue)         (timm qkv/proj/fc1/fc2, patch-embed, head)
-    E3(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
-    E3(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_RELU),
-    E3(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_GELU),
-    E3(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32),
-    E3(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_RESID),
-    E3(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_PATCH),
-    // 1x1/s1 conv and the stem (explicit im2col) forward with BN statistics
-    E3(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_STATS),
-    // Linear / 1x1 conv dgrad: dX = dY W
-    E3(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16),
-    E3(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_DGELU),
-    E3(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_ADD),
-    E3(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_F32),
-    // Linear / 1x1 conv wgrad: dW += dY^T X
-    E3(DFU_OPND_MNMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_F32_ACC),
-    // implicit-GEMM conv (3x3, strided 1x1)
-    E3(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_BF16_STATS),
-    E3(DFU_OPND_CONV_DGRAD, DFU_OPND_CONV_DGRAD_W, DFU_EPI_BF16),
-    E3(DFU_OPND_CONV_DGRAD, DFU_OPND_CONV_DGRAD_W, DFU_EPI_BF16_ADD),
-    E3(DFU_OPND_MNMAJOR, DFU_OPND_CONV_WGRAD_X, DFU_EPI_F32_ACC_CONVW),
-};
-#undef E3
-
 inline int round8(int x) { return (x + 7) & ~7; }
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+struct Plan {
+  const Entry* entry = nullptr;
+  int tile = 0, split = 1;
+  double cost = 1e30;
+};
+
+Plan plan_gemm(const dfu_gemm_desc* d) {
+  const bool acc_epi = d->epilogue == DFU_EPI_F32_ACC;
+  const int ktiles = cdiv(d->K, BK);
+  Plan best;
+  for (int t = 0; t < NTILES; ++t) {
+    if (d->tile > 0 && d->tile - 1 != t) continue;
+    const Entry* en = find_entry(d->a_mode, d->b_mode, d->epilogue, t);
+    if (!en) continue;
+    const int tiles = cdiv(d->M, kTM[t]) * cdiv(d->N, kTN[t]);
+    int s_lo = 1, s_hi = 1;
+    if (acc_epi) {
+      if (d->split_k > 0) s_lo = s_hi = d->split_k;
+      else s_hi = ktiles < 32 ? ktiles : 32;
+    }
+    for (int s = s_lo; s <= s_hi; ++s) {
+      const int kps = cdiv(ktiles, s);
+      const int se = cdiv(ktiles, kps);
+      if (se != s && s != s_lo) continue;
+      const int rounds = cdiv(tiles * se, kCUs);
+      double cost = rounds * (kps * kStepUs * (kTM[t] * kTN[t]) / (128.0 * 128.0) / kEff[t] +
+                              kRoundOverheadUs);
+      if (se > 1) cost += 8.0 * se * (double)d->M * d->N / (kSlabGBs * 1e3);
+      if (cost < best.cost) {
+        best.cost = cost;
+        best.entry = en;
+        best.tile = t;
+        best.split = se;
+      }
+    }
+  }
+  return best;
+}
+
+__global__ void k_splitk_reduce(const float* __restrict__ slab, int splits, int M, int N,
+                                float* __restrict__ C, int64_t ldc) {
+  const int64_t n4 = (int64_t)M * N / 4;
+  const int64_t plane = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 s = ((const f32x4*)slab)[i];
+    for (int k = 1; k < splits; ++k) {
+      const f32x4 v = *(const f32x4*)(slab + k * plane + 4 * i);
+      s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
+    }
+    const int64_t e = 4 * i;
+    const int64_t m = e / N;
+    const int n = (int)(e - m * N);
+    float* c = C + m * ldc + n;  // N % 4 == 0, ldc % 4 == 0, C 16-B aligned (host-checked)
+    f32x4 cv = *(f32x4*)c;
+    *(f32x4*)c = (f32x4){cv[0] + s[0], cv[1] + s[1], cv[2] + s[2], cv[3] + s[3]};
+  }
+}
+
+__global__ void k_splitk_reduce_scalar(const float* __restrict__ slab, int splits, int M, int N,
+                                       float* __restrict__ C, int64_t ldc) {
+  const int64_t n = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += slab[k * n + i];
+    const int64_t m = i / N;
+    C[m * ldc + (i - m * N)] += s;
+  }
+}
 
 }  // namespace
 
-extern "C" int dfu_gemm_stats_tiles(int32_t M) { return (M + BM - 1) / BM; }
+extern "C" int dfu_gemm_stats_tiles(int32_t M) { return (M + 127) / 128; }
+
+extern "C" int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* d) {
+  if (!d || d->epilogue != DFU_EPI_F32_ACC) return 0;
+  const Plan pl = plan_gemm(d);
+  return pl.entry && pl.split > 1 ? (int64_t)pl.split * d->M * d->N * 4 : 0;
+}
 
 extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
   DFU_CHECK_ARG(d != nullptr, "dfu_gemm: null descriptor");
@@ -59,20 +121,18 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
   const bool b_kc = d->b_mode == DFU_OPND_KMAJOR;
   DFU_CHECK_ARG(!(a_kc || b_kc) || d->K % 8 == 0,
                 "dfu_gemm: K=%d must be a multiple of 8 for K-contiguous operands", d->K);
-  gemm_fn fn = nullptr;
-  for (const Entry& e : kTable)
-    if (e.a == d->a_mode && e.b == d->b_mode && e.e == d->epilogue) fn = e.fn;
-  if (!fn) {
-    dfu_set_error("dfu_gemm: unsupported combination a_mode=%d b_mode=%d epilogue=%d",
-                  d->a_mode, d->b_mode, d->epilogue);
+  DFU_CHECK_ARG(d->tile >= 0 && d->tile <= NTILES, "dfu_gemm: bad tile hint %d", d->tile);
+  const bool acc_epi = d->epilogue == DFU_EPI_F32_ACC;
+  DFU_CHECK_ARG(d->split_k >= 0, "dfu_gemm: split_k must be >= 0 (0 = auto)");
+  DFU_CHECK_ARG(d->split_k <= 1 || acc_epi, "dfu_gemm: split_k > 1 needs the F32_ACC epilogue");
+  const Plan pl = plan_gemm(d);
+  if (!pl.entry) {
+    dfu_set_error("dfu_gemm: unsupported combination a_mode=%d b_mode=%d epilogue=%d tile=%d",
+                  d->a_mode, d->b_mode, d->epilogue, d->tile);
     return DFU_E_UNSUPPORTED;
   }
-  const bool acc_epi = d->epilogue == DFU_EPI_F32_ACC || d->epilogue == DFU_EPI_F32_ACC_CONVW;
-  DFU_CHECK_ARG(d->split_k >= 1, "dfu_gemm: split_k must be >= 1");
-  DFU_CHECK_ARG(d->split_k == 1 || acc_epi, "dfu_gemm: split_k > 1 needs an F32_ACC epilogue");
   DFU_CHECK_ARG(((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0,
                 "dfu_gemm: A and B must be 16-byte aligned");
-  // leading dims must keep every 16-B vector aligned
   if (d->a_mode == DFU_OPND_KMAJOR || d->a_mode == DFU_OPND_MNMAJOR)
     DFU_CHECK_ARG(d->lda % 8 == 0, "dfu_gemm: lda=%lld must be a multiple of 8", (long long)d->lda);
   if (d->b_mode == DFU_OPND_KMAJOR || d->b_mode == DFU_OPND_MNMAJOR)
@@ -85,12 +145,13 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
     DFU_CHECK_ARG(d->stats != nullptr, "dfu_gemm: STATS epilogue needs a stats slab");
 
   GemmArgs a;
+  const int TM = kTM[pl.tile], TN = kTN[pl.tile];
   a.M = d->M; a.N = d->N; a.K = d->K;
-  a.ktiles = (d->K + BK - 1) / BK;
-  a.kt_per_split = (a.ktiles + d->split_k - 1) / d->split_k;
-  const int splits = (a.ktiles + a.kt_per_split - 1) / a.kt_per_split;
-  a.tiles_m = (d->M + BM - 1) / BM;
-  a.tiles_n = (d->N + BN - 1) / BN;
+  a.ktiles = cdiv(d->K, BK);
+  a.kt_per_split = cdiv(a.ktiles, pl.split);
+  const int splits = cdiv(a.ktiles, a.kt_per_split);
+  a.tiles_m = cdiv(d->M, TM);
+  a.tiles_n = cdiv(d->N, TN);
   a.A = (const bf16_t*)d->A; a.lda = d->lda;
   a.B = (const bf16_t*)d->B; a.ldb = d->ldb;
   a.C = d->C; a.ldc = d->ldc;
@@ -100,14 +161,17 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
   a.aux_out = d->aux_out; a.ldaux_out = d->ldaux_out;
   a.stats = d->stats;
   a.split = splits;
+  a.slab = nullptr;
+  if (acc_epi && splits > 1 && d->workspace != nullptr &&
+      d->workspace_bytes >= (int64_t)splits * d->M * d->N * 4)
+    a.slab = (float*)d->workspace;
   a.ep_tokens = d->ep_tokens;
   a.cn = d->conv_n; a.ch = d->conv_h; a.cw = d->conv_w; a.cc = d->conv_c;
   a.ck = d->conv_k; a.cr = d->conv_r; a.cs = d->conv_s;
   a.cstride = d->conv_stride; a.cpad = d->conv_pad; a.cp = d->conv_p; a.cq = d->conv_q;
   a.m_ld_bound = round8(d->M);
   a.n_ld_bound = round8(d->N);
-  const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD ||
-                    d->epilogue == DFU_EPI_F32_ACC_CONVW;
+  const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
   if (conv) {
     DFU_CHECK_ARG(d->conv_n > 0 && d->conv_h > 0 && d->conv_w > 0 && d->conv_c > 0 &&
                       d->conv_k > 0 && d->conv_r > 0 && d->conv_s > 0 && d->conv_stride > 0 &&
@@ -138,8 +202,22 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
       a.n_ld_bound = d->N;
     }
   }
+  hipStream_t s = (hipStream_t)stream;
   dim3 grid(a.tiles_m * a.tiles_n, splits);
-  hipLaunchKernelGGL(fn, grid, dim3(NT), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(pl.entry->fn, grid, dim3(NT), 0, s, a);
   DFU_LAUNCH_CHECK();
+  if (a.slab != nullptr) {
+    const int64_t n = (int64_t)d->M * d->N;
+    const bool vec = d->N % 4 == 0 && d->ldc % 4 == 0 && ((uintptr_t)d->C & 15) == 0;
+    int64_t blocks = (vec ? n / 4 : n) / 256 + 1;
+    if (blocks > 8192) blocks = 8192;
+    if (vec)
+      hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, a.slab, splits,
+                         d->M, d->N, (float*)d->C, d->ldc);
+    else
+      hipLaunchKernelGGL(k_splitk_reduce_scalar, dim3((unsigned)blocks), dim3(256), 0, s, a.slab,
+                         splits, d->M, d->N, (float*)d->C, d->ldc);
+    DFU_LAUNCH_CHECK();
+  }
   return DFU_OK;
 }

@@ -1,15 +1,16 @@
 // bf16 MFMA GEMM template for gfx950 with implicit-GEMM convolution loaders and fused
 // epilogues.  One kernel body serves every contraction of the DFU training step
-// (SURVEY.md §2.2): ViT Linear fwd/dgrad/wgrad, NHWC conv fwd/dgrad/wgrad, fusion head.
+// (SURVEY.md §2.2): ViT Linear fwd/dgrad/wgrad, NHWC conv fwd/dgrad/wgrad, patch-embed.
 //
-// Geometry: 256 threads = 4 waves (2 x 2), block tile 128 x 128, K-step 64, each wave owns a
-// 64 x 64 sub-tile = 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators (fp32).
-// Operands are staged global -> registers -> LDS (two LDS stages, one barrier per K-step):
-// the register stage is what lets one loader serve plain, transposed and gathered (im2col)
-// operands.  Two LDS images:
-//   K-contiguous  [128 rows][64 k]  128-B rows, 16-B chunk index ^= (row & 7)  -> ds_read_b128
-//   MN-contiguous [64 k][128 cols]  256-B rows, 16-B chunk index ^= f(k)       -> ds_read_b64_tr_b16
-// both conflict-free for their reads and for the 16-B register-staged writes.
+// Geometry: 512 threads = 8 waves (2 per SIMD), one workgroup per CU, output tile TM x TN
+// (128x128, 256x128, 128x256 or 256x256), K-step 64, v_mfma_f32_16x16x32_bf16 with fp32
+// accumulators.  Operands move global -> LDS by LDS-DMA (global_load_lds_dwordx4) into an
+// NSTAGE-deep ring (3 stages when they fit in 160 KiB, else 2), tracked by counted vmcnt and
+// published with a raw s_barrier — no VGPR staging, so gathered (im2col) and transposed
+// operands cost no registers.  Two LDS images:
+//   K-contiguous  [rows][64 k]         128-B rows, 16-B chunk ^= (row & 7)   -> ds_read_b128
+//   MN-contiguous [64 k][128 cols] x n 256-B rows, 16-B chunk ^= f(k)        -> ds_read_b64_tr_b16
+// both conflict-free; the swizzle is applied on the DMA SOURCE (the LDS write is lane-linear).
 // The MFMA is issued with the operands swapped (B fragment as "A"), so each lane ends with 4
 // consecutive output COLUMNS of one row: 8-B (bf16) / 16-B (fp32) epilogue stores.
 #pragma once
@@ -17,10 +18,23 @@
 
 namespace dfu {
 
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE_BYTES = 128 * 64 * 2;  // 16 KiB per operand tile
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;  // 64 KiB -> 2 workgroups per CU
+constexpr int BK = 64, NT = 512, NWAVE = 8;
+constexpr int LDS_MAX = 160 * 1024;
+
+template <int TM_, int TN_>
+struct Tile {
+  static constexpr int TM = TM_, TN = TN_;
+  static constexpr int WGM = (TM == 256 && TN == 128) ? 4 : 2;  // wave grid
+  static constexpr int WGN = NWAVE / WGM;
+  static constexpr int WTM = TM / WGM, WTN = TN / WGN;         // per-wave sub-tile
+  static constexpr int FM = WTM / 16, FN = WTN / 16;           // MFMA accumulators per wave
+  static constexpr int NLDA = TM / 64, NLDB = TN / 64;         // DMA instructions per thread
+  static constexpr int A_BYTES = TM * BK * 2, B_BYTES = TN * BK * 2;
+  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int NSTAGE = 3 * STAGE_BYTES <= LDS_MAX ? 3 : 2;
+  static constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES;
+  static constexpr int DMA_PER_STAGE = NLDA + NLDB;
+};
 
 struct GemmArgs {
   int M, N, K;
@@ -39,12 +53,13 @@ struct GemmArgs {
   void* aux_out;
   int64_t ldaux_out;
   float* stats;
+  float* slab;  // split-K partial slabs [split][M][N] (F32_ACC with a workspace)
   int split;
   int ep_tokens;
   // conv geometry
   int cn, ch, cw, cc, ck, cr, cs, cstride, cpad, cp, cq;
   FastDiv div_pq, div_q, div_hw, div_w, div_c, div_k, div_s;
-  int m_ld_bound;  // rows of MN-contiguous operands may be read up to this column bound
+  int m_ld_bound;  // MN-contiguous operands may be read up to this column bound
   int n_ld_bound;
 };
 
@@ -53,41 +68,56 @@ DFU_DEV int kc_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7))
 DFU_DEV int mn_swz(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
 DFU_DEV int mn_off(int krow, int chunk) { return krow * 256 + ((chunk ^ mn_swz(krow)) << 4); }
 
-DFU_DEV bool is_kcontig(int mode) {
-  return mode == DFU_OPND_KMAJOR || mode == DFU_OPND_CONV_FWD || mode == DFU_OPND_CONV_DGRAD;
+template <int MODE>
+constexpr bool kcontig() {
+  return MODE == DFU_OPND_KMAJOR || MODE == DFU_OPND_CONV_FWD || MODE == DFU_OPND_CONV_DGRAD;
 }
 
 // ------------------------------------------------------------------------------ loaders
-// Each thread moves 4 x 16 B per operand per K-step.
-struct Stage {
-  u32x4 v[4];
-};
+// One DMA wave-instruction writes 1 KiB of LDS at a wave-uniform base, lane l at base+16*l.
+// Instruction i of wave w lands at byte 1024*(w + 8*i) of the operand tile.
+//   K-contiguous tile: that is rows 8*(w+8i) .. +7, i.e. thread row (tid>>3) + 64*i, and the
+//     lane at LDS slot (lane&7) of its row fetches chunk (lane&7) ^ (row&7) = kc_lane_chunk.
+//   MN-contiguous tile (128-column sub-images of 16 KiB): 1-KiB piece q = w + 8*i is k-rows
+//     4*(q&15) .. +3 of sub-image q>>4, i.e. k-row (tid>>4) + 32*(i&1), columns
+//     128*(i>>1) + 8*chunk with chunk = (lane&15) ^ f(k-row) (same f for every i).
+// Out-of-range lanes fetch 16 zero bytes from g_zero16.
+__device__ __attribute__((aligned(16))) const uint32_t g_zero16[4] = {0u, 0u, 0u, 0u};
 
-// Per-thread precomputed state for one operand (rows fixed across the K loop).
+DFU_DEV int kc_lane_chunk(int lane) { return (lane & 7) ^ ((lane >> 3) & 7); }
+DFU_DEV int mn_lane_chunk(int tid) { return (tid & 15) ^ mn_swz(tid >> 4); }
+
+template <int NLD>
 struct LoadState {
-  const bf16_t* ptr[4];  // row base pointers (KMAJOR) / unused
-  int i0[4], i1[4];      // conv: ih0/iw0 (fwd) or h/w (dgrad) per row; wgrad: r,s per chunk
-  int valid[4];
-  int bofs[4];           // conv: batch offset index
-  int col;               // MN-contiguous: column (mn) of this thread's chunk
-  int c_in;              // wgrad: channel of this thread's chunk
+  const bf16_t* ptr[NLD];  // KMAJOR: row pointer incl. the swizzled chunk offset
+  int i0[NLD], i1[NLD];    // conv: ih0/iw0 (fwd) or h+pad/w+pad (dgrad); wgrad: r, s per sub
+  int valid[NLD];
+  int bofs[NLD];           // conv: batch index
+  int cin[NLD];            // wgrad: channel per sub-image
+  int kc;                  // K-contiguous: element offset of this lane's (swizzled) chunk
+  int col;                 // MN-contiguous: first column (sub-image 0) of this lane's chunk
 };
 
-template <int MODE>
-DFU_DEV void load_init(const GemmArgs& p, LoadState& st, const bf16_t* base, int64_t ld, int mn0,
-                       int MN, int tid) {
+template <int MODE, int NLD>
+DFU_DEV void load_init(const GemmArgs& p, LoadState<NLD>& st, const bf16_t* base, int64_t ld,
+                       int mn0, int MN, int tid) {
+  const int lane = tid & 63;
+  if constexpr (kcontig<MODE>()) {
+    st.kc = kc_lane_chunk(lane) * 8;
+  } else {
+    st.col = mn0 + mn_lane_chunk(tid) * 8;
+  }
   if constexpr (MODE == DFU_OPND_KMAJOR) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = mn0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < NLD; ++i) {
+      const int row = mn0 + (tid >> 3) + 64 * i;
       st.valid[i] = row < MN;
-      st.ptr[i] = base + (int64_t)(st.valid[i] ? row : 0) * ld + (tid & 7) * 8;
+      st.ptr[i] = base + (int64_t)(st.valid[i] ? row : 0) * ld + st.kc;
     }
   } else if constexpr (MODE == DFU_OPND_CONV_FWD) {
-    // rows = output positions m = (b, oh, ow)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = mn0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < NLD; ++i) {  // rows = output positions (b, oh, ow)
+      const int m = mn0 + (tid >> 3) + 64 * i;
       st.valid[i] = m < MN;
       const uint32_t mm = st.valid[i] ? m : 0;
       const uint32_t b = fdiv(mm, p.div_pq);
@@ -99,10 +129,9 @@ DFU_DEV void load_init(const GemmArgs& p, LoadState& st, const bf16_t* base, int
       st.bofs[i] = (int)b;
     }
   } else if constexpr (MODE == DFU_OPND_CONV_DGRAD) {
-    // rows = input positions m = (b, h, w) of dX
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = mn0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < NLD; ++i) {  // rows = input positions (b, h, w) of dX
+      const int m = mn0 + (tid >> 3) + 64 * i;
       st.valid[i] = m < MN;
       const uint32_t mm = st.valid[i] ? m : 0;
       const uint32_t b = fdiv(mm, p.div_hw);
@@ -113,54 +142,64 @@ DFU_DEV void load_init(const GemmArgs& p, LoadState& st, const bf16_t* base, int
       st.i1[i] = (int)w + p.cpad;
       st.bofs[i] = (int)b;
     }
-  } else if constexpr (MODE == DFU_OPND_MNMAJOR || MODE == DFU_OPND_CONV_DGRAD_W) {
-    st.col = mn0 + (tid & 15) * 8;
   } else if constexpr (MODE == DFU_OPND_CONV_WGRAD_X) {
-    st.col = mn0 + (tid & 15) * 8;  // n' = (r, s, c)
-    const uint32_t n = st.col;
-    const uint32_t rs = fdiv(n, p.div_c);
-    st.c_in = (int)(n - rs * p.cc);
-    const uint32_t r = fdiv(rs, p.div_s);
-    st.i0[0] = (int)r;
-    st.i1[0] = (int)(rs - r * p.cs);
+    constexpr int NSUB = NLD >= 2 ? NLD / 2 : 1;
+#pragma unroll
+    for (int sub = 0; sub < NSUB; ++sub) {  // n' = (r, s, c) per sub-image
+      const uint32_t n = st.col + 128 * sub;
+      const uint32_t rs = fdiv(n, p.div_c);
+      st.cin[sub] = (int)(n - rs * p.cc);
+      const uint32_t r = fdiv(rs, p.div_s);
+      st.i0[sub] = (int)r;
+      st.i1[sub] = (int)(rs - r * p.cs);
+    }
   }
 }
 
-// Global -> registers for K-step kt.  MN is the extent of the operand's row/col dimension.
-template <int MODE>
-DFU_DEV void load_tile(const GemmArgs& p, const LoadState& st, const bf16_t* base, int64_t ld,
-                       int MN_bound, int kt, int kend, int tid, Stage& s) {
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void glb_void;
+
+DFU_DEV void glds16(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, 0);
+}
+
+// Issue this thread's NLD LDS-DMA instructions for K-step kt into `tile`.
+template <int MODE, int NLD>
+DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_t* base,
+                        int64_t ld, int MN_bound, int kt, int kend, int tid, char* tile) {
   const int k0 = kt * BK;
-  const u32x4 z = {0u, 0u, 0u, 0u};
+  char* dst = tile + 1024 * (tid >> 6);
+  const void* zero = (const void*)g_zero16;
   if constexpr (MODE == DFU_OPND_KMAJOR) {
-    const int k = k0 + (tid & 7) * 8;
-    const bool kin = k < kend;
+    const bool kin = k0 + st.kc < kend;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      s.v[i] = (st.valid[i] && kin) ? *(const u32x4*)(st.ptr[i] + k0) : z;
+    for (int i = 0; i < NLD; ++i) {
+      const bool ok = st.valid[i] && kin;
+      glds16(ok ? (const void*)(st.ptr[i] + k0) : zero, dst + 8192 * i);
+    }
   } else if constexpr (MODE == DFU_OPND_CONV_FWD) {
     // whole K-step lies in one filter tap (C % 64 == 0, host-checked)
     const uint32_t rs = fdiv((uint32_t)k0, p.div_c);
-    const int c0 = k0 - (int)rs * p.cc + (tid & 7) * 8;
+    const int c0 = k0 - (int)rs * p.cc + st.kc;
     const uint32_t r = fdiv(rs, p.div_s);
     const int sx = (int)(rs - r * p.cs);
     const bool kin = k0 < kend;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NLD; ++i) {
       const int ih = st.i0[i] + (int)r, iw = st.i1[i] + sx;
       const bool ok = kin && st.valid[i] && (unsigned)ih < (unsigned)p.ch && (unsigned)iw < (unsigned)p.cw;
       const int64_t off = (((int64_t)st.bofs[i] * p.ch + ih) * p.cw + iw) * p.cc + c0;
-      s.v[i] = ok ? *(const u32x4*)(base + off) : z;
+      glds16(ok ? (const void*)(base + off) : zero, dst + 8192 * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_DGRAD) {
     // K' = (r, s, kout); gather dY[b][(h+pad-r)/st][(w+pad-s)/st][kout]
     const uint32_t rs = fdiv((uint32_t)k0, p.div_k);
-    const int k_0 = k0 - (int)rs * p.ck + (tid & 7) * 8;
+    const int k_0 = k0 - (int)rs * p.ck + st.kc;
     const uint32_t r = fdiv(rs, p.div_s);
     const int sx = (int)(rs - r * p.cs);
     const bool kin = k0 < kend;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NLD; ++i) {
       const int hn = st.i0[i] - (int)r, wn = st.i1[i] - sx;
       bool ok = kin && st.valid[i] && hn >= 0 && wn >= 0;
       int oh = hn, ow = wn;
@@ -171,57 +210,46 @@ DFU_DEV void load_tile(const GemmArgs& p, const LoadState& st, const bf16_t* bas
       }
       ok = ok && oh < p.cp && ow < p.cq;
       const int64_t off = (((int64_t)st.bofs[i] * p.cp + oh) * p.cq + ow) * p.ck + k_0;
-      s.v[i] = ok ? *(const u32x4*)(base + off) : z;
+      glds16(ok ? (const void*)(base + off) : zero, dst + 8192 * i);
     }
   } else if constexpr (MODE == DFU_OPND_MNMAJOR) {
-    const bool cin = st.col < MN_bound;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = k0 + (tid >> 4) + 16 * i;
-      s.v[i] = (cin && k < kend) ? *(const u32x4*)(base + (int64_t)k * ld + st.col) : z;
+    for (int i = 0; i < NLD; ++i) {
+      const int k = k0 + (tid >> 4) + 32 * (i & 1);
+      const int col = st.col + 128 * (i >> 1);
+      const bool ok = col < MN_bound && k < kend;
+      glds16(ok ? (const void*)(base + (int64_t)k * ld + col) : zero, dst + 8192 * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_DGRAD_W) {
     // B[k'=(r,s,kout)][c] = Wkrsc[kout][r][s][c];  ld = R*S*C
     const uint32_t rs = fdiv((uint32_t)k0, p.div_k);
     const int kout0 = k0 - (int)rs * p.ck;
-    const bool cin = st.col < MN_bound && k0 < kend;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kout = kout0 + (tid >> 4) + 16 * i;
-      s.v[i] = cin ? *(const u32x4*)(base + (int64_t)kout * ld + (int64_t)rs * p.cc + st.col) : z;
+    for (int i = 0; i < NLD; ++i) {
+      const int kout = kout0 + (tid >> 4) + 32 * (i & 1);
+      const int col = st.col + 128 * (i >> 1);
+      const bool ok = col < MN_bound && k0 < kend;
+      glds16(ok ? (const void*)(base + (int64_t)kout * ld + (int64_t)rs * p.cc + col) : zero,
+             dst + 8192 * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_WGRAD_X) {
     // B[k'=m (b,oh,ow)][n'=(r,s,c)] = X[b][oh*st-pad+r][ow*st-pad+s][c]
-    const bool cin = st.col < MN_bound;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = k0 + (tid >> 4) + 16 * i;
-      bool ok = cin && m < kend;
+    for (int i = 0; i < NLD; ++i) {
+      const int sub = i >> 1;
+      const int m = k0 + (tid >> 4) + 32 * (i & 1);
+      bool ok = (st.col + 128 * sub) < MN_bound && m < kend;
       const uint32_t mm = ok ? m : 0;
       const uint32_t b = fdiv(mm, p.div_pq);
       const uint32_t rem = mm - b * (uint32_t)(p.cp * p.cq);
       const uint32_t oh = fdiv(rem, p.div_q);
       const uint32_t ow = rem - oh * p.cq;
-      const int ih = (int)oh * p.cstride - p.cpad + st.i0[0];
-      const int iw = (int)ow * p.cstride - p.cpad + st.i1[0];
+      const int ih = (int)oh * p.cstride - p.cpad + st.i0[sub];
+      const int iw = (int)ow * p.cstride - p.cpad + st.i1[sub];
       ok = ok && (unsigned)ih < (unsigned)p.ch && (unsigned)iw < (unsigned)p.cw;
-      const int64_t off = (((int64_t)b * p.ch + ih) * p.cw + iw) * p.cc + st.c_in;
-      s.v[i] = ok ? *(const u32x4*)(base + off) : z;
+      const int64_t off = (((int64_t)b * p.ch + ih) * p.cw + iw) * p.cc + st.cin[sub];
+      glds16(ok ? (const void*)(base + off) : zero, dst + 8192 * i);
     }
-  }
-}
-
-template <int MODE>
-DFU_DEV void store_tile(char* lds, int tid, const Stage& s) {
-  if constexpr (MODE == DFU_OPND_KMAJOR || MODE == DFU_OPND_CONV_FWD ||
-                MODE == DFU_OPND_CONV_DGRAD) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *(u32x4*)(lds + kc_off((tid >> 3) + 32 * i, tid & 7)) = s.v[i];
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *(u32x4*)(lds + mn_off((tid >> 4) + 16 * i, tid & 15)) = s.v[i];
   }
 }
 
@@ -237,29 +265,43 @@ DFU_DEV bf16x8 read_frag(const char* lds, int rb, int ks, int lane) {
     const int chunk = ks * 4 + (lane >> 4);
     return *(const bf16x8*)(lds + kc_off(row, chunk));
   } else {
+    const char* img = lds + 16384 * (rb >> 7);
     const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
     const int krow = ks * 32 + 8 * g + q;
-    const int col = rb + 4 * pp;
+    const int col = (rb & 127) + 4 * pp;
     const int chunk = col >> 3, half = (col >> 2) & 1;
-    const char* a0 = lds + mn_off(krow, chunk) + half * 8;
-    const char* a1 = lds + mn_off(krow + 4, chunk) + half * 8;
+    const char* a0 = img + mn_off(krow, chunk) + half * 8;
+    const char* a1 = img + mn_off(krow + 4, chunk) + half * 8;
     bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
     bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
     return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
 
+template <int N>
+DFU_DEV void wait_vmcnt() {
+  static_assert(N == 0 || N == 4 || N == 6 || N == 8, "vmcnt literal");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
 // ------------------------------------------------------------------------------ kernel
-template <int AMODE, int BMODE, int EPI>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(const GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+template <int AMODE, int BMODE, int EPI, int TM, int TN>
+__global__ __launch_bounds__(NT, 1) void gemm_kernel(const GemmArgs p) {
+  using T = Tile<TM, TN>;
+  constexpr int WGM = T::WGM, WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
+  constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
+  __shared__ __attribute__((aligned(16))) char smem[T::LDS_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WGN, wc = wave % WGN;
 
-  // XCD-aware bijective remap: blocks b and b+8 share an XCD; give each XCD a contiguous
-  // range of tiles so neighbouring tiles (shared A panel) hit the same L2.
+  // XCD-aware bijective remap (blocks b and b+8 share an XCD): each XCD gets a contiguous
+  // range of tile ids; then a grouped raster (GROUP_M x tiles_n bands walked column by
+  // column) keeps the tiles live on one XCD sharing A and B panels in its L2.
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
   int wgid = bid;
@@ -267,94 +309,101 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const GemmArgs p) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int tn = wgid % p.tiles_n;
-  const int tm = wgid / p.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  constexpr int GROUP_M = 4;
+  const int band = GROUP_M * p.tiles_n;
+  const int g0 = (wgid / band) * GROUP_M;
+  const int gm = min(GROUP_M, p.tiles_m - g0);
+  const int within = wgid - (wgid / band) * band;
+  const int tm = g0 + within % gm;
+  const int tn = within / gm;
+  const int m0 = tm * TM, n0 = tn * TN;
 
   const int kt_begin = blockIdx.y * p.kt_per_split;
   const int kt_end = min(p.ktiles, kt_begin + p.kt_per_split);
   const int kend = p.K;
 
-  LoadState sa, sb;
-  load_init<AMODE>(p, sa, p.A, p.lda, m0, p.M, tid);
-  load_init<BMODE>(p, sb, p.B, p.ldb, n0, p.N, tid);
+  LoadState<T::NLDA> sa;
+  LoadState<T::NLDB> sb;
+  load_init<AMODE, T::NLDA>(p, sa, p.A, p.lda, m0, p.M, tid);
+  load_init<BMODE, T::NLDB>(p, sb, p.B, p.ldb, n0, p.N, tid);
 
-  f32x4 acc[4][4];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  constexpr bool AK = (AMODE == DFU_OPND_KMAJOR || AMODE == DFU_OPND_CONV_FWD ||
-                       AMODE == DFU_OPND_CONV_DGRAD);
-  constexpr bool BKc = (BMODE == DFU_OPND_KMAJOR || BMODE == DFU_OPND_CONV_FWD ||
-                        BMODE == DFU_OPND_CONV_DGRAD);
+  constexpr bool AK = kcontig<AMODE>();
+  constexpr bool BKc = kcontig<BMODE>();
 
-  if (kt_begin < kt_end) {
-    Stage ra, rb;
-    load_tile<AMODE>(p, sa, p.A, p.lda, p.m_ld_bound, kt_begin, kend, tid, ra);
-    load_tile<BMODE>(p, sb, p.B, p.ldb, p.n_ld_bound, kt_begin, kend, tid, rb);
-    store_tile<AMODE>(smem, tid, ra);
-    store_tile<BMODE>(smem + TILE_BYTES, tid, rb);
-    __syncthreads();
-
-    for (int kt = kt_begin; kt < kt_end; ++kt) {
-      const int cur = (kt - kt_begin) & 1;
-      const bool has_next = kt + 1 < kt_end;
-      if (has_next) {
-        load_tile<AMODE>(p, sa, p.A, p.lda, p.m_ld_bound, kt + 1, kend, tid, ra);
-        load_tile<BMODE>(p, sb, p.B, p.ldb, p.n_ld_bound, kt + 1, kend, tid, rb);
-      }
-      const char* la = smem + cur * STAGE_BYTES;
-      const char* lb = la + TILE_BYTES;
+  auto issue = [&](int kt, char* stage) {
+    issue_tile<AMODE, T::NLDA>(p, sa, p.A, p.lda, p.m_ld_bound, kt, kend, tid, stage);
+    issue_tile<BMODE, T::NLDB>(p, sb, p.B, p.ldb, p.n_ld_bound, kt, kend, tid,
+                               stage + T::A_BYTES);
+  };
+  auto compute = [&](const char* la) {
+    const char* lb = la + T::A_BYTES;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 fa[4], fb[4];
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[FM], fb[FN];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = read_frag<AK>(la, wr * 64 + i * 16, ks, lane);
+      for (int i = 0; i < FM; ++i) fa[i] = read_frag<AK>(la, wr * WTM + i * 16, ks, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = read_frag<BKc>(lb, wc * 64 + j * 16, ks, lane);
+      for (int j = 0; j < FN; ++j) fb[j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-      }
-      if (has_next) {
-        char* ln = smem + (cur ^ 1) * STAGE_BYTES;
-        store_tile<AMODE>(ln, tid, ra);
-        store_tile<BMODE>(ln + TILE_BYTES, tid, rb);
-      }
-      __syncthreads();
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
+  };
+  // Pipeline: K-step i+NSTAGE-1 is issued (into the slot K-step i-1 vacated) right after the
+  // barrier that publishes K-step i; completion is tracked with counted vmcnt (the DMA is
+  // invisible to the compiler's waits).
+  const int nk = kt_end - kt_begin;
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) issue(kt_begin + s, smem + s * T::STAGE_BYTES);
+  for (int i = 0; i < nk; ++i) {
+    if constexpr (NSTAGE == 3) {
+      if (i + 1 < nk) wait_vmcnt<T::DMA_PER_STAGE>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (i + NSTAGE - 1 < nk)
+      issue(kt_begin + i + NSTAGE - 1, smem + ((i + NSTAGE - 1) % NSTAGE) * T::STAGE_BYTES);
+    compute(smem + (i % NSTAGE) * T::STAGE_BYTES);
   }
+  __syncthreads();
 
   // ---------------------------------------------------------------- epilogue
-  // lane holds C[m = m0 + wr*64 + 16i + (lane&15)][n = n0 + wc*64 + 16j + 4*(lane>>4) + r]
+  // lane holds C[m = m0 + wr*WTM + 16i + (lane&15)][n = n0 + wc*WTN + 16j + 4*(lane>>4) + r]
   const int lrow = lane & 15, lcol = 4 * (lane >> 4);
 
   if constexpr (EPI == DFU_EPI_BF16_STATS) {
-    // Store bf16 and emit per-column (sum, M2) of this 128-row tile over the rounded values.
-    float* red = (float*)smem;  // [2 waves-rows][128 cols][2]
-    float cnt_w = 0.f;
+    // bf16 store + per-column (sum, M2) of this TM-row tile over the rounded values:
+    // per wave two-pass in registers, then Chan's merge across the WGM row-waves in LDS.
+    static_assert(WGM * TN * 3 * 4 <= T::LDS_BYTES, "stats scratch");
+    float* red = (float*)smem;  // [WGM][TN][3]
+    float cnt = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cnt_w += (m0 + wr * 64 + 16 * i + lrow < p.M) ? 1.f : 0.f;
-    // rows valid per wave: sum over the 16 lanes sharing a column
-    float cnt = cnt_w;
+    for (int i = 0; i < FM; ++i) cnt += (m0 + wr * WTM + 16 * i + lrow < p.M) ? 1.f : 0.f;
     cnt += __shfl_xor(cnt, 1, 64);
     cnt += __shfl_xor(cnt, 2, 64);
     cnt += __shfl_xor(cnt, 4, 64);
     cnt += __shfl_xor(cnt, 8, 64);
-    float sum[4][4], m2[4][4];
+    bf16_t* C = (bf16_t*)p.C;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < FN; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float s = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + wr * 64 + 16 * i + lrow;
-          float v = bf2f(f2bf(acc[i][j][r] * p.alpha));
+        for (int i = 0; i < FM; ++i) {
+          const int m = m0 + wr * WTM + 16 * i + lrow;
+          const float v = bf2f(f2bf(acc[i][j][r] * p.alpha));
           acc[i][j][r] = v;
           s += (m < p.M) ? v : 0.f;
         }
@@ -362,12 +411,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const GemmArgs p) {
         s += __shfl_xor(s, 2, 64);
         s += __shfl_xor(s, 4, 64);
         s += __shfl_xor(s, 8, 64);
-        sum[j][r] = s;
         const float mean = cnt > 0.f ? s / cnt : 0.f;
         float q = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + wr * 64 + 16 * i + lrow;
+        for (int i = 0; i < FM; ++i) {
+          const int m = m0 + wr * WTM + 16 * i + lrow;
           const float d = acc[i][j][r] - mean;
           q += (m < p.M) ? d * d : 0.f;
         }
@@ -375,72 +423,65 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const GemmArgs p) {
         q += __shfl_xor(q, 2, 64);
         q += __shfl_xor(q, 4, 64);
         q += __shfl_xor(q, 8, 64);
-        m2[j][r] = q;
+        if (lrow == 0) {
+          const int c = wc * WTN + 16 * j + lcol + r;
+          red[(wr * TN + c) * 3 + 0] = s;
+          red[(wr * TN + c) * 3 + 1] = q;
+          red[(wr * TN + c) * 3 + 2] = cnt;
+        }
       }
     }
-    // bf16 stores
-    bf16_t* C = (bf16_t*)p.C;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wr * 64 + 16 * i + lrow;
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wr * WTM + 16 * i + lrow;
       if (m >= p.M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wc * 64 + 16 * j + lcol;
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wc * WTN + 16 * j + lcol;
         if (n + 3 < p.N) {
-          u32x2 w;
-          w[0] = pack2(acc[i][j][0], acc[i][j][1]);
-          w[1] = pack2(acc[i][j][2], acc[i][j][3]);
-          *(u32x2*)(C + (int64_t)m * p.ldc + n) = w;
+          *(u32x2*)(C + (int64_t)m * p.ldc + n) =
+              (u32x2){pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3])};
         } else {
           for (int r = 0; r < 4; ++r)
             if (n + r < p.N) C[(int64_t)m * p.ldc + n + r] = f2bf(acc[i][j][r]);
         }
       }
     }
-    // combine the two row-waves with Chan's formula
     __syncthreads();
-    if (lrow == 0 && wr == 1) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = wc * 64 + 16 * j + lcol + r;
-          red[c * 3 + 0] = sum[j][r];
-          red[c * 3 + 1] = m2[j][r];
-          red[c * 3 + 2] = cnt;
+    // one (sum, M2) record per 128-row block: merge the row-waves that cover each block
+    constexpr int HALVES = TM / 128;
+    for (int idx = tid; idx < TN * HALVES; idx += NT) {
+      const int c = idx % TN, h = idx / TN;
+      const int n = n0 + c;
+      if (n >= p.N || m0 + 128 * h >= p.M) continue;
+      float S = 0.f, Q = 0.f, Cn = 0.f;
+      for (int w = 0; w < WGM; ++w) {
+        if ((w * WTM) / 128 != h) continue;
+        const float s1 = red[(w * TN + c) * 3 + 0], q1 = red[(w * TN + c) * 3 + 1];
+        const float c1 = red[(w * TN + c) * 3 + 2];
+        if (c1 <= 0.f) continue;
+        if (Cn > 0.f) {
+          const float d = s1 / c1 - S / Cn;
+          Q += q1 + d * d * Cn * c1 / (Cn + c1);
+        } else {
+          Q = q1;
         }
-    }
-    __syncthreads();
-    if (lrow == 0 && wr == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int cl = wc * 64 + 16 * j + lcol + r;
-          const int n = n0 + cl;
-          if (n >= p.N) continue;
-          const float s1 = red[cl * 3 + 0], q1 = red[cl * 3 + 1], c1 = red[cl * 3 + 2];
-          const float s0 = sum[j][r], q0 = m2[j][r], c0 = cnt;
-          const float ct = c0 + c1;
-          float M2 = q0 + q1;
-          if (c0 > 0.f && c1 > 0.f) {
-            const float d = s1 / c1 - s0 / c0;
-            M2 += d * d * c0 * c1 / ct;
-          }
-          p.stats[((int64_t)tm * 2 + 0) * p.N + n] = s0 + s1;
-          p.stats[((int64_t)tm * 2 + 1) * p.N + n] = M2;
-        }
+        S += s1;
+        Cn += c1;
+      }
+      const int64_t blk = m0 / 128 + h;
+      p.stats[(blk * 2 + 0) * p.N + n] = S;
+      p.stats[(blk * 2 + 1) * p.N + n] = Q;
     }
     return;
   } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wr * 64 + 16 * i + lrow;
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wr * WTM + 16 * i + lrow;
       if (m >= p.M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wc * 64 + 16 * j + lcol;
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wc * WTN + 16 * j + lcol;
         if (n >= p.N) continue;
         const bool full = (n + 3 < p.N);
         float v[4];
@@ -471,7 +512,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const GemmArgs p) {
           bf16_t* Pre = (bf16_t*)p.aux_out + (int64_t)m * p.ldaux_out + n;
           float g[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) g[r] = gelu_f(bf2f(f2bf(v[r])));
+          for (int r = 0; r < 4; ++r) g[r] = gelu_f(v[r]);
           if (full) {
             *(u32x2*)Pre = (u32x2){pack2(v[0], v[1]), pack2(v[2], v[3])};
             *(u32x2*)C = (u32x2){pack2(g[0], g[1]), pack2(g[2], g[3])};
@@ -517,35 +558,33 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const GemmArgs p) {
               if (n + r < p.N) C[r] = f2bf(v[r]);
           }
         } else if constexpr (EPI == DFU_EPI_F32_ACC) {
-          float* C = (float*)p.C + (int64_t)m * p.ldc + n;
-          if (p.split > 1) {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) atomicAdd(C + r, v[r]);
-          } else if (full) {
-            f32x4 c = *(f32x4*)C;
-            *(f32x4*)C = (f32x4){c[0] + v[0], c[1] + v[1], c[2] + v[2], c[3] + v[3]};
+          if (p.slab != nullptr) {
+            // split-K partial: plain coalesced store into this split's slab
+            float* S = p.slab + ((int64_t)blockIdx.y * p.M + m) * p.N + n;
+            if (full) {
+              *(f32x4*)S = (f32x4){v[0], v[1], v[2], v[3]};
+            } else {
+              for (int r = 0; r < 4; ++r)
+                if (n + r < p.N) S[r] = v[r];
+            }
           } else {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) C[r] += v[r];
-          }
-        } else if constexpr (EPI == DFU_EPI_F32_ACC_CONVW) {
-          // m = kout, n = (r, s, c) -> OIHW offset kout*C*R*S + c*R*S + r*S + s
-          float* C = (float*)p.C;
-          const int RS = p.cr * p.cs;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int nn = n + r;
-            if (nn >= p.N) continue;
-            const int rs = nn / p.cc, c = nn - rs * p.cc;
-            const int64_t off = (int64_t)m * p.ldc + (int64_t)c * RS + rs;
-            if (p.split > 1) atomicAdd(C + off, v[r]);
-            else C[off] += v[r];
+            float* C = (float*)p.C + (int64_t)m * p.ldc + n;
+            if (p.split > 1) {
+              for (int r = 0; r < 4; ++r)
+                if (n + r < p.N) atomicAdd(C + r, v[r]);
+            } else if (full) {
+              f32x4 c = *(f32x4*)C;
+              *(f32x4*)C = (f32x4){c[0] + v[0], c[1] + v[1], c[2] + v[2], c[3] + v[3]};
+            } else {
+              for (int r = 0; r < 4; ++r)
+                if (n + r < p.N) C[r] += v[r];
+            }
           }
         } else if constexpr (EPI == DFU_EPI_PATCH) {
           // m = b*T + t  ->  row b*(T+1) + 1 + t of the fp32 token matrix
-          const int T = p.ep_tokens;
-          const int b = m / T, t = m - b * T;
-          float* C = (float*)p.C + ((int64_t)b * (T + 1) + 1 + t) * p.ldc + n;
+          const int Tt = p.ep_tokens;
+          const int b = m / Tt, t = m - b * Tt;
+          float* C = (float*)p.C + ((int64_t)b * (Tt + 1) + 1 + t) * p.ldc + n;
           const float* P = (const float*)p.aux + (int64_t)(1 + t) * p.ldaux + n;
           if (full) {
             const f32x4 pp = *(const f32x4*)P;

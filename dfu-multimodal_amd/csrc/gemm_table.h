@@ -1,0 +1,24 @@
+// Dispatch-table entries of the GEMM template, one table per tile shape (gemm_t*.hip).
+#pragma once
+#include "gemm_kernel.h"
+
+namespace dfu {
+typedef void (*gemm_fn)(const GemmArgs);
+struct Entry {
+  int a, b, e, tile;
+  gemm_fn fn;
+  int lds_bytes;
+};
+enum TileId { T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, NTILES = 4 };
+extern const Entry kTable128x128[];
+extern const int kTable128x128N;
+extern const Entry kTable256x128[];
+extern const int kTable256x128N;
+extern const Entry kTable128x256[];
+extern const int kTable128x256N;
+extern const Entry kTable256x256[];
+extern const int kTable256x256N;
+}  // namespace dfu
+
+#define DFU_ENTRY(A, B, E, TMv, TNv, TID) \
+  { A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv>, dfu::Tile<TMv, TNv>::LDS_BYTES }

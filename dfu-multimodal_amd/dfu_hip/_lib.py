@@ -47,6 +47,8 @@ class GemmDesc(ctypes.Structure):
         ("conv_k", c_int32), ("conv_r", c_int32), ("conv_s", c_int32),
         ("conv_stride", c_int32), ("conv_pad", c_int32),
         ("conv_p", c_int32), ("conv_q", c_int32),
+        ("tile", c_int32),
+        ("workspace", c_void_p), ("workspace_bytes", c_int64),
     ]
 
 
@@ -62,7 +64,10 @@ PROTOTYPES = {
     "dfu_zero": [P, I64, P],
     "dfu_gemm": [ctypes.POINTER(GemmDesc), P],
     "dfu_gemm_stats_tiles": [I32],
+    "dfu_gemm_workspace_bytes": [ctypes.POINTER(GemmDesc)],
+    "dfu_gemm_f32": [I32, I32, I32, P, I64, I64, P, I64, I64, P, I64, P, I32, I32, P],
     "dfu_pack_conv_weight": [P, P, I32, I32, I32, I32, P],
+    "dfu_conv_grad_krsc_to_oihw": [P, P, I32, I32, I32, I32, P],
     "dfu_cast_rows_bf16": [P, I64, P, I64, I32, I32, P],
     "dfu_cast_rows_f32": [P, I64, P, I64, I32, I32, P],
     "dfu_im2col_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],
@@ -70,7 +75,7 @@ PROTOTYPES = {
     "dfu_bn_finalize": [P, I32, I32, I32, P, P, F, F, P, P, P, P, P, P, P, P],
     "dfu_bn_eval_coeffs": [P, P, P, P, F, I32, P, P, P],
     "dfu_bn_apply": [P, P, P, P, I32, P, I64, I32, P],
-    "dfu_bn_bwd_blocks": [I64],
+    "dfu_bn_bwd_blocks": [I64, I32],
     "dfu_bn_bwd_reduce": [P, P, P, I32, P, P, I64, I32, P, P],
     "dfu_bn_bwd_finalize": [P, I32, I64, I32, P, P, I32, P, P, P, P],
     "dfu_bn_bwd_apply": [P, P, P, I32, P, P, P, I64, I32, P, P, P],
@@ -104,7 +109,7 @@ PROTOTYPES = {
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
 }
-_RESTYPE = {"dfu_last_error_string": c_char_p}
+_RESTYPE = {"dfu_last_error_string": c_char_p, "dfu_gemm_workspace_bytes": c_int64}
 
 
 def header_symbols(path=HEADER_PATH):
@@ -115,7 +120,9 @@ def header_symbols(path=HEADER_PATH):
 
 
 class DfuError(RuntimeError):
-    pass
+    def __init__(self, msg, code=0):
+        super().__init__(msg)
+        self.code = code
 
 
 _lib = None
@@ -143,4 +150,4 @@ def check(rc, what=""):
     if rc != 0:
         msg = load().dfu_last_error_string()
         msg = msg.decode() if msg else ""
-        raise DfuError(f"{what or 'dfu call'} failed (rc={rc}): {msg}")
+        raise DfuError(f"{what or 'dfu call'} failed (rc={rc}): {msg}", rc)

@@ -95,10 +95,6 @@ def weight_bf16_rows(w, ld=None):
     return ops.cast_rows_bf16(w2, ld_out=ld)
 
 
-def split_for(M, N, K):
-    return ops.choose_split(M, N, K)
-
-
 # ---------------------------------------------------------------------- BatchNorm helper
 class _BN:
     """Forward/backward state of one BatchNorm2d applied to a GEMM output with stats."""
@@ -172,15 +168,17 @@ def conv_wgrad(dy_rows, x_rows, geom, dw):
     g = geom
     M = g.n * g.p * g.q
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
-        split = split_for(g.k, g.c, M)
         ops.gemm(g.k, g.c, M, dy_rows, g.k, x_rows, g.c, dw, g.c, a_mode=L.OPND_MNMAJOR,
-                 b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC, split_k=split)
+                 b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
     else:
+        # accumulate in KRSC order (contiguous n' = (r, s, c): coalesced epilogue atomics),
+        # then permute-add into the OIHW fp32 parameter gradient
         N = g.r * g.s * g.c
-        split = split_for(g.k, N, M)
-        ops.gemm(g.k, N, M, dy_rows, g.k, x_rows, 0, dw, N, a_mode=L.OPND_MNMAJOR,
-                 b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC_CONVW, split_k=split,
-                 conv=g)
+        acc = _empty((g.k, N), F32, dy_rows.device)
+        ops.zero_(acc)
+        ops.gemm(g.k, N, M, dy_rows, g.k, x_rows, 0, acc, N, a_mode=L.OPND_MNMAJOR,
+                 b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC, conv=g)
+        ops.conv_grad_krsc_to_oihw(acc, dw)
 
 
 def _geom(conv, B, H, W):
@@ -237,8 +235,7 @@ class StemFn(torch.autograd.Function):
             dw = grad_buffer(w).view(Cout, -1)
             K = C * R * S
             ops.gemm(Cout, K, M, dy, Cout, col, Kp, dw, K, a_mode=L.OPND_MNMAJOR,
-                     b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC,
-                     split_k=split_for(Cout, K, M))
+                     b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
             grads_done(w)
         dx = None
         if ctx.x_requires_grad:
@@ -427,8 +424,7 @@ class PatchEmbedFn(torch.autograd.Function):
         if _wants(w):
             dw = grad_buffer(w).view(D, K)
             ops.gemm(D, K, B * T, gpatch, D, patches, K, dw, K, a_mode=L.OPND_MNMAJOR,
-                     b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC,
-                     split_k=split_for(D, K, B * T))
+                     b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
         grads_done(w, b, cls, pos)
         return None, None, None, None, None, None
 
@@ -438,7 +434,7 @@ def _linear_wgrad(dy_bf, x_bf, w, rows):
     """w.grad [N, K] += dy^T x  (dy [rows, N], x [rows, K], both bf16)."""
     N, K = w.shape
     ops.gemm(N, K, rows, dy_bf, N, x_bf, K, grad_buffer(w), K, a_mode=L.OPND_MNMAJOR,
-             b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC, split_k=split_for(N, K, rows))
+             b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
 
 
 def _ln_fwd(x2d, norm, rows, D, out_bf):
@@ -606,7 +602,13 @@ class TokenNormFn(torch.autograd.Function):
 
 # --------------------------------------------------------------------------- fusion head
 class LinearFn(torch.autograd.Function):
-    """y = x W^T + b (fp32 out) for the late-fusion MLP; x fp32 or bf16, any leading dims."""
+    """y = x W^T + b (fp32 out) for the late-fusion MLP and replaced heads.
+
+    Small problems (the fusion head: rows = batch) run in exact fp32 (dfu_gemm_f32) — the head
+    is 0.003 % of the step's FLOPs and fp32 keeps the logits free of bf16 rounding; large ones
+    use the bf16 MFMA GEMM."""
+
+    SMALL_MACS = 1 << 31
 
     @staticmethod
     def forward(ctx, x, w, b, relu):
@@ -615,51 +617,71 @@ class LinearFn(torch.autograd.Function):
         N = w.shape[0]
         x2 = x.detach().reshape(-1, K)
         rows = x2.shape[0]
-        xb = x2.contiguous() if x2.dtype == BF16 else ops.cast_rows_bf16(x2)
-        wb = weight_bf16_rows(w)
+        bias = b.detach() if b is not None else None
+        small = rows * N * K <= LinearFn.SMALL_MACS
         y = _empty((rows, N), F32, x.device)
-        ops.gemm(rows, N, K, xb, K, wb, K, y, N, epilogue=L.EPI_F32,
-                 bias=b.detach() if b is not None else None)
-        if relu:
-            y = ops.relu_fwd(y)
+        if small:
+            xf = x2.float().contiguous()
+            wf = w.detach()
+            ops.gemm_f32(rows, N, K, xf, K, 1, wf, K, 1, y, N, bias=bias, relu=relu)
+            saved = (xf, wf)
+        else:
+            xb = x2.contiguous() if x2.dtype == BF16 else ops.cast_rows_bf16(x2)
+            wb = weight_bf16_rows(w)
+            ops.gemm(rows, N, K, xb, K, wb, K, y, N, epilogue=L.EPI_F32, bias=bias)
+            if relu:
+                y = ops.relu_fwd(y)
+            saved = (xb, wb)
+        ctx.small = small
         ctx.relu = relu
         ctx.params = (w, b)
         ctx.x_dtype = x.dtype
         ctx.lead = lead
-        ctx.save_for_backward(xb, wb, y if relu else None)
+        ctx.save_for_backward(*saved, y if relu else None)
         return y.view(*lead, N)
 
     @staticmethod
     def backward(ctx, gy):
-        xb, wb, y = ctx.saved_tensors
+        xs, ws, y = ctx.saved_tensors
         w, b = ctx.params
-        rows, K = xb.shape
-        N = wb.shape[0]
+        rows, K = xs.shape
+        N = ws.shape[0]
         g = gy.reshape(rows, N)
         if g.dtype != F32:
             g = g.float()
         g = g.contiguous()
         if ctx.relu:
             g = ops.relu_bwd(g, y)
-        gb = ops.cast_rows_bf16(g, ld_out=max(8, (N + 7) // 8 * 8))
         dx = None
-        if ctx.needs_input_grad[0]:
-            # dX[rows, K] = g[rows, N] W[N, K]; N may be tiny (2), pad the contraction to 8
-            Np = gb.shape[1]
-            if Np != N:
-                wp = _empty((Np, K), BF16, xb.device)
-                ops.zero_(wp)
-                wp[:N].copy_(wb)
-            else:
-                wp = wb
-            out_bf = ctx.x_dtype == BF16
-            dx = _empty((rows, K), BF16 if out_bf else F32, xb.device)
-            ops.gemm(rows, K, Np, gb, Np, wp, K, dx, K, b_mode=L.OPND_MNMAJOR,
-                     epilogue=L.EPI_BF16 if out_bf else L.EPI_F32)
-            dx = dx.view(*ctx.lead, K)
-        if _wants(w):
-            ops.gemm(N, K, rows, gb, gb.shape[1], xb, K, grad_buffer(w), K,
-                     a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+        if ctx.small:
+            if ctx.needs_input_grad[0]:
+                dx = _empty((rows, K), F32, xs.device)
+                # dX[r][k] = sum_n g[r][n] W[n][k]
+                ops.gemm_f32(rows, K, N, g, N, 1, ws, 1, K, dx, K)
+                if ctx.x_dtype != F32:
+                    dx = dx.to(ctx.x_dtype)
+                dx = dx.view(*ctx.lead, K)
+            if _wants(w):
+                # dW[n][k] += sum_r g[r][n] X[r][k]
+                ops.gemm_f32(N, K, rows, g, 1, N, xs, 1, K, grad_buffer(w), K, accumulate=True)
+        else:
+            gb = ops.cast_rows_bf16(g, ld_out=max(8, (N + 7) // 8 * 8))
+            if ctx.needs_input_grad[0]:
+                Np = gb.shape[1]
+                if Np != N:
+                    wp = _empty((Np, K), BF16, xs.device)
+                    ops.zero_(wp)
+                    wp[:N].copy_(ws)
+                else:
+                    wp = ws
+                out_bf = ctx.x_dtype == BF16
+                dx = _empty((rows, K), BF16 if out_bf else F32, xs.device)
+                ops.gemm(rows, K, Np, gb, Np, wp, K, dx, K, b_mode=L.OPND_MNMAJOR,
+                         epilogue=L.EPI_BF16 if out_bf else L.EPI_F32)
+                dx = dx.view(*ctx.lead, K)
+            if _wants(w):
+                ops.gemm(N, K, rows, gb, gb.shape[1], xs, K, grad_buffer(w), K,
+                         a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
         if _wants(b):
             ops.colsum_add(g, grad_buffer(b))
         grads_done(w, b)
@@ -694,13 +716,13 @@ class DropoutFn(torch.autograd.Function):
 
 
 class ConcatFn(torch.autograd.Function):
-    """torch.cat([rgb_feat, thermal_feat], 1) into one bf16 GEMM operand."""
+    """torch.cat([rgb_feat, thermal_feat], 1) (train_multimodal_fusion.py:321), fp32."""
 
     @staticmethod
     def forward(ctx, a, b):
         ctx.dims = (a.shape[1], b.shape[1])
         ctx.dtypes = (a.dtype, b.dtype)
-        return ops.concat2_bf16(a.detach(), b.detach())
+        return ops.concat2_f32(a.detach().float(), b.detach().float())
 
     @staticmethod
     def backward(ctx, g):

@@ -47,9 +47,16 @@ class ConvGeom:
         self.q = (w + 2 * pad - s) // stride + 1
 
 
+TILES = {"auto": 0, "128x128": 1, "256x128": 2, "128x256": 3, "256x256": 4}
+
+
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
          epilogue=L.EPI_BF16, alpha=1.0, bias=None, aux=None, ldaux=0, aux_out=None,
-         ldaux_out=0, stats=None, split_k=1, ep_tokens=0, conv=None):
+         ldaux_out=0, stats=None, split_k=0, ep_tokens=0, conv=None, tile=0, workspace=None):
+    """C = epilogue(A @ B^T).  `split_k` (F32_ACC only): 0 = library cost model, 1 = none.
+    `tile`: 0 = library cost model, else a TILES id.  Split-K partials go to fp32 slabs in
+    `workspace` (allocated here from the stream-ordered caching allocator when None) and are
+    reduced deterministically by a second kernel."""
     d = L.GemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
     d.a_mode, d.b_mode = int(a_mode), int(b_mode)
@@ -65,26 +72,38 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
     d.stats = stats.data_ptr() if stats is not None else None
     d.split_k = int(split_k)
     d.ep_tokens = int(ep_tokens)
+    d.tile = int(tile)
     if conv is not None:
         d.conv_n, d.conv_h, d.conv_w, d.conv_c = conv.n, conv.h, conv.w, conv.c
         d.conv_k, d.conv_r, d.conv_s = conv.k, conv.r, conv.s
         d.conv_stride, d.conv_pad, d.conv_p, d.conv_q = conv.stride, conv.pad, conv.p, conv.q
+    if epilogue == L.EPI_F32_ACC:
+        need = lib().dfu_gemm_workspace_bytes(ctypes.byref(d))
+        if need > 0:
+            if workspace is None or workspace.numel() * workspace.element_size() < need:
+                workspace = torch.empty(need, dtype=torch.uint8, device=C.device)
+            d.workspace = workspace.data_ptr()
+            d.workspace_bytes = int(need)
     check(lib().dfu_gemm(ctypes.byref(d), stream_ptr()), "dfu_gemm")
+
+
+def gemm_workspace_bytes(M, N, K, a_mode, b_mode, epilogue=L.EPI_F32_ACC, split_k=0, tile=0):
+    d = L.GemmDesc()
+    d.M, d.N, d.K = int(M), int(N), int(K)
+    d.a_mode, d.b_mode, d.epilogue = int(a_mode), int(b_mode), int(epilogue)
+    d.split_k, d.tile = int(split_k), int(tile)
+    return int(lib().dfu_gemm_workspace_bytes(ctypes.byref(d)))
+
+
+def gemm_f32(M, N, K, A, sam, sak, B, sbn, sbk, C, ldc, bias=None, relu=False, accumulate=False):
+    """Exact fp32 strided GEMM (fusion head)."""
+    check(lib().dfu_gemm_f32(int(M), int(N), int(K), ptr(A), int(sam), int(sak), ptr(B), int(sbn),
+                             int(sbk), ptr(C), int(ldc), ptr(bias), int(relu), int(accumulate),
+                             stream_ptr()), "dfu_gemm_f32")
 
 
 def stats_tiles(M):
     return lib().dfu_gemm_stats_tiles(int(M))
-
-
-def choose_split(M, N, K, target_blocks=512, min_k_per_split=256):
-    """split-K for weight-gradient GEMMs whose output tile grid underfills 256 CUs."""
-    tiles = ((M + 127) // 128) * ((N + 127) // 128)
-    ktiles = (K + 63) // 64
-    if tiles >= target_blocks:
-        return 1
-    split = max(1, target_blocks // tiles)
-    split = min(split, max(1, ktiles // (min_k_per_split // 64)))
-    return int(split)
 
 
 # ------------------------------------------------------------------------------- layouts
@@ -97,6 +116,12 @@ def pack_conv_weight(w, out=None):
     check(lib().dfu_pack_conv_weight(ptr(w.contiguous()), ptr(out), K, C, R, S, stream_ptr()),
           "dfu_pack_conv_weight")
     return out
+
+
+def conv_grad_krsc_to_oihw(krsc, oihw):
+    K, C, R, S = oihw.shape
+    check(lib().dfu_conv_grad_krsc_to_oihw(ptr(krsc), ptr(oihw), K, C, R, S, stream_ptr()),
+          "dfu_conv_grad_krsc_to_oihw")
 
 
 def cast_rows_bf16(x, ld_out=None, out=None):
@@ -171,7 +196,7 @@ def bn_apply(y, scale, shift, residual, relu, out, M, C):
 def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta,
            batch_stats=True):
     """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply."""
-    blocks = lib().dfu_bn_bwd_blocks(M)
+    blocks = lib().dfu_bn_bwd_blocks(M, C)
     partial = torch.empty((blocks, 2, C), dtype=F32, device=y.device)
     coef = torch.empty((C, 3), dtype=F32, device=y.device)
     s = stream_ptr()
@@ -301,6 +326,19 @@ def dropout_bwd(dy, mask, p):
     check(lib().dfu_dropout_bwd(ptr(dy), ptr(mask), ptr(dx), dy.numel(), float(p),
                                 int(dy.dtype == BF16), stream_ptr()), "dfu_dropout_bwd")
     return dx
+
+
+def concat2_f32(a, b):
+    """[a | b] fp32 (rows x (Na+Nb)) by two strided row copies."""
+    rows, Na = a.shape
+    Nb = b.shape[1]
+    out = torch.empty((rows, Na + Nb), dtype=F32, device=a.device)
+    s = stream_ptr()
+    check(lib().dfu_gather_rows_f32(ptr(a.contiguous()), Na, 1, 0, rows, Na, ptr(out), Na + Nb, s),
+          "dfu_gather_rows_f32")
+    check(lib().dfu_gather_rows_f32(ptr(b.contiguous()), Nb, 1, 0, rows, Nb, ptr(out[:, Na:]),
+                                    Na + Nb, s), "dfu_gather_rows_f32")
+    return out
 
 
 def concat2_bf16(a, b):

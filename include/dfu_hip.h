@@ -52,13 +52,13 @@ enum dfu_operand_mode {
 enum dfu_epilogue {
   DFU_EPI_BF16 = 0,          /* C bf16 = alpha*acc + bias                                  */
   DFU_EPI_BF16_RELU = 1,     /* C bf16 = relu(alpha*acc + bias)                             */
-  DFU_EPI_BF16_GELU = 2,     /* aux_out bf16 = acc + bias (pre-act); C bf16 = gelu(pre)     */
+  DFU_EPI_BF16_GELU = 2,     /* aux_out bf16 = pre = acc + bias; C bf16 = gelu(pre fp32)    */
   DFU_EPI_F32 = 3,           /* C f32 = alpha*acc + bias                                    */
   DFU_EPI_F32_RESID = 4,     /* C f32 = aux f32 + alpha*acc + bias  (residual stream)       */
   DFU_EPI_BF16_DGELU = 5,    /* C bf16 = acc * gelu'(aux bf16)                              */
   DFU_EPI_BF16_ADD = 6,      /* C bf16 = acc + aux bf16                                     */
-  DFU_EPI_F32_ACC = 7,       /* C f32 += acc   (split-K: atomic add)                        */
-  DFU_EPI_F32_ACC_CONVW = 8, /* C f32 (OIHW weight grad) += acc, n = (r,s,c) scattered      */
+  DFU_EPI_F32_ACC = 7,       /* C f32 += acc   (split-K: fp32 slabs + reduce, or atomics)   */
+  DFU_EPI_F32_ACC_CONVW = 8, /* retired: conv wgrad accumulates KRSC + dfu_conv_grad_krsc... */
   DFU_EPI_BF16_STATS = 9,    /* C bf16 = acc; per-column (sum, M2) of each 128-row tile     */
   DFU_EPI_PATCH = 10         /* ViT patch-embed: C f32 [B][T+1][N] row 1+p = acc+bias+pos   */
 };
@@ -79,25 +79,39 @@ typedef struct dfu_gemm_desc {
   int64_t ldaux;
   void* aux_out;       /* GELU pre-activation output                            */
   int64_t ldaux_out;
-  float* stats;        /* DFU_EPI_BF16_STATS: [ceil(M/128)][2][N] fp32          */
-  int32_t split_k;     /* >1 only with the F32_ACC epilogues                    */
+  float* stats;        /* DFU_EPI_BF16_STATS: [ceil(M/128)][2][N] fp32 (sum, M2)  */
+  int32_t split_k;     /* F32_ACC only: 0 = auto (cost model), 1 = none, >1 fixed */
   int32_t ep_tokens;   /* DFU_EPI_PATCH: patches per image                      */
   /* implicit-GEMM convolution geometry (modes 2-5 and the CONVW epilogue)       */
   int32_t conv_n, conv_h, conv_w, conv_c; /* input  N,H,W,C                        */
   int32_t conv_k, conv_r, conv_s;         /* output channels, filter R,S           */
   int32_t conv_stride, conv_pad;
   int32_t conv_p, conv_q;                 /* output H,W                            */
+  int32_t tile;        /* 0 = auto; 1..4 = 128x128, 256x128, 128x256, 256x256   */
+  void* workspace;     /* split-K fp32 slabs (dfu_gemm_workspace_bytes); NULL =  */
+  int64_t workspace_bytes; /*   split-K partials accumulate with fp32 atomics     */
 } dfu_gemm_desc;
 
 int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
-/* Rows of 128 produced by DFU_EPI_BF16_STATS for M rows. */
+/* 128-row blocks (rows of the stats slab) produced by DFU_EPI_BF16_STATS for M rows. */
 int dfu_gemm_stats_tiles(int32_t M);
+/* Workspace bytes for deterministic split-K slabs of this descriptor (0 if not split). */
+int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* desc);
+/* Exact fp32 GEMM for the tiny fusion head (train_multimodal_fusion.py:305-313):
+ * C[m][n] = accumulate*C[m][n] + sum_k A[m*sam + k*sak] * B[n*sbn + k*sbk] (+bias[n]) (relu). */
+int dfu_gemm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t sam, int64_t sak,
+                 const float* B, int64_t sbn, int64_t sbk, float* C, int64_t ldc,
+                 const float* bias, int32_t relu, int32_t accumulate, void* stream);
 
 /* ---------------------------------------------------------------- layout / packing -- */
 /* fp32 OIHW conv weight -> bf16 KRSC ([K][R][S][C]) for the implicit-GEMM convs
  * (torchvision resnet.py conv3x3/conv1x1 weights; state_dict stays OIHW fp32). */
 int dfu_pack_conv_weight(const float* w, void* out_bf16, int32_t K, int32_t C, int32_t R,
                          int32_t S, void* stream);
+/* Conv weight gradient accumulated in KRSC fp32 (coalesced GEMM epilogue) -> ADD into the
+ * OIHW fp32 parameter gradient: oihw[k][c][r][s] += krsc[k][r][s][c]. */
+int dfu_conv_grad_krsc_to_oihw(const float* krsc, float* oihw, int32_t K, int32_t C, int32_t R,
+                               int32_t S, void* stream);
 /* fp32 [rows][cols] -> bf16 [rows][ld_out] (cols..ld_out-1 zero-filled). */
 int dfu_cast_rows_bf16(const float* in, int64_t ld_in, void* out, int64_t ld_out, int32_t rows,
                        int32_t cols, void* stream);
@@ -131,8 +145,8 @@ int dfu_bn_eval_coeffs(const float* gamma, const float* beta, const float* runni
 int dfu_bn_apply(const void* y, const float* scale, const float* shift, const void* residual,
                  int32_t relu, void* out, int64_t M, int32_t C, void* stream);
 /* Backward of out = act(bn(y) (+res)).  reduce: per-channel partial sums of g and g*xhat,
- * g = dout * [out > 0 if relu]; written as [blocks][2][C] (dfu_bn_bwd_blocks()). */
-int dfu_bn_bwd_blocks(int64_t M);
+ * g = dout * [out > 0 if relu]; written as [blocks][2][C] (dfu_bn_bwd_blocks(M, C)). */
+int dfu_bn_bwd_blocks(int64_t M, int32_t C);
 int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* out, int32_t relu,
                       const float* mean, const float* invstd, int64_t M, int32_t C,
                       float* partial, void* stream);

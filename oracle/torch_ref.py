@@ -174,7 +174,7 @@ class Mlp(nn.Module):
         self.fc2 = nn.Linear(hidden, dim)
 
     def forward(self, x):
-        return linear(rb(self.act(rb(linear(x, self.fc1)))), self.fc2)
+        return linear(rb(self.act(linear(x, self.fc1))), self.fc2)
 
 
 class Block(nn.Module):
@@ -226,10 +226,8 @@ class MLPFusion(nn.Module):
                                         nn.Linear(hidden_dim, num_classes))
 
     def forward(self, rgb_feat, thermal_feat):
-        x = torch.cat([rgb_feat, thermal_feat], dim=1)
-        for m in self.classifier:
-            x = linear(x, m) if isinstance(m, nn.Linear) else m(x)
-        return x
+        # the MI355X head runs in exact fp32 (dfu_gemm_f32): no bf16 rounding here
+        return self.classifier(torch.cat([rgb_feat, thermal_feat], dim=1))
 
 
 class MultimodalFusionModel(nn.Module):

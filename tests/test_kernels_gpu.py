@@ -28,76 +28,123 @@ def close(a, b, atol, rtol=0.0, what=""):
 
 
 # ------------------------------------------------------------------------------ GEMM
+TILES = [0, 1, 2, 3, 4]  # auto, 128x128, 256x128, 128x256, 256x256
+
+
+def gemm_t(*args, tile=0, **kw):
+    """ops.gemm with a forced tile; skip the case when that tile has no such instantiation."""
+    try:
+        ops.gemm(*args, tile=tile, **kw)
+    except L.DfuError as e:
+        if tile and e.code == L.DFU_E_UNSUPPORTED:
+            pytest.skip(f"tile {tile} not instantiated for this combination")
+        raise
+
+
+@pytest.mark.parametrize("tile", TILES)
 @pytest.mark.parametrize("M,N,K", [(300, 200, 136), (128, 128, 64), (1000, 2304, 768), (64, 2, 512),
                                    (12608, 768, 768)])
-def test_gemm_nt_f32(M, N, K):
+def test_gemm_nt_f32(M, N, K, tile):
     A = rnd(M, K, seed=1)
     B = rnd(N, K, seed=2)
     C = torch.empty(M, N, dtype=torch.float32, device=DEV)
-    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_F32)
+    gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_F32, tile=tile)
     ref = A.float() @ B.float().t()
     close(C, ref, atol=2e-3 * math.sqrt(K), what="nt_f32")
 
 
+@pytest.mark.parametrize("tile", TILES)
 @pytest.mark.parametrize("M,N,K", [(300, 200, 136), (777, 768, 3072)])
-def test_gemm_nn_f32(M, N, K):
+def test_gemm_nn_f32(M, N, K, tile):
     A = rnd(M, K, seed=3)
     Bkn = rnd(K, N, seed=4)
     C = torch.empty(M, N, dtype=torch.float32, device=DEV)
-    ops.gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32)
+    gemm_t(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32, tile=tile)
     close(C, A.float() @ Bkn.float(), atol=2e-3 * math.sqrt(K), what="nn_f32")
 
 
-@pytest.mark.parametrize("M,N,K,split", [(200, 136, 300, 1), (768, 2304, 12608, 4), (64, 147, 5000, 7)])
-def test_gemm_tn_acc(M, N, K, split):
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("M,N,K,split", [(200, 136, 300, 1), (768, 2304, 12608, 4), (64, 147, 5000, 7),
+                                         (768, 3072, 12608, 0), (296, 200, 4000, 0)])
+def test_gemm_tn_acc(M, N, K, split, tile):
     Akm = rnd(K, M, seed=5)
     Bkn = rnd(K, (N + 7) // 8 * 8, seed=6)
     C = rnd(M, N, dtype=torch.float32, seed=7)
     ref = C + Akm.float().t() @ Bkn.float()[:, :N]
-    ops.gemm(M, N, K, Akm, M, Bkn, Bkn.shape[1], C, N, a_mode=L.OPND_MNMAJOR,
-             b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC, split_k=split)
+    gemm_t(M, N, K, Akm, M, Bkn, Bkn.shape[1], C, N, a_mode=L.OPND_MNMAJOR,
+           b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC, split_k=split, tile=tile)
     close(C, ref, atol=3e-3 * math.sqrt(K), what="tn_acc")
 
 
-def test_gemm_epilogues():
+def test_gemm_split_slab_deterministic():
+    """Split-K through fp32 slabs + reduce kernel is bitwise reproducible."""
+    M, N, K = 768, 768, 12608
+    Akm = rnd(K, M, seed=40)
+    Bkn = rnd(K, N, seed=41)
+    outs = []
+    for _ in range(2):
+        C = torch.zeros(M, N, dtype=torch.float32, device=DEV)
+        ops.gemm(M, N, K, Akm, M, Bkn, N, C, N, a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR,
+                 epilogue=L.EPI_F32_ACC, split_k=8)
+        outs.append(C)
+    assert torch.equal(outs[0], outs[1])
+
+
+def gemm_or_auto(*args, tile=0, **kw):
+    """ops.gemm with a tile preference; falls back to auto where that tile is not built."""
+    try:
+        ops.gemm(*args, tile=tile, **kw)
+    except L.DfuError as e:
+        if not (tile and e.code == L.DFU_E_UNSUPPORTED):
+            raise
+        ops.gemm(*args, **kw)
+
+
+@pytest.mark.parametrize("tile", TILES)
+def test_gemm_epilogues(tile):
+    def gemm(*a, **k):
+        gemm_or_auto(*a, tile=tile, **k)
+
     M, N, K = 333, 256, 192
     A = rnd(M, K, seed=8)
     B = rnd(N, K, seed=9)
     bias = rnd(N, dtype=torch.float32, seed=10)
     acc = A.float() @ B.float().t()
     C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16, bias=bias, alpha=0.5)
+    gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16, bias=bias, alpha=0.5)
     close(C, acc * 0.5 + bias, atol=3e-2, rtol=1e-2, what="bf16 bias alpha")
-    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_RELU, bias=bias)
+    gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_RELU, bias=bias)
     close(C, torch.relu(acc + bias), atol=3e-2, rtol=1e-2, what="relu")
     pre = torch.empty_like(C)
-    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_GELU, bias=bias, aux_out=pre, ldaux_out=N)
+    gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_GELU, bias=bias, aux_out=pre, ldaux_out=N)
     close(pre, acc + bias, atol=3e-2, rtol=1e-2, what="gelu pre")
     close(C, F.gelu(acc + bias), atol=3e-2, rtol=1e-2, what="gelu")
     res = rnd(M, N, dtype=torch.float32, seed=11)
     Cf = torch.empty(M, N, dtype=torch.float32, device=DEV)
-    ops.gemm(M, N, K, A, K, B, K, Cf, N, epilogue=L.EPI_F32_RESID, bias=bias, aux=res, ldaux=N)
+    gemm(M, N, K, A, K, B, K, Cf, N, epilogue=L.EPI_F32_RESID, bias=bias, aux=res, ldaux=N)
     close(Cf, res + acc + bias, atol=2e-3 * math.sqrt(K), what="resid")
     # dgrad-style epilogues (B as [K][N])
     Bkn = rnd(K, N, seed=12)
     acc2 = A.float() @ Bkn.float()
     h = rnd(M, N, seed=13)
-    ops.gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N)
+    gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N)
     x = h.float()
     dg = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
     close(C, acc2 * dg, atol=5e-2, rtol=1e-2, what="dgelu")
-    ops.gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16_ADD, aux=h, ldaux=N)
+    gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16_ADD, aux=h, ldaux=N)
     close(C, acc2 + h.float(), atol=5e-2, rtol=1e-2, what="add")
 
 
-def test_gemm_stats():
-    M, N, K = 1000, 192, 128
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("M", [1000, 1100, 1024])
+def test_gemm_stats(M, tile):
+    N, K = 192, 128
     A = rnd(M, K, seed=14)
     B = rnd(N, K, seed=15)
     C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     tiles = ops.stats_tiles(M)
     stats = torch.empty(tiles, 2, N, dtype=torch.float32, device=DEV)
-    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_STATS, stats=stats)
+    gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_STATS, stats=stats, tile=tile)
     ref = A.float() @ B.float().t()
     close(C, ref, atol=5e-2, rtol=1e-2, what="stats store")
     Cf = C.float()
@@ -135,8 +182,9 @@ def _nhwc(t):
     return t.permute(0, 2, 3, 1).contiguous()
 
 
+@pytest.mark.parametrize("tile", TILES)
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_dgrad_wgrad(case):
+def test_conv_fwd_dgrad_wgrad(case, tile):
     N, H, W, C, K, R, S, st, pad = case
     g = ops.ConvGeom(N, H, W, C, K, R, S, st, pad)
     x = rnd(N, C, H, W, seed=20)
@@ -152,22 +200,23 @@ def test_conv_fwd_dgrad_wgrad(case):
     Y = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
     stats = torch.empty(ops.stats_tiles(M), 2, K, dtype=torch.float32, device=DEV)
     if R == 1 and S == 1 and st == 1:
-        ops.gemm(M, K, C, x_nhwc, C, w_krsc, C, Y, K, epilogue=L.EPI_BF16_STATS, stats=stats)
+        gemm_or_auto(M, K, C, x_nhwc, C, w_krsc, C, Y, K, epilogue=L.EPI_BF16_STATS, stats=stats, tile=tile)
     else:
-        ops.gemm(M, K, R * S * C, x_nhwc, 0, w_krsc, R * S * C, Y, K, a_mode=L.OPND_CONV_FWD,
-                 epilogue=L.EPI_BF16_STATS, stats=stats, conv=g)
+        gemm_or_auto(M, K, R * S * C, x_nhwc, 0, w_krsc, R * S * C, Y, K, a_mode=L.OPND_CONV_FWD,
+                 epilogue=L.EPI_BF16_STATS, stats=stats, conv=g, tile=tile)
     close(Y.view(N, g.p, g.q, K), _nhwc(y_ref.detach()), atol=5e-2, rtol=1e-2, what="conv fwd")
     # dgrad
     dy_nhwc = _nhwc(dy)
     dX = torch.empty(N * H * W, C, dtype=torch.bfloat16, device=DEV)
-    ops.gemm(N * H * W, C, R * S * K, dy_nhwc, 0, w_krsc, R * S * C, dX, C,
-             a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=L.EPI_BF16, conv=g)
+    gemm_or_auto(N * H * W, C, R * S * K, dy_nhwc, 0, w_krsc, R * S * C, dX, C,
+             a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=L.EPI_BF16, conv=g, tile=tile)
     close(dX.view(N, H, W, C), _nhwc(xf.grad), atol=5e-2, rtol=1e-2, what="conv dgrad")
     # wgrad (OIHW fp32 accumulate)
     dW = torch.zeros(K, C, R, S, dtype=torch.float32, device=DEV)
-    split = ops.choose_split(K, R * S * C, M)
-    ops.gemm(K, R * S * C, M, dy_nhwc, K, x_nhwc, 0, dW, C * R * S, a_mode=L.OPND_MNMAJOR,
-             b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC_CONVW, split_k=split, conv=g)
+    acc = torch.zeros(K, R * S * C, dtype=torch.float32, device=DEV)
+    gemm_or_auto(K, R * S * C, M, dy_nhwc, K, x_nhwc, 0, acc, R * S * C, a_mode=L.OPND_MNMAJOR,
+             b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC, conv=g, tile=tile)
+    ops.conv_grad_krsc_to_oihw(acc, dW)
     close(dW, wf.grad, atol=2e-2 * math.sqrt(M / 100), rtol=1e-2, what="conv wgrad")
 
 
