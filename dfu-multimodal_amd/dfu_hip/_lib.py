@@ -116,7 +116,7 @@ def header_symbols(path=HEADER_PATH):
     """Every function name declared in include/dfu_hip.h (used by the symbol-export test)."""
     with open(path) as f:
         text = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dfu_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(dfu_\w+)\s*\(", text, re.M)))
 
 
 class DfuError(RuntimeError):

@@ -57,6 +57,9 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
     `tile`: 0 = library cost model, else a TILES id.  Split-K partials go to fp32 slabs in
     `workspace` (allocated here from the stream-ordered caching allocator when None) and are
     reduced deterministically by a second kernel."""
+    for t, name in ((A, "A"), (B, "B"), (C, "C")):
+        if not t.is_cuda:
+            raise ValueError(f"gemm: operand {name} must be on the GPU (there is no host path)")
     d = L.GemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
     d.a_mode, d.b_mode = int(a_mode), int(b_mode)

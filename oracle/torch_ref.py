@@ -216,14 +216,19 @@ class VisionTransformer(nn.Module):
 
 # ------------------------------------------------------------------ fusion head / model
 class MLPFusion(nn.Module):
-    """grad_cam_visualization.py:289-302 (Dropout p configurable, 0.7 there)."""
+    """grad_cam_visualization.py:289-302 (Dropout p configurable, 0.7 there);
+    hidden_dims=(512, 256) gives the train-script head, train_multimodal_fusion.py:305-313."""
 
     def __init__(self, rgb_feat_dim=2048, thermal_feat_dim=768, hidden_dim=512, num_classes=2,
-                 dropout=0.7):
+                 dropout=0.7, hidden_dims=None):
         super().__init__()
-        self.classifier = nn.Sequential(nn.Linear(rgb_feat_dim + thermal_feat_dim, hidden_dim),
-                                        nn.ReLU(), nn.Dropout(dropout),
-                                        nn.Linear(hidden_dim, num_classes))
+        dims = tuple(hidden_dims) if hidden_dims is not None else (hidden_dim,)
+        layers, d = [], rgb_feat_dim + thermal_feat_dim
+        for h in dims:
+            layers += [nn.Linear(d, h), nn.ReLU(), nn.Dropout(dropout)]
+            d = h
+        layers.append(nn.Linear(d, num_classes))
+        self.classifier = nn.Sequential(*layers)
 
     def forward(self, rgb_feat, thermal_feat):
         # the MI355X head runs in exact fp32 (dfu_gemm_f32): no bf16 rounding here

@@ -1,0 +1,126 @@
+"""Host-side checks that need no GPU: the C ABI library loads and exports every symbol
+include/dfu_hip.h declares, the ctypes descriptor mirrors the C struct byte for byte, argument
+validation fails loudly, the GEMM planner's host logic, and the flat-parameter layout."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+import torch
+
+from dfu_hip import _lib as L
+from dfu_hip import ops
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = L.load()
+    declared = L.header_symbols()
+    assert len(declared) >= 40
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, f"declared in include/dfu_hip.h but not exported: {missing}"
+    assert set(declared) == set(L.PROTOTYPES), "ctypes prototypes out of sync with the header"
+    assert lib.dfu_version() >= 1
+
+
+def test_gemm_desc_layout_matches_c(tmp_path):
+    fields = [f[0] for f in L.GemmDesc._fields_]
+    src = ['#include <stddef.h>', '#include <stdio.h>', '#include "dfu_hip.h"', "int main(void){",
+           'printf("%zu\\n", sizeof(dfu_gemm_desc));']
+    src += [f'printf("%zu\\n", offsetof(dfu_gemm_desc, {f}));' for f in fields]
+    src += ["return 0;}"]
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), str(c), "-o", str(exe)],
+                   check=True)
+    out = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
+                                          text=True).stdout.split()]
+    assert out[0] == ctypes.sizeof(L.GemmDesc)
+    for f, off in zip(fields, out[1:]):
+        assert getattr(L.GemmDesc, f).offset == off, f
+
+
+def _desc(**kw):
+    d = L.GemmDesc()
+    d.M, d.N, d.K = 256, 256, 256
+    d.A = d.B = d.C = 1 << 20  # never dereferenced: validation fails before any launch
+    d.lda = d.ldb = d.ldc = 256
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(M=0), "bad shape"),
+    (dict(K=100), "multiple of 8"),
+    (dict(tile=9), "bad tile"),
+    (dict(split_k=4), "needs the F32_ACC"),
+    (dict(lda=100), "lda"),
+    (dict(epilogue=L.EPI_BF16_STATS), "stats slab"),
+    (dict(a_mode=L.OPND_CONV_FWD, epilogue=L.EPI_BF16_STATS, stats=1 << 20, conv_n=1),
+     "conv geometry"),
+    (dict(A=(1 << 20) + 4), "16-byte aligned"),
+])
+def test_gemm_validation_errors(kw, msg):
+    lib = L.load()
+    d = _desc(**kw)
+    rc = lib.dfu_gemm(ctypes.byref(d), None)
+    assert rc == L.DFU_E_INVALID
+    assert msg in lib.dfu_last_error_string().decode()
+    with pytest.raises(L.DfuError):
+        L.check(rc, "dfu_gemm")
+
+
+def test_gemm_unsupported_combination():
+    lib = L.load()
+    d = _desc(epilogue=L.EPI_F32, tile=4)  # EPI_F32 is built for 128x128 only
+    assert lib.dfu_gemm(ctypes.byref(d), None) == L.DFU_E_UNSUPPORTED
+
+
+def test_gemm_planner_workspace():
+    MN = L.OPND_MNMAJOR
+    # ViT fc1 weight gradient at B=64: 36 output tiles of 256x256 for 256 CUs -> split-K slabs
+    ws = ops.gemm_workspace_bytes(3072, 768, 64 * 197, MN, MN)
+    assert ws > 0 and ws % (3072 * 768 * 4) == 0
+    splits = ws // (3072 * 768 * 4)
+    assert 2 <= splits <= 32
+    # a forced split is honoured exactly
+    assert ops.gemm_workspace_bytes(768, 768, 12608, MN, MN, split_k=8) == 8 * 768 * 768 * 4
+    # no split -> no workspace; non-accumulating epilogues never need one
+    assert ops.gemm_workspace_bytes(768, 768, 12608, MN, MN, split_k=1) == 0
+    assert ops.gemm_workspace_bytes(12608, 768, 768, L.OPND_KMAJOR, L.OPND_KMAJOR,
+                                    epilogue=L.EPI_BF16) == 0
+
+
+@pytest.mark.parametrize("M,tiles", [(1, 1), (128, 1), (129, 2), (200704, 1568), (3136, 25)])
+def test_stats_tiles_are_128_row_blocks(M, tiles):
+    assert ops.stats_tiles(M) == tiles
+
+
+def test_ops_reject_host_tensors():
+    a = torch.zeros(128, 128, dtype=torch.bfloat16)
+    c = torch.zeros(128, 128, dtype=torch.float32)
+    with pytest.raises((ValueError, TypeError)):
+        ops.gemm(128, 128, 128, a, 128, a, 128, c, 128, epilogue=L.EPI_F32)
+
+
+def test_conv_geometry():
+    g = ops.ConvGeom(64, 56, 56, 128, 128, 3, 3, 2, 1)
+    assert (g.p, g.q) == (28, 28)
+    g = ops.ConvGeom(64, 224, 224, 3, 64, 7, 7, 2, 3)
+    assert (g.p, g.q) == (112, 112)
+
+
+def test_flat_params_layout():
+    from dfu_hip.optim import FlatParams
+    ps = [torch.nn.Parameter(torch.randn(n)) for n in (3, 8, 5, 1)]
+    vals = [p.detach().clone() for p in ps]
+    fp = FlatParams(ps)
+    for p, v, o in zip(ps, vals, fp.offsets):
+        assert o % 4 == 0  # 16-byte aligned views for the vectorised kernels
+        assert torch.equal(p.data, v)
+        assert p.data.data_ptr() == fp.data.data_ptr() + 4 * o
+        assert p.grad.data_ptr() == fp.grad.data_ptr() + 4 * o
+    assert fp.numel == 4 + 8 + 8 + 4
