@@ -76,12 +76,13 @@ def build(config, device):
     return model.to(device).train(), fwd
 
 
-def cpu_baseline(config, threads):
+def cpu_baseline(config, threads, budget_s=10.0):
     """The oracle (plain PyTorch fp32, oracle/torch_ref.py) timed on the host cores on a bounded
-    sample of the same workload: full train step (fwd+bwd+AdamW) at B=4, 1 warm-up + 2 timed."""
+    sample of the same workload: full train step (fwd+bwd+AdamW) at B=8, 1 warm-up, then timed
+    steps until ~budget_s of CPU work (at most 6)."""
     from oracle import torch_ref as R
     torch.set_num_threads(threads)
-    B = 4
+    B = 8
     torch.manual_seed(0)
     if config == "fusion":
         model = R.MultimodalFusionModel(num_classes=2, dropout=0.7)
@@ -105,14 +106,62 @@ def cpu_baseline(config, threads):
 
     step()
     t0 = time.perf_counter()
-    n = 2
-    for _ in range(n):
+    n = 0
+    while n < 6 and (n == 0 or time.perf_counter() - t0 < budget_s):
         step()
+        n += 1
     dt = time.perf_counter() - t0
     return {"value": round(B * n / dt, 3), "unit": "images/sec", "cores": threads,
             "kind": "port",
             "sample": f"oracle fp32 eager {config} train step (fwd+bwd+AdamW), batch {B}, "
-                      f"{n} timed steps after 1 warm-up, torch.set_num_threads({threads})"}
+                      f"{n} timed steps ({dt:.1f} s) after 1 warm-up, "
+                      f"torch.set_num_threads({threads})"}
+
+
+def gemm_traffic():
+    """HBM bytes per GEMM launch from the latest committed PMC measurement
+    (profiles/r*_gemm_traffic.json, written by tools/prof_summary.py from separate rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this bench; bench.py cannot read counters itself)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_gemm_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    return t["bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
+def gemm_roofline(fwd_bwd, tail, replays=3):
+    """Dominant kernel: the MFMA GEMM template (dfu_gemm: every ViT linear and ResNet conv, fwd,
+    dgrad and wgrad — all of the step's algorithmic GEMM/conv FLOPs except attention's QK^T/PV
+    and the fp32 head).  One eager step records every dfu_gemm launch (descriptor + live
+    buffers); the recorded launches are then replayed back-to-back on the same stream between
+    two HIP events, `replays` times.  achieved = algorithmic FLOPs / measured duration; the
+    per-launch average includes each launch's split-K slab reduction (rocprofv3 lists those as
+    k_splitk_reduce) and is what profiles/*_kernel_stats.md checks against rocprof."""
+    from dfu_hip import ops
+    ops.gemm_record = []
+    try:
+        fwd_bwd()
+        tail()
+        rec = ops.gemm_record
+    finally:
+        ops.gemm_record = None
+    torch.cuda.synchronize()
+    ops.gemm_replay(rec)  # warm
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(replays):
+        ops.gemm_replay(rec)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / replays  # per step
+    flops = sum(r[1] for r in rec)
+    nbytes = sum(r[2] for r in rec)
+    n = len(rec)
+    return {"launches_per_step": n, "avg_launch_us": us / n, "flops_per_launch": flops / n,
+            "bytes_per_launch": nbytes / n, "gemm_ms_per_step": us / 1e3,
+            "achieved": flops / (us * 1e-6) / 1e12}
 
 
 def main():
@@ -207,6 +256,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, gpu_s = t.tolist()
         gpu_ms = gpu_s * 1000.0
+    # every rank runs the instrumented steps (their all-reduces must pair up); rank 0 reports
+    opt.check_grads = True
+    gr = gemm_roofline(fwd_bwd, tail)
     imgs = args.batch * args.gpus * args.steps
     value = imgs / elapsed
     per_gpu_step_s = (gpu_ms / 1000.0) / args.steps
@@ -221,6 +273,7 @@ def main():
         metric = {"fusion": "images/sec (fusion fwd+bwd, bs=64/GPU)",
                   "thermal": "images/sec (thermal ViT-B/16 fwd+bwd, bs=64/GPU)",
                   "rgb": "images/sec (RGB ResNet50 fwd+bwd, bs=64/GPU)"}[args.config]
+        traffic, traffic_src = gemm_traffic()
         line = {
             "metric": metric,
             "value": round(value, 2),
@@ -241,12 +294,24 @@ def main():
                        "global_batch": args.batch * args.gpus, "per_gpu_batch": args.batch,
                        "image": 224, "parallelism": f"dp{args.gpus}",
                        "hip_graph": graph is not None},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
+            "roofline": {"bound": "mfma", "achieved": round(gr["achieved"], 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                         "basis": f"{FLOPS_PER_UNIT[args.config] / 1e9:.2f} GFLOP per image "
-                                  f"(SURVEY 8d) x {args.batch} per launch of the captured step / "
-                                  f"HIP-event step time {per_gpu_step_s * 1e3:.3f} ms"},
+                         "frac": round(gr["achieved"] / PEAK_BF16_TFLOPS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_unit": "bytes per launch (HBM, PMC)",
+                         "algorithmic_bytes_per_launch": round(gr["bytes_per_launch"]),
+                         "traffic_source": traffic_src,
+                         "kernel": "dfu gemm_kernel (MFMA bf16 GEMM template: all ViT linears "
+                                   "and implicit-GEMM convs, fwd/dgrad/wgrad)",
+                         "launches_per_step": gr["launches_per_step"],
+                         "avg_launch_us": round(gr["avg_launch_us"], 2),
+                         "gflop_per_launch": round(gr["flops_per_launch"] / 1e9, 4),
+                         "gemm_ms_per_step": round(gr["gemm_ms_per_step"], 3),
+                         "step": {"achieved": round(achieved, 1),
+                                  "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                                  "basis": f"{FLOPS_PER_UNIT[args.config] / 1e9:.2f} GFLOP per "
+                                           f"image pair (SURVEY 8d) x {args.batch} / HIP-event "
+                                           f"step time {per_gpu_step_s * 1e3:.3f} ms"}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -49,6 +49,35 @@ class ConvGeom:
 
 TILES = {"auto": 0, "128x128": 1, "256x128": 2, "128x256": 3, "256x256": 4}
 
+# Optional recording of GEMM launches (bench.py's roofline): when set to a list, every
+# dfu_gemm call appends (descriptor, algorithmic flops, tensors it touches) — the tensor
+# references keep the buffers alive so the launches can be replayed back-to-back later.
+# Never set inside graph capture.
+gemm_record = None
+
+
+def _algorithmic_bytes(d, conv):
+    """Compulsory HBM bytes of one launch: each operand tensor read once, C written once
+    (read too when accumulated), epilogue side inputs/outputs once."""
+    M, N, K = d.M, d.N, d.K
+    act_in = 2 * conv.n * conv.h * conv.w * conv.c if conv is not None else 0
+    a = {L.OPND_CONV_FWD: act_in,
+         L.OPND_CONV_DGRAD: 2 * conv.n * conv.p * conv.q * conv.k if conv is not None else 0
+         }.get(d.a_mode, 2 * M * K)
+    b = act_in if d.b_mode == L.OPND_CONV_WGRAD_X else 2 * N * K
+    e = d.epilogue
+    c = {L.EPI_F32: 4, L.EPI_F32_RESID: 8, L.EPI_F32_ACC: 8, L.EPI_PATCH: 4,
+         L.EPI_BF16_GELU: 4, L.EPI_BF16_DGELU: 4, L.EPI_BF16_ADD: 4}.get(e, 2) * M * N
+    return a + b + c
+
+
+def gemm_replay(records, stream=None):
+    """Re-issue recorded dfu_gemm launches (same descriptors) on the current stream."""
+    s = stream_ptr() if stream is None else stream
+    fn = lib().dfu_gemm
+    for d, _, _, _ in records:
+        check(fn(ctypes.byref(d), s), "dfu_gemm replay")
+
 
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
          epilogue=L.EPI_BF16, alpha=1.0, bias=None, aux=None, ldaux=0, aux_out=None,
@@ -88,6 +117,12 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
             d.workspace = workspace.data_ptr()
             d.workspace_bytes = int(need)
     check(lib().dfu_gemm(ctypes.byref(d), stream_ptr()), "dfu_gemm")
+    if gemm_record is not None:
+        flops = 2.0 * M * N * K
+        if a_mode == L.OPND_CONV_DGRAD and conv is not None:
+            flops /= conv.stride * conv.stride  # algorithmic: only the 1/stride^2 live taps
+        gemm_record.append((d, flops, _algorithmic_bytes(d, conv),
+                            (A, B, C, bias, aux, aux_out, stats, workspace)))
 
 
 def gemm_workspace_bytes(M, N, K, a_mode, b_mode, epilogue=L.EPI_F32_ACC, split_k=0, tile=0):

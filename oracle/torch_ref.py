@@ -38,23 +38,25 @@ import torch.nn.functional as F
 # and output), while accumulation stays fp32.  This is the "bf16-rounded oracle" of SURVEY.md
 # §7 (hard parts: report both the fp32-oracle and the bf16-rounded-oracle deltas).
 _EMU = False
+_EXACT_SITES = set()  # rounding sites left in fp32 (precision studies, tools/precision_study.py)
 
 
-def set_bf16_emulation(on):
-    global _EMU
+def set_bf16_emulation(on, exact_sites=()):
+    global _EMU, _EXACT_SITES
     _EMU = bool(on)
+    _EXACT_SITES = set(exact_sites)
 
 
-def rb(x):
-    return x.to(torch.bfloat16).float() if _EMU else x
+def rb(x, site=None):
+    return x.to(torch.bfloat16).float() if _EMU and site not in _EXACT_SITES else x
 
 
 def conv(x, w, stride=1, padding=0):
     return F.conv2d(rb(x), rb(w), stride=stride, padding=padding)
 
 
-def linear(x, lin):
-    return F.linear(rb(x), rb(lin.weight), lin.bias)
+def linear(x, lin, site=None):
+    return F.linear(rb(x, site), rb(lin.weight, site and site + "_w"), lin.bias)
 
 
 # ------------------------------------------------------------------ torchvision ResNet50
@@ -139,8 +141,46 @@ class PatchEmbed(nn.Module):
         self.norm = nn.Identity()
 
     def forward(self, x):
-        y = F.conv2d(rb(x), rb(self.proj.weight), self.proj.bias, stride=self.proj.stride)
+        y = F.conv2d(rb(x, "patch"), rb(self.proj.weight, "patch_w"), self.proj.bias,
+                     stride=self.proj.stride)
         return self.norm(y.flatten(2).transpose(1, 2))
+
+
+class _EmuAttention(torch.autograd.Function):
+    """bf16-emulated SDPA with the MI355X kernels' rounding points (dfu-multimodal_amd/csrc/
+    attn.hip): fp32 scores; forward P V with the unnormalised P rounded to bf16, output
+    normalised then rounded; backward P recomputed from the log-sum-exp, delta = rowsum(dO * O)
+    from the stored bf16 O, dV = bf16(P)^T dO, dS = P (dP - delta) rounded to bf16 before
+    dQ = dS K * scale and dK = dS^T Q * scale."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        s = q @ k.transpose(-1, -2)
+        mx = s.amax(-1, keepdim=True)
+        p = torch.exp((s - mx) * scale)
+        l = p.sum(-1, keepdim=True)
+        o = rb((rb(p, "p") @ v) / l, "attn_out")
+        lse = mx * scale + torch.log(l)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.scale = scale
+        ctx.exact = None if _EMU else "all"  # rounding state captured at forward time
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        scale = ctx.scale
+
+        def r(x, site):
+            exact = ctx.exact == "all" or site in _EXACT_SITES
+            return x if exact else x.to(torch.bfloat16).float()
+        p = torch.exp(q @ k.transpose(-1, -2) * scale - lse)
+        delta = (do * o).sum(-1, keepdim=True)
+        dv = r(p, "p").transpose(-1, -2) @ do
+        ds = r(p * (do @ v.transpose(-1, -2) - delta), "ds")
+        dq = (ds @ k) * scale
+        dk = (ds.transpose(-1, -2) @ q) * scale
+        return dq, dk, dv, None
 
 
 class Attention(nn.Module):
@@ -154,16 +194,13 @@ class Attention(nn.Module):
 
     def forward(self, x):
         B, N, C = x.shape
-        qkv = rb(linear(x, self.qkv)).reshape(B, N, 3, self.num_heads, self.head_dim)
+        qkv = rb(linear(x, self.qkv, "ln1"), "qkv").reshape(B, N, 3, self.num_heads, self.head_dim)
         q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
         if _EMU:
-            # the HIP kernel: fp32 scores, unnormalised exp rounded to bf16 for P V, fp32 sum
-            s = (q @ k.transpose(-1, -2)) * self.scale
-            p = torch.exp(s - s.amax(-1, keepdim=True))
-            x = rb((rb(p) @ v) / p.sum(-1, keepdim=True))
+            x = _EmuAttention.apply(q, k, v, self.scale)
         else:
             x = F.scaled_dot_product_attention(q, k, v)
-        return linear(x.transpose(1, 2).reshape(B, N, C), self.proj)
+        return linear(x.transpose(1, 2).reshape(B, N, C), self.proj, "attn_out")
 
 
 class Mlp(nn.Module):
@@ -174,7 +211,7 @@ class Mlp(nn.Module):
         self.fc2 = nn.Linear(hidden, dim)
 
     def forward(self, x):
-        return linear(rb(self.act(linear(x, self.fc1))), self.fc2)
+        return linear(rb(self.act(linear(x, self.fc1, "ln2")), "gelu"), self.fc2, "gelu")
 
 
 class Block(nn.Module):
@@ -186,8 +223,8 @@ class Block(nn.Module):
         self.mlp = Mlp(dim, dim * 4)
 
     def forward(self, x):
-        x = x + self.attn(rb(self.norm1(x)))
-        return x + self.mlp(rb(self.norm2(x)))
+        x = x + self.attn(rb(self.norm1(x), "ln1"))
+        return x + self.mlp(rb(self.norm2(x), "ln2"))
 
 
 class VisionTransformer(nn.Module):
