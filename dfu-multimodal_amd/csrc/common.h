@@ -57,11 +57,33 @@ DFU_DEV float wave_max(float v) {
 }
 
 // Exact (erf) GELU as timm's nn.GELU default, and its derivative.
-DFU_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// Exact-erf GELU (timm nn.GELU default) for GEMM epilogues.  Phi(u) = 0.5 erfc(-u/sqrt2) with
+// Abramowitz & Stegun 7.1.26: erfc(z) = t (a1 + t (a2 + t (a3 + t (a4 + t a5)))) exp(-z^2),
+// t = 1 / (1 + p z), z = |u|/sqrt2 >= 0; Phi(u) = tail for u < 0, 1 - tail otherwise, with
+// tail = 0.5 erfc(z) (no cancellation on the negative side).  |Phi error| <= 3e-7; relative
+// error of GELU stays below bf16's half-ulp except where |GELU(u)| < 4e-7 (u < -5.25).
+// exp(-z^2) = exp(-u^2/2) is also the Gaussian pdf's exponential, so GELU and its derivative
+// cost one v_exp_f32, one v_rcp_f32 and a few FMAs (OCML erff branches per magnitude range).
+struct CdfPdf {
+  float cdf, pdf;
+};
+DFU_DEV CdfPdf gauss_cdf_pdf(float u) {
+  const float z = fabsf(u) * 0.70710678118654752f;
+  const float e = __expf(-0.5f * u * u);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f),
+                       -0.284496736f), 0.254829592f);
+  const float tail = 0.5f * poly * e;  // Phi(-|u|)
+  CdfPdf r;
+  r.cdf = u < 0.f ? tail : 1.0f - tail;
+  r.pdf = 0.39894228040143268f * e;
+  return r;
+}
+DFU_DEV float gelu_f(float x) { return x * gauss_cdf_pdf(x).cdf; }
 DFU_DEV float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  const CdfPdf c = gauss_cdf_pdf(x);
+  return c.cdf + x * c.pdf;
 }
 
 // Unsigned division by a runtime constant d >= 1 (Granlund-Montgomery, exact for every

@@ -12,11 +12,15 @@ namespace {
 constexpr int kCUs = 256;
 constexpr int kTM[NTILES] = {128, 256, 128, 256};
 constexpr int kTN[NTILES] = {128, 128, 256, 256};
-// Relative MFMA throughput per tile area (measured on MI355X, tools/gemm_bench.py).
-constexpr double kEff[NTILES] = {1.0, 1.25, 1.25, 1.45};
-constexpr double kStepUs = 0.55;        // one 128x128x64 K-step at kEff = 1
-constexpr double kRoundOverheadUs = 3.0;  // prologue fill + epilogue per workgroup round
-constexpr double kSlabGBs = 4500.0;      // fp32 slab write + reduce read rate
+// Wave-quantisation cost model: a launch takes ceil(tiles * splits / 256) rounds (one 512-thread
+// workgroup per CU), each costing kRoundUs (prologue fill + epilogue) + k-steps * kStepUs.
+// Fitted on MI355X to tools/gemm_bench.py --sweep (ViT qkv K=768 vs fc2 K=3072 forward rows,
+// r01): 128x128 0.57 us/step + 4.8 us/round ... 256x256 1.41 us/step + 13.9 us/round, i.e.
+// 256x256 moves 1.62x more MFMA work per microsecond than 128x128.
+constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41};
+constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9};
+constexpr double kSlabGBs = 5000.0;  // split-K: slab write + reduce (read slabs, RMW C)
+constexpr double kReduceLaunchUs = 2.0;
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256};
@@ -56,9 +60,9 @@ Plan plan_gemm(const dfu_gemm_desc* d) {
       const int se = cdiv(ktiles, kps);
       if (se != s && s != s_lo) continue;
       const int rounds = cdiv(tiles * se, kCUs);
-      double cost = rounds * (kps * kStepUs * (kTM[t] * kTN[t]) / (128.0 * 128.0) / kEff[t] +
-                              kRoundOverheadUs);
-      if (se > 1) cost += 8.0 * se * (double)d->M * d->N / (kSlabGBs * 1e3);
+      double cost = rounds * (kRoundUs[t] + kps * kStepUs[t]);
+      if (se > 1)
+        cost += kReduceLaunchUs + 4.0 * (se + 2) * (double)d->M * d->N / (kSlabGBs * 1e3);
       if (cost < best.cost) {
         best.cost = cost;
         best.entry = en;
@@ -110,6 +114,18 @@ extern "C" int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* d) {
   if (!d || d->epilogue != DFU_EPI_F32_ACC) return 0;
   const Plan pl = plan_gemm(d);
   return pl.entry && pl.split > 1 ? (int64_t)pl.split * d->M * d->N * 4 : 0;
+}
+
+extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* split_k) {
+  DFU_CHECK_ARG(d != nullptr && tile != nullptr && split_k != nullptr, "dfu_gemm_plan: null");
+  const Plan pl = plan_gemm(d);
+  if (!pl.entry) {
+    dfu_set_error("dfu_gemm_plan: unsupported combination");
+    return DFU_E_UNSUPPORTED;
+  }
+  *tile = pl.tile + 1;
+  *split_k = pl.split;
+  return DFU_OK;
 }
 
 extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {

@@ -64,15 +64,16 @@ __global__ void k_ln_bwd(const void* __restrict__ dyv, int64_t lddy, const float
                          int64_t ldx, const float* __restrict__ mean_in,
                          const float* __restrict__ rstd_in, const float* __restrict__ gamma,
                          int rows, int D, float* __restrict__ gx, int64_t ldg,
-                         bf16_t* __restrict__ gx_bf, float* __restrict__ partial) {
-  __shared__ float red[2][4][1024];
+                         bf16_t* __restrict__ gx_bf, float* __restrict__ partial,
+                         float* __restrict__ gsum_partial) {
+  __shared__ float red[3][4][1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = D / 4;
-  float dg[MAXV][4], db[MAXV][4];
+  float dg[MAXV][4], db[MAXV][4], gs[MAXV][4];
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { dg[i][e] = 0.f; db[i][e] = 0.f; }
+    for (int e = 0; e < 4; ++e) { dg[i][e] = 0.f; db[i][e] = 0.f; gs[i][e] = 0.f; }
   f32x4 gm[MAXV];
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
@@ -120,7 +121,10 @@ __global__ void k_ln_bwd(const void* __restrict__ dyv, int64_t lddy, const float
       float* g = gx + (int64_t)row * ldg + 4 * j;
       f32x4 gv = *(f32x4*)g;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) gv[e] += rs * (dy[i][e] * gm[i][e] - s1 - xh[i][e] * s2);
+      for (int e = 0; e < 4; ++e) {
+        gv[e] += rs * (dy[i][e] * gm[i][e] - s1 - xh[i][e] * s2);
+        gs[i][e] += gv[e];
+      }
       *(f32x4*)g = gv;
       if (gx_bf) {
         bf16_t* gb = gx_bf + (int64_t)row * ldg + 4 * j;
@@ -134,9 +138,17 @@ __global__ void k_ln_bwd(const void* __restrict__ dyv, int64_t lddy, const float
     const int j = lane + 64 * i;
     if (j < nv)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { red[0][wave][4 * j + e] = dg[i][e]; red[1][wave][4 * j + e] = db[i][e]; }
+      for (int e = 0; e < 4; ++e) {
+        red[0][wave][4 * j + e] = dg[i][e];
+        red[1][wave][4 * j + e] = db[i][e];
+        red[2][wave][4 * j + e] = gs[i][e];
+      }
   }
   __syncthreads();
+  if (gsum_partial)  // column sums of the updated residual gradient (the upstream bias grad)
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+      gsum_partial[(int64_t)blockIdx.x * D + d] =
+          red[2][0][d] + red[2][1][d] + red[2][2][d] + red[2][3][d];
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     partial[((int64_t)blockIdx.x * 2 + 0) * D + d] =
         red[0][0][d] + red[0][1][d] + red[0][2][d] + red[0][3][d];
@@ -170,7 +182,8 @@ extern "C" int dfu_ln_bwd_blocks(int32_t rows) { return (rows + LNB_ROWS - 1) / 
 extern "C" int dfu_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_bf16, const float* x,
                                  int64_t ldx, const float* mean, const float* rstd,
                                  const float* gamma, int32_t rows, int32_t D, float* gx,
-                                 int64_t ldg, void* gx_bf16, float* partial, void* stream) {
+                                 int64_t ldg, void* gx_bf16, float* partial, float* gsum_partial,
+                                 void* stream) {
   DFU_CHECK_ARG(dy && x && mean && rstd && gamma && gx && partial && rows > 0 && D % 4 == 0 &&
                     D <= 1024,
                 "dfu_layernorm_bwd: bad args");
@@ -178,10 +191,10 @@ extern "C" int dfu_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_bf16, 
   dim3 grid(dfu_ln_bwd_blocks(rows));
   if (dy_bf16)
     hipLaunchKernelGGL(k_ln_bwd<true>, grid, dim3(256), 0, (hipStream_t)stream, dy, lddy, x, ldx,
-                       mean, rstd, gamma, rows, D, gx, ldg, (bf16_t*)gx_bf16, partial);
+                       mean, rstd, gamma, rows, D, gx, ldg, (bf16_t*)gx_bf16, partial, gsum_partial);
   else
     hipLaunchKernelGGL(k_ln_bwd<false>, grid, dim3(256), 0, (hipStream_t)stream, dy, lddy, x, ldx,
-                       mean, rstd, gamma, rows, D, gx, ldg, (bf16_t*)gx_bf16, partial);
+                       mean, rstd, gamma, rows, D, gx, ldg, (bf16_t*)gx_bf16, partial, gsum_partial);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

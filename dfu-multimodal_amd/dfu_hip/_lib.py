@@ -65,7 +65,9 @@ PROTOTYPES = {
     "dfu_gemm": [ctypes.POINTER(GemmDesc), P],
     "dfu_gemm_stats_tiles": [I32],
     "dfu_gemm_workspace_bytes": [ctypes.POINTER(GemmDesc)],
-    "dfu_gemm_f32": [I32, I32, I32, P, I64, I64, P, I64, I64, P, I64, P, I32, I32, P],
+    "dfu_gemm_plan": [ctypes.POINTER(GemmDesc), ctypes.POINTER(c_int32), ctypes.POINTER(c_int32)],
+    "dfu_gemm_f32": [I32, I32, I32, P, I64, I64, P, I64, I64, P, I64, P, I32, I32, P, I64, P],
+    "dfu_gemm_f32_workspace_bytes": [I32, I32, I32],
     "dfu_pack_conv_weight": [P, P, I32, I32, I32, I32, P],
     "dfu_conv_grad_krsc_to_oihw": [P, P, I32, I32, I32, I32, P],
     "dfu_cast_rows_bf16": [P, I64, P, I64, I32, I32, P],
@@ -85,7 +87,7 @@ PROTOTYPES = {
     "dfu_avgpool_bwd": [P, I32, I32, I32, P, P],
     "dfu_layernorm_fwd": [P, I64, I32, I32, P, P, F, P, I64, I32, P, P, P],
     "dfu_ln_bwd_blocks": [I32],
-    "dfu_layernorm_bwd": [P, I64, I32, P, I64, P, P, P, I32, I32, P, I64, P, P, P],
+    "dfu_layernorm_bwd": [P, I64, I32, P, I64, P, P, P, I32, I32, P, I64, P, P, P, P],
     "dfu_reduce_partials": [P, I32, I32, I32, P, P, P],
     "dfu_attention_fwd": [P, I32, I32, I32, I32, F, P, P, P],
     "dfu_attention_bwd": [P, P, P, P, I32, I32, I32, I32, F, P, P, P],
@@ -109,7 +111,8 @@ PROTOTYPES = {
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
 }
-_RESTYPE = {"dfu_last_error_string": c_char_p, "dfu_gemm_workspace_bytes": c_int64}
+_RESTYPE = {"dfu_last_error_string": c_char_p, "dfu_gemm_workspace_bytes": c_int64,
+            "dfu_gemm_f32_workspace_bytes": c_int64}
 
 
 def header_symbols(path=HEADER_PATH):

@@ -445,11 +445,22 @@ def _ln_fwd(x2d, norm, rows, D, out_bf):
     return mean, rstd
 
 
-def _ln_bwd(dy_bf, x2d, mean, rstd, norm, rows, D, g, g_bf):
-    ops.layernorm_bwd(dy_bf, D, True, x2d, D, mean, rstd, norm.weight, rows, D, g, D, g_bf,
-                      grad_buffer(norm.weight) if _wants(norm.weight) else None,
-                      grad_buffer(norm.bias) if _wants(norm.bias) else None)
+def _ln_bwd(dy_bf, x2d, mean, rstd, norm, rows, D, g, g_bf, gsum=False):
+    gsp = ops.layernorm_bwd(dy_bf, D, True, x2d, D, mean, rstd, norm.weight, rows, D, g, D, g_bf,
+                            grad_buffer(norm.weight) if _wants(norm.weight) else None,
+                            grad_buffer(norm.bias) if _wants(norm.bias) else None, gsum=gsum)
     grads_done(norm.weight, norm.bias)
+    return gsp
+
+
+def _colsum_of_grad(g, out):
+    """out += column sums of an fp32 residual-stream gradient: from the partial sums its
+    producing LayerNorm backward emitted (stashed on the tensor), else a colsum pass."""
+    gsp = getattr(g, "_dfu_colsum", None)
+    if gsp is not None:
+        ops.reduce_partials_add(gsp, out)
+    else:
+        ops.colsum_add(g.reshape(-1, g.shape[-1]), out)
 
 
 def _bf16_of_grad(g):
@@ -528,7 +539,7 @@ class ViTBlockFn(torch.autograd.Function):
         if _wants(mlp.fc2.weight):
             _linear_wgrad(gb, h, mlp.fc2.weight, rows)
         if _wants(mlp.fc2.bias):
-            ops.colsum_add(g2, grad_buffer(mlp.fc2.bias))
+            _colsum_of_grad(g, grad_buffer(mlp.fc2.bias))
         grads_done(mlp.fc2.weight, mlp.fc2.bias)
         dxn2 = _empty((rows, D), BF16, dev)
         ops.gemm(rows, D, Dh, dh_pre, Dh, wfc1, D, dxn2, D, b_mode=L.OPND_MNMAJOR,
@@ -539,14 +550,15 @@ class ViTBlockFn(torch.autograd.Function):
             ops.colsum_add(dh_pre, grad_buffer(mlp.fc1.bias))
         grads_done(mlp.fc1.weight, mlp.fc1.bias)
         gmb = _empty((rows, D), BF16, dev)
-        _ln_bwd(dxn2, xm, m2, r2, blk.norm2, rows, D, g2, gmb)  # g2 := g_mid (in place)
+        gsp = _ln_bwd(dxn2, xm, m2, r2, blk.norm2, rows, D, g2, gmb,
+                      gsum=_wants(attn.proj.bias))  # g2 := g_mid (in place)
         # ---- attention branch: x_mid = x_in + proj(attn(norm1(x_in)))
         do = _empty((rows, D), BF16, dev)
         ops.gemm(rows, D, D, gmb, D, wproj, D, do, D, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16)
         if _wants(attn.proj.weight):
             _linear_wgrad(gmb, o, attn.proj.weight, rows)
         if _wants(attn.proj.bias):
-            ops.colsum_add(g2, grad_buffer(attn.proj.bias))
+            ops.reduce_partials_add(gsp, grad_buffer(attn.proj.bias))
         grads_done(attn.proj.weight, attn.proj.bias)
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, T, H, dh, attn.scale)
         dxn1 = _empty((rows, D), BF16, dev)
@@ -558,9 +570,11 @@ class ViTBlockFn(torch.autograd.Function):
             ops.colsum_add(dqkv, grad_buffer(attn.qkv.bias))
         grads_done(attn.qkv.weight, attn.qkv.bias)
         gib = _empty((B, T, D), BF16, dev)
-        _ln_bwd(dxn1, x2, m1, r1, blk.norm1, rows, D, g2, gib.view(rows, D))  # g2 := g_in
+        gsp = _ln_bwd(dxn1, x2, m1, r1, blk.norm1, rows, D, g2, gib.view(rows, D),
+                      gsum=True)  # g2 := g_in
         gin = g.view(B, T, D)
         gin._dfu_bf16 = gib
+        gin._dfu_colsum = gsp  # the previous block's fc2.bias gradient, pre-reduced
         n_params = len(ctx.needs_input_grad) - 2
         return (gin,) + (None,) * n_params + (None,)
 
@@ -592,11 +606,12 @@ class TokenNormFn(torch.autograd.Function):
         ops.zero_(gx)
         gxb = _empty((B, T, D), BF16, x.device)
         ops.zero_(gxb)
-        ops.layernorm_bwd(g, D, False, x, T * D, mean, rstd, norm.weight, B, D, gx, T * D, gxb,
-                          grad_buffer(norm.weight) if _wants(norm.weight) else None,
-                          grad_buffer(norm.bias) if _wants(norm.bias) else None)
+        gsp = ops.layernorm_bwd(g, D, False, x, T * D, mean, rstd, norm.weight, B, D, gx, T * D,
+                                gxb, grad_buffer(norm.weight) if _wants(norm.weight) else None,
+                                grad_buffer(norm.bias) if _wants(norm.bias) else None, gsum=True)
         grads_done(norm.weight, norm.bias)
         gx._dfu_bf16 = gxb
+        gx._dfu_colsum = gsp  # only the class-token rows are non-zero: their sums are the total
         return gx, None, None, None
 
 

@@ -125,19 +125,34 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
                             (A, B, C, bias, aux, aux_out, stats, workspace)))
 
 
-def gemm_workspace_bytes(M, N, K, a_mode, b_mode, epilogue=L.EPI_F32_ACC, split_k=0, tile=0):
+def _plan_desc(M, N, K, a_mode, b_mode, epilogue, split_k, tile):
     d = L.GemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
     d.a_mode, d.b_mode, d.epilogue = int(a_mode), int(b_mode), int(epilogue)
     d.split_k, d.tile = int(split_k), int(tile)
+    return d
+
+
+def gemm_workspace_bytes(M, N, K, a_mode, b_mode, epilogue=L.EPI_F32_ACC, split_k=0, tile=0):
+    d = _plan_desc(M, N, K, a_mode, b_mode, epilogue, split_k, tile)
     return int(lib().dfu_gemm_workspace_bytes(ctypes.byref(d)))
 
 
+def gemm_plan(M, N, K, a_mode, b_mode, epilogue, split_k=0, tile=0):
+    """(tile id 1..4, split-K) the library's cost model picks."""
+    d = _plan_desc(M, N, K, a_mode, b_mode, epilogue, split_k, tile)
+    t, sk = ctypes.c_int32(), ctypes.c_int32()
+    check(lib().dfu_gemm_plan(ctypes.byref(d), ctypes.byref(t), ctypes.byref(sk)), "dfu_gemm_plan")
+    return t.value, sk.value
+
+
 def gemm_f32(M, N, K, A, sam, sak, B, sbn, sbk, C, ldc, bias=None, relu=False, accumulate=False):
-    """Exact fp32 strided GEMM (fusion head)."""
+    """Exact fp32 strided GEMM (fusion head); split-K slabs from the caching allocator."""
+    need = lib().dfu_gemm_f32_workspace_bytes(int(M), int(N), int(K))
+    ws = torch.empty(need, dtype=torch.uint8, device=C.device) if need > 0 else None
     check(lib().dfu_gemm_f32(int(M), int(N), int(K), ptr(A), int(sam), int(sak), ptr(B), int(sbn),
                              int(sbk), ptr(C), int(ldc), ptr(bias), int(relu), int(accumulate),
-                             stream_ptr()), "dfu_gemm_f32")
+                             ptr(ws), int(need), stream_ptr()), "dfu_gemm_f32")
 
 
 def stats_tiles(M):
@@ -285,16 +300,27 @@ def layernorm_fwd(x, ldx, rows, D, gamma, beta, eps, out, ldo, out_bf16, mean, r
 
 
 def layernorm_bwd(dy, lddy, dy_bf16, x, ldx, mean, rstd, gamma, rows, D, gx, ldg, gx_bf16,
-                  dgamma, dbeta):
+                  dgamma, dbeta, gsum=False):
+    """LayerNorm backward (gx += dx).  With gsum=True also returns the [blocks][D] partial
+    column sums of the updated gx (reduce with reduce_partials_add)."""
     blocks = lib().dfu_ln_bwd_blocks(rows)
     partial = torch.empty((blocks, 2, D), dtype=F32, device=x.device)
+    gsp = torch.empty((blocks, D), dtype=F32, device=x.device) if gsum else None
     s = stream_ptr()
     check(lib().dfu_layernorm_bwd(ptr(dy), lddy, int(dy_bf16), ptr(x), ldx, ptr(mean), ptr(rstd),
                                   ptr(gamma), rows, D, ptr(gx), ldg, ptr(gx_bf16), ptr(partial),
-                                  s), "dfu_layernorm_bwd")
+                                  ptr(gsp), s), "dfu_layernorm_bwd")
     if dgamma is not None or dbeta is not None:
         check(lib().dfu_reduce_partials(ptr(partial), blocks, 2, D, ptr(dgamma), ptr(dbeta), s),
               "dfu_reduce_partials")
+    return gsp
+
+
+def reduce_partials_add(partial, out):
+    """out[d] += sum_b partial[b][d]."""
+    blocks, D = partial.shape
+    check(lib().dfu_reduce_partials(ptr(partial), blocks, 1, D, ptr(out), None, stream_ptr()),
+          "dfu_reduce_partials")
 
 
 # ----------------------------------------------------------------------------- attention

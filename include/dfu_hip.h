@@ -97,11 +97,17 @@ int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
 int dfu_gemm_stats_tiles(int32_t M);
 /* Workspace bytes for deterministic split-K slabs of this descriptor (0 if not split). */
 int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* desc);
+/* The tile (1..4, as dfu_gemm_desc.tile) and split-K the cost model picks for this descriptor. */
+int dfu_gemm_plan(const dfu_gemm_desc* desc, int32_t* tile, int32_t* split_k);
 /* Exact fp32 GEMM for the tiny fusion head (train_multimodal_fusion.py:305-313):
  * C[m][n] = accumulate*C[m][n] + sum_k A[m*sam + k*sak] * B[n*sbn + k*sbk] (+bias[n]) (relu). */
 int dfu_gemm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t sam, int64_t sak,
                  const float* B, int64_t sbn, int64_t sbk, float* C, int64_t ldc,
-                 const float* bias, int32_t relu, int32_t accumulate, void* stream);
+                 const float* bias, int32_t relu, int32_t accumulate, void* workspace,
+                 int64_t workspace_bytes, void* stream);
+/* Workspace for dfu_gemm_f32's deterministic split-K slabs (0 = runs unsplit). With a smaller
+ * or NULL workspace dfu_gemm_f32 runs unsplit (correct, slower). */
+int64_t dfu_gemm_f32_workspace_bytes(int32_t M, int32_t N, int32_t K);
 
 /* ---------------------------------------------------------------- layout / packing -- */
 /* fp32 OIHW conv weight -> bf16 KRSC ([K][R][S][C]) for the implicit-GEMM convs
@@ -178,12 +184,15 @@ int dfu_layernorm_fwd(const float* x, int64_t ldx, int32_t rows, int32_t D, cons
                       const float* beta, float eps, void* out, int64_t ldo, int32_t out_bf16,
                       float* mean, float* rstd, void* stream);
 /* dx (fp32, += into gx which is also read as the incoming residual grad) and a bf16 copy of
- * the updated residual grad; dgamma/dbeta partials [blocks][2][D] (dfu_ln_bwd_blocks). */
+ * the updated residual grad; dgamma/dbeta partials [blocks][2][D] (dfu_ln_bwd_blocks).
+ * gsum_partial (optional, [blocks][D]): column sums of the UPDATED gx — the bias gradient of
+ * the Linear whose output is that residual stream (timm Block proj / fc2), so no separate
+ * pass over the fp32 gradient is needed. */
 int dfu_ln_bwd_blocks(int32_t rows);
 int dfu_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_bf16, const float* x,
                       int64_t ldx, const float* mean, const float* rstd, const float* gamma,
                       int32_t rows, int32_t D, float* gx, int64_t ldg, void* gx_bf16,
-                      float* partial, void* stream);
+                      float* partial, float* gsum_partial, void* stream);
 /* Sum a [blocks][nvec][D] partial slab over blocks and ADD into out[v] (v < nvec). */
 int dfu_reduce_partials(const float* partial, int32_t blocks, int32_t nvec, int32_t D,
                         float* out0, float* out1, void* stream);

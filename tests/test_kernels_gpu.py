@@ -305,8 +305,12 @@ def test_layernorm_fwd_bwd():
     gxb = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
     dgam = torch.zeros(D, device=DEV)
     dbet = torch.zeros(D, device=DEV)
-    ops.layernorm_bwd(dy, D, True, x, D, mean, rstd, gamma, rows, D, gx, D, gxb, dgam, dbet)
+    gsp = ops.layernorm_bwd(dy, D, True, x, D, mean, rstd, gamma, rows, D, gx, D, gxb, dgam, dbet,
+                            gsum=True)
     close(gx, gx0 + xr.grad, atol=1e-3, rtol=1e-3, what="ln dx")
+    gsum = torch.zeros(D, device=DEV)
+    ops.reduce_partials_add(gsp, gsum)
+    close(gsum, gx.sum(0), atol=1e-3, rtol=1e-4, what="ln updated-gradient column sums")
     close(gxb, gx, atol=2e-2, rtol=1e-2, what="ln dx bf16")
     close(dgam, gr.grad, atol=1e-2, rtol=1e-3, what="ln dgamma")
     close(dbet, br.grad, atol=1e-2, rtol=1e-3, what="ln dbeta")
