@@ -10,21 +10,26 @@ using namespace dfu;
 namespace {
 
 constexpr int kCUs = 256;
-constexpr int kTM[NTILES] = {128, 256, 128, 256};
-constexpr int kTN[NTILES] = {128, 128, 256, 256};
+constexpr int kTM[NTILES] = {128, 256, 128, 256, 128};
+constexpr int kTN[NTILES] = {128, 128, 256, 256, 128};
+constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2};  // workgroups per CU
 // Wave-quantisation cost model: a launch takes ceil(tiles * splits / 256) rounds (one 512-thread
 // workgroup per CU), each costing kRoundUs (prologue fill + epilogue) + k-steps * kStepUs.
 // Fitted on MI355X to tools/gemm_bench.py --sweep (ViT qkv K=768 vs fc2 K=3072 forward rows,
 // r01): 128x128 0.57 us/step + 4.8 us/round ... 256x256 1.41 us/step + 13.9 us/round, i.e.
 // 256x256 moves 1.62x more MFMA work per microsecond than 128x128.
-constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41};
-constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9};
+// The 2-per-CU 128x128 variant: two co-resident workgroups share the MFMA pipe (step cost per
+// workgroup ~doubles) but hide each other's fill and epilogue.
+constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70};
+constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1};
 constexpr double kSlabGBs = 5000.0;  // split-K: slab write + reduce (read slabs, RMW C)
 constexpr double kReduceLaunchUs = 2.0;
 
 const Entry* find_entry(int a, int b, int e, int tile) {
-  const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256};
-  const int ns[NTILES] = {kTable128x128N, kTable256x128N, kTable128x256N, kTable256x256N};
+  const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
+                               kTable128x128o2};
+  const int ns[NTILES] = {kTable128x128N, kTable256x128N, kTable128x256N, kTable256x256N,
+                          kTable128x128o2N};
   for (int i = 0; i < ns[tile]; ++i) {
     const Entry& en = tabs[tile][i];
     if (en.a == a && en.b == b && en.e == e) return &en;
@@ -41,8 +46,43 @@ struct Plan {
   double cost = 1e30;
 };
 
+// Offline-tuned plans (tools/gemm_tune.py on MI355X: every distinct GEMM of the training step,
+// all tiles x split-K candidates timed, fastest kept) take precedence over the cost model.
+struct TunedPlan {
+  int a, b, e, M, N, K, cn, ch, cw, cc, ck, cr, cs, cstride, cpad;
+  int tile, split;  // tile id 1..NTILES, split-K (1 = none)
+};
+const TunedPlan kTuned[] = {
+#include "gemm_tuned.inc"
+    {-1, -1, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
+
+const TunedPlan* find_tuned(const dfu_gemm_desc* d) {
+  const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
+  for (const TunedPlan& t : kTuned) {
+    if (t.a != d->a_mode || t.b != d->b_mode || t.e != d->epilogue || t.M != d->M ||
+        t.N != d->N || t.K != d->K)
+      continue;
+    if (conv && (t.cn != d->conv_n || t.ch != d->conv_h || t.cw != d->conv_w ||
+                 t.cc != d->conv_c || t.ck != d->conv_k || t.cr != d->conv_r ||
+                 t.cs != d->conv_s || t.cstride != d->conv_stride || t.cpad != d->conv_pad))
+      continue;
+    return &t;
+  }
+  return nullptr;
+}
+
 Plan plan_gemm(const dfu_gemm_desc* d) {
   const bool acc_epi = d->epilogue == DFU_EPI_F32_ACC;
+  if (d->tile == 0 && d->split_k == 0) {
+    if (const TunedPlan* tp = find_tuned(d)) {
+      Plan pl;
+      pl.tile = tp->tile - 1;
+      pl.entry = find_entry(d->a_mode, d->b_mode, d->epilogue, pl.tile);
+      pl.split = acc_epi ? tp->split : 1;
+      pl.cost = 0.0;
+      if (pl.entry) return pl;
+    }
+  }
   const int ktiles = cdiv(d->K, BK);
   Plan best;
   for (int t = 0; t < NTILES; ++t) {
@@ -53,13 +93,13 @@ Plan plan_gemm(const dfu_gemm_desc* d) {
     int s_lo = 1, s_hi = 1;
     if (acc_epi) {
       if (d->split_k > 0) s_lo = s_hi = d->split_k;
-      else s_hi = ktiles < 32 ? ktiles : 32;
+      else s_hi = ktiles < 256 ? ktiles : 256;  // long-K weight gradients: up to 1 split per CU
     }
     for (int s = s_lo; s <= s_hi; ++s) {
       const int kps = cdiv(ktiles, s);
       const int se = cdiv(ktiles, kps);
       if (se != s && s != s_lo) continue;
-      const int rounds = cdiv(tiles * se, kCUs);
+      const int rounds = cdiv(tiles * se, kCUs * kOcc[t]);
       double cost = rounds * (kRoundUs[t] + kps * kStepUs[t]);
       if (se > 1)
         cost += kReduceLaunchUs + 4.0 * (se + 2) * (double)d->M * d->N / (kSlabGBs * 1e3);

@@ -21,9 +21,11 @@ namespace dfu {
 constexpr int BK = 64, NT = 512, NWAVE = 8;
 constexpr int LDS_MAX = 160 * 1024;
 
-template <int TM_, int TN_>
+// OCC = workgroups per CU the variant is built for (launch bounds); OCC 2 forces a 2-stage
+// ring so two workgroups' LDS fit (their prologues/epilogues overlap each other's main loop).
+template <int TM_, int TN_, int OCC_ = 1>
 struct Tile {
-  static constexpr int TM = TM_, TN = TN_;
+  static constexpr int TM = TM_, TN = TN_, OCC = OCC_;
   static constexpr int WGM = (TM == 256 && TN == 128) ? 4 : 2;  // wave grid
   static constexpr int WGN = NWAVE / WGM;
   static constexpr int WTM = TM / WGM, WTN = TN / WGN;         // per-wave sub-tile
@@ -31,9 +33,10 @@ struct Tile {
   static constexpr int NLDA = TM / 64, NLDB = TN / 64;         // DMA instructions per thread
   static constexpr int A_BYTES = TM * BK * 2, B_BYTES = TN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  static constexpr int NSTAGE = 3 * STAGE_BYTES <= LDS_MAX ? 3 : 2;
+  static constexpr int NSTAGE = (OCC == 1 && 3 * STAGE_BYTES <= LDS_MAX) ? 3 : 2;
   static constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES;
   static constexpr int DMA_PER_STAGE = NLDA + NLDB;
+  static_assert(OCC * LDS_BYTES <= LDS_MAX, "LDS for the requested occupancy");
 };
 
 struct GemmArgs {
@@ -288,9 +291,9 @@ DFU_DEV void wait_vmcnt() {
 }
 
 // ------------------------------------------------------------------------------ kernel
-template <int AMODE, int BMODE, int EPI, int TM, int TN>
-__global__ __launch_bounds__(NT, 1) void gemm_kernel(const GemmArgs p) {
-  using T = Tile<TM, TN>;
+template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1>
+__global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
+  using T = Tile<TM, TN, OCC>;
   constexpr int WGM = T::WGM, WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
   constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
   __shared__ __attribute__((aligned(16))) char smem[T::LDS_BYTES];

@@ -9,7 +9,7 @@ struct Entry {
   gemm_fn fn;
   int lds_bytes;
 };
-enum TileId { T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, NTILES = 4 };
+enum TileId { T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, T128x128o2 = 4, NTILES = 5 };
 extern const Entry kTable128x128[];
 extern const int kTable128x128N;
 extern const Entry kTable256x128[];
@@ -18,7 +18,14 @@ extern const Entry kTable128x256[];
 extern const int kTable128x256N;
 extern const Entry kTable256x256[];
 extern const int kTable256x256N;
+extern const Entry kTable128x128o2[];
+extern const int kTable128x128o2N;
 }  // namespace dfu
 
 #define DFU_ENTRY(A, B, E, TMv, TNv, TID) \
   { A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv>, dfu::Tile<TMv, TNv>::LDS_BYTES }
+#define DFU_ENTRY_OCC(A, B, E, TMv, TNv, OCCv, TID)                       \
+  {                                                                       \
+    A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv, OCCv>,             \
+        dfu::Tile<TMv, TNv, OCCv>::LDS_BYTES                              \
+  }

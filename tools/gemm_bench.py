@@ -14,7 +14,7 @@ from dfu_hip import ops  # noqa: E402
 
 dev = "cuda"
 bf = torch.bfloat16
-TILE_NAMES = ["auto", "128x128", "256x128", "128x256", "256x256"]
+TILE_NAMES = ["auto", "128x128", "256x128", "128x256", "256x256", "128x128o2"]
 
 
 def T(*s, dtype=bf):
@@ -107,7 +107,7 @@ conv("l4ds 1x1 1024->2048 s2 14", 64, 14, 1024, 2048, 1, 2)
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 flt = args[0] if args else ""
 sweep = "--sweep" in sys.argv
-tiles = range(5) if sweep else [0]
+tiles = range(len(TILE_NAMES)) if sweep else [0]
 print(f"{'case':42s} " + " ".join(f"{TILE_NAMES[t]:>16s}" for t in tiles))
 tot_us = 0.0
 for name, flops, fn in cases:

@@ -1,0 +1,137 @@
+"""Offline GEMM plan tuning on MI355X -> dfu-multimodal_amd/csrc/gemm_tuned.inc.
+
+Records every dfu_gemm launch of one real training step (bench.py's model and batch), and for
+each distinct descriptor times every tile shape (1..5) x split-K candidate (weight gradients),
+keeping the fastest.  The generated table is compiled into libdfu_hip.so and takes precedence
+over the analytic cost model (csrc/gemm.hip), so plans are deterministic (no runtime tuning).
+
+  python tools/gemm_tune.py [--batch 64] [--config fusion] [--out PATH] [--iters 10]
+"""
+import argparse
+import ctypes
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dfu-multimodal_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from dfu_hip import _lib as L  # noqa: E402
+from dfu_hip import ops  # noqa: E402
+
+SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256]
+OPND = ["KM", "MN", "CONV_FWD", "CONV_DGRAD", "CONV_DGRAD_W", "CONV_WGRAD_X"]
+EPI = ["BF16", "BF16_RELU", "BF16_GELU", "F32", "F32_RESID", "BF16_DGELU", "BF16_ADD", "F32_ACC",
+       "F32_ACC_CONVW", "BF16_STATS", "PATCH"]
+CONV_FIELDS = ("conv_n", "conv_h", "conv_w", "conv_c", "conv_k", "conv_r", "conv_s",
+               "conv_stride", "conv_pad")
+
+
+def key(d):
+    conv = d.a_mode >= L.OPND_CONV_FWD or d.b_mode >= L.OPND_CONV_FWD
+    return (d.a_mode, d.b_mode, d.epilogue, d.M, d.N, d.K) + (
+        tuple(getattr(d, f) for f in CONV_FIELDS) if conv else (0,) * 9)
+
+
+def copy_desc(d):
+    n = L.GemmDesc()
+    ctypes.memmove(ctypes.byref(n), ctypes.byref(d), ctypes.sizeof(d))
+    return n
+
+
+def time_desc(d, iters, ws):
+    lib = ops.lib()
+    need = lib.dfu_gemm_workspace_bytes(ctypes.byref(d))
+    if need > ws.numel():
+        ws = torch.empty(need, dtype=torch.uint8, device="cuda")
+    d.workspace = ws.data_ptr() if need > 0 else None
+    d.workspace_bytes = int(need)
+    s = ops.stream_ptr()
+    for _ in range(2):
+        ops.check(lib.dfu_gemm(ctypes.byref(d), s), "dfu_gemm")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        lib.dfu_gemm(ctypes.byref(d), s)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters, ws
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--config", default="fusion")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--out", default=os.path.join(ROOT, "dfu-multimodal_amd", "csrc",
+                                                  "gemm_tuned.inc"))
+    ap.add_argument("--append", action="store_true", help="keep entries already in --out")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(42)
+    from dfu_hip import nn as hnn
+    from dfu_hip.optim import FusedAdamW
+    model, fwd = bench.build(a.config, dev)
+    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
+    rgb, th, y = bench.synthetic(a.batch, dev, 42)
+    ops.gemm_record = []
+    opt.zero_grad()
+    crit(fwd(model, rgb, th), y).backward()
+    opt.step()
+    rec, ops.gemm_record = ops.gemm_record, None
+    torch.cuda.synchronize()
+    uniq = {}
+    for d, flops, _, refs in rec:
+        uniq.setdefault(key(d), (d, flops, refs, []))[3].append(1)
+    print(f"{len(rec)} launches, {len(uniq)} distinct GEMMs", flush=True)
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    lines, t_auto_sum, t_best_sum = [], 0.0, 0.0
+    t0 = time.time()
+    for k, (d0, flops, refs, cnt) in uniq.items():
+        n = len(cnt)
+        d = copy_desc(d0)
+        d.tile, d.split_k = 0, 0
+        t_auto, ws = time_desc(d, a.iters, ws)
+        best = (t_auto, 0, 0)
+        ktiles = (d0.K + 63) // 64
+        splits = [s for s in SPLITS if s <= ktiles] if d0.epilogue == L.EPI_F32_ACC else [1]
+        for tile in range(1, 6):
+            for sk in splits:
+                d = copy_desc(d0)
+                d.tile, d.split_k = tile, sk
+                try:
+                    t, ws = time_desc(d, a.iters, ws)
+                except L.DfuError:
+                    break  # tile not instantiated for this combination
+                if t < best[0]:
+                    best = (t, tile, sk)
+        t_auto_sum += n * t_auto
+        t_best_sum += n * min(best[0], t_auto)
+        name = (f"{OPND[d0.a_mode]}x{OPND[d0.b_mode]}->{EPI[d0.epilogue]} "
+                f"{d0.M}x{d0.N}x{d0.K} (x{n}/step)")
+        print(f"{name:62s} auto {t_auto:8.1f} us  best {best[0]:8.1f} us tile {best[1]} "
+              f"split {best[2]}  {flops / best[0] / 1e6:6.0f} TFLOP/s", flush=True)
+        if best[1]:
+            lines.append("    {" + ", ".join(str(v) for v in k) + f", {best[1]}, {best[2]}}},"
+                         f"  // {name}: {best[0]:.1f} us (model {t_auto:.1f} us)")
+    print(f"GEMM time per step: model plans {t_auto_sum / 1e3:.3f} ms -> tuned "
+          f"{t_best_sum / 1e3:.3f} ms ({time.time() - t0:.0f} s tuning)")
+    keep = []
+    if a.append and os.path.exists(a.out):
+        keep = [ln.rstrip("\n") for ln in open(a.out) if ln.startswith("    {")]
+        have = {ln.split("}")[0] for ln in lines}
+        keep = [ln for ln in keep if ln.split("}")[0] not in have]
+    with open(a.out, "w") as f:
+        f.write("// Generated by tools/gemm_tune.py on MI355X (gfx950): fastest tile/split-K per GEMM of\n"
+                "// the DFU training step. Fields: a_mode, b_mode, epilogue, M, N, K, conv n,h,w,c,k,r,s,"
+                "stride,pad,\n// tile (1..5), split.\n")
+        for ln in keep + lines:
+            f.write(ln + "\n")
+    print(f"wrote {len(keep) + len(lines)} entries to {a.out}")
+
+
+if __name__ == "__main__":
+    main()
