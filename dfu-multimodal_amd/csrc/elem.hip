@@ -69,35 +69,42 @@ __global__ void k_cast_rows_f32(const bf16_t* __restrict__ in, int64_t ld_in,
 
 // ---------------------------------------------------------------- stem im2col / patchify
 // out[m][k], m = (b, oh, ow), k = c*R*S + r*S + s; each thread writes one 16-B vector (8 k).
-__global__ void k_im2col_f32(const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh,
-                             int64_t sw, int B, int C, int H, int W, int R, int S, int stride,
-                             int pad, int P, int Q, bf16_t* __restrict__ out, int Kp) {
-  const int vec_per_row = Kp / 8;
-  const int64_t n = (int64_t)B * P * Q * vec_per_row;
+// Stem im2col: fp32 NCHW input -> bf16 [B*P*Q][Kp] rows, k = (c, r, s) (OIHW weight order),
+// zero-padded to Kp.  Each thread owns one 16-byte chunk kv of the row (its 8 taps decoded
+// once); a block of VPR*RPB threads covers RPB consecutive rows per iteration, so a wave's
+// stores are contiguous row bytes.  One division per row decodes (b, oh, ow).
+template <int VPR>
+__global__ __launch_bounds__(VPR * 16) void k_im2col_f32(
+    const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int B, int C,
+    int H, int W, int R, int S, int stride, int pad, int P, int Q, bf16_t* __restrict__ out) {
+  constexpr int RPB = 16;
+  constexpr int Kp = VPR * 8;
+  const int kv = threadIdx.x % VPR, rsub = threadIdx.x / VPR;
   const int KK = C * R * S;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / vec_per_row;
-    const int kv = (int)(i - m * vec_per_row);
-    const int b = (int)(m / (P * Q));
-    const int rem = (int)(m - (int64_t)b * P * Q);
+  int tc[8], tr[8], ts[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = kv * 8 + e;
+    const int c = k / (R * S), rs = k - (k / (R * S)) * (R * S);
+    tc[e] = k < KK ? c : -1;
+    tr[e] = rs / S;
+    ts[e] = rs - (rs / S) * S;
+  }
+  const int rows = B * P * Q;
+  for (int m = blockIdx.x * RPB + rsub; m < rows; m += gridDim.x * RPB) {
+    const int b = m / (P * Q);
+    const int rem = m - b * P * Q;
     const int oh = rem / Q, ow = rem - (rem / Q) * Q;
+    const int ih0 = oh * stride - pad, iw0 = ow * stride - pad;
+    const float* xb = x + b * sn;
     float f[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int k = kv * 8 + e;
-      float v = 0.f;
-      if (k < KK) {
-        const int c = k / (R * S);
-        const int rs = k - c * R * S;
-        const int r = rs / S, s = rs - (rs / S) * S;
-        const int ih = oh * stride - pad + r, iw = ow * stride - pad + s;
-        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-          v = x[b * sn + c * sc + ih * sh + iw * sw];
-      }
-      f[e] = v;
+      const int ih = ih0 + tr[e], iw = iw0 + ts[e];
+      const bool ok = tc[e] >= 0 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      f[e] = ok ? xb[tc[e] * sc + ih * sh + iw * sw] : 0.f;
     }
-    *(u32x4*)(out + m * Kp + kv * 8) = pack8(f);
+    *(u32x4*)(out + (int64_t)m * Kp + kv * 8) = pack8(f);
   }
 }
 
@@ -545,8 +552,20 @@ extern "C" int dfu_im2col_f32(const float* x, int64_t sn, int64_t sc, int64_t sh
                               int32_t Kp, void* stream) {
   DFU_CHECK_ARG(x && out && Kp % 8 == 0 && Kp >= C * R * S, "dfu_im2col_f32: bad Kp=%d", Kp);
   DFU_CHECK_ARG(((uintptr_t)out & 15) == 0, "dfu_im2col_f32: out must be 16-B aligned");
-  LAUNCH(k_im2col_f32, (int64_t)B * P * Q * (Kp / 8), stream, x, sn, sc, sh, sw, B, C, H, W, R,
-         S, stride, pad, P, Q, (bf16_t*)out, Kp);
+  const int64_t rows = (int64_t)B * P * Q;
+  DFU_CHECK_ARG(rows < (1ll << 31), "dfu_im2col_f32: too many rows");
+  const int blocks = (int)((rows + 15) / 16 < 8192 ? (rows + 15) / 16 : 8192);
+  hipStream_t st = (hipStream_t)stream;
+  switch (Kp) {
+    case 160:
+      hipLaunchKernelGGL(k_im2col_f32<20>, dim3(blocks), dim3(320), 0, st, x, sn, sc, sh, sw, B,
+                         C, H, W, R, S, stride, pad, P, Q, (bf16_t*)out);
+      break;
+    default:
+      dfu_set_error("dfu_im2col_f32: Kp=%d not instantiated (160 = the ResNet 7x7x3 stem)", Kp);
+      return DFU_E_UNSUPPORTED;
+  }
+  DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
 

@@ -168,6 +168,53 @@ extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* spl
   return DFU_OK;
 }
 
+namespace {
+
+// One stride phase of a strided dgrad (see GemmArgs::ph_*): rows h = h'*st + ph, taps
+// r = r0 + st*ri; qh = (ph + pad - r0) / st is the phase's stride-1 "padding".
+struct Phase {
+  int ph, pw, r0, s0, nr, ns, qh, qw, Hs, Ws;
+};
+
+Phase make_phase(const dfu_gemm_desc* d, int ph, int pw) {
+  const int st = d->conv_stride, pad = d->conv_pad;
+  Phase f;
+  f.ph = ph;
+  f.pw = pw;
+  f.r0 = (ph + pad) % st;
+  f.s0 = (pw + pad) % st;
+  f.nr = f.r0 < d->conv_r ? (d->conv_r - f.r0 + st - 1) / st : 0;
+  f.ns = f.s0 < d->conv_s ? (d->conv_s - f.s0 + st - 1) / st : 0;
+  f.qh = (ph + pad - f.r0) / st;
+  f.qw = (pw + pad - f.s0) / st;
+  f.Hs = ph < d->conv_h ? (d->conv_h - ph + st - 1) / st : 0;
+  f.Ws = pw < d->conv_w ? (d->conv_w - pw + st - 1) / st : 0;
+  return f;
+}
+
+// dX rows of a phase without live taps: 0 (BF16) or the addend (BF16_ADD).
+__global__ void k_phase_fill(bf16_t* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ aux,
+                             int64_t ldaux, int B, int Hs, int Ws, int H, int W, int st, int ph,
+                             int pw, int N) {
+  const int64_t rows = (int64_t)B * Hs * Ws;
+  const int nv = N / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * nv;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / nv;
+    const int c = (int)(i - m * nv) * 8;
+    const int b = (int)(m / ((int64_t)Hs * Ws));
+    const int rem = (int)(m - (int64_t)b * Hs * Ws);
+    const int h = rem / Ws, w = rem - (rem / Ws) * Ws;
+    const int64_t row = ((int64_t)b * H + h * st + ph) * W + w * st + pw;
+    const u32x4 v = aux ? *(const u32x4*)(aux + row * ldaux + c) : (u32x4){0u, 0u, 0u, 0u};
+    *(u32x4*)(C + row * ldc + c) = v;
+  }
+}
+
+int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t s);
+
+}  // namespace
+
 extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
   DFU_CHECK_ARG(d != nullptr, "dfu_gemm: null descriptor");
   DFU_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0, "dfu_gemm: bad shape M=%d N=%d K=%d", d->M,
@@ -200,6 +247,71 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
   if (d->epilogue == DFU_EPI_BF16_STATS)
     DFU_CHECK_ARG(d->stats != nullptr, "dfu_gemm: STATS epilogue needs a stats slab");
 
+  const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
+  if (conv) {
+    DFU_CHECK_ARG(d->conv_n > 0 && d->conv_h > 0 && d->conv_w > 0 && d->conv_c > 0 &&
+                      d->conv_k > 0 && d->conv_r > 0 && d->conv_s > 0 && d->conv_stride > 0 &&
+                      d->conv_p > 0 && d->conv_q > 0,
+                  "dfu_gemm: conv geometry missing");
+    if (d->a_mode == DFU_OPND_CONV_FWD) {
+      DFU_CHECK_ARG(d->conv_c % BK == 0, "dfu_gemm: implicit conv fwd needs C %% 64 == 0");
+      DFU_CHECK_ARG(d->K == d->conv_r * d->conv_s * d->conv_c, "dfu_gemm: conv fwd K != RSC");
+      DFU_CHECK_ARG(d->M == d->conv_n * d->conv_p * d->conv_q, "dfu_gemm: conv fwd M != NPQ");
+    }
+    if (d->a_mode == DFU_OPND_CONV_DGRAD) {
+      DFU_CHECK_ARG(d->conv_k % BK == 0, "dfu_gemm: conv dgrad needs Kout %% 64 == 0");
+      DFU_CHECK_ARG(d->K == d->conv_r * d->conv_s * d->conv_k, "dfu_gemm: conv dgrad K != RSK");
+      DFU_CHECK_ARG(d->M == d->conv_n * d->conv_h * d->conv_w, "dfu_gemm: conv dgrad M != NHW");
+      DFU_CHECK_ARG(d->conv_c % 8 == 0, "dfu_gemm: conv dgrad needs C %% 8 == 0");
+      DFU_CHECK_ARG(d->b_mode == DFU_OPND_CONV_DGRAD_W, "dfu_gemm: conv dgrad needs DGRAD_W B");
+    }
+    if (d->b_mode == DFU_OPND_CONV_WGRAD_X) {
+      DFU_CHECK_ARG(d->conv_c % 8 == 0, "dfu_gemm: conv wgrad needs C %% 8 == 0");
+      DFU_CHECK_ARG(d->N == d->conv_r * d->conv_s * d->conv_c, "dfu_gemm: conv wgrad N != RSC");
+      DFU_CHECK_ARG(d->K == d->conv_n * d->conv_p * d->conv_q, "dfu_gemm: conv wgrad K != NPQ");
+    }
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (d->a_mode != DFU_OPND_CONV_DGRAD || d->conv_stride == 1) return launch(d, pl, nullptr, s);
+
+  // Strided dgrad: stride^2 phase launches, each a dense stride-1 gather over its live taps
+  // (a dense launch would spend (1 - 1/stride^2) of its MFMA work on zero taps).
+  const int st = d->conv_stride;
+  for (int ph = 0; ph < st; ++ph)
+    for (int pw = 0; pw < st; ++pw) {
+      const Phase f = make_phase(d, ph, pw);
+      if (f.Hs == 0 || f.Ws == 0) continue;
+      if (f.nr == 0 || f.ns == 0) {  // no live tap: the rows are 0 (or the addend)
+        DFU_CHECK_ARG(d->epilogue == DFU_EPI_BF16 || d->epilogue == DFU_EPI_BF16_ADD,
+                      "dfu_gemm: strided dgrad supports the BF16 / BF16_ADD epilogues");
+        if (d->epilogue == DFU_EPI_BF16_ADD && d->aux == d->C && d->ldaux == d->ldc) continue;
+        const int64_t n = (int64_t)d->conv_n * f.Hs * f.Ws * (d->N / 8);
+        const int blocks = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+        hipLaunchKernelGGL(k_phase_fill, dim3(blocks), dim3(256), 0, s, (bf16_t*)d->C, d->ldc,
+                           d->epilogue == DFU_EPI_BF16_ADD ? (const bf16_t*)d->aux : nullptr,
+                           d->ldaux, d->conv_n, f.Hs, f.Ws, d->conv_h, d->conv_w, st, ph, pw,
+                           d->N);
+        DFU_LAUNCH_CHECK();
+        continue;
+      }
+      dfu_gemm_desc pd = *d;
+      pd.M = d->conv_n * f.Hs * f.Ws;
+      pd.K = f.nr * f.ns * d->conv_k;
+      const Plan pp = plan_gemm(&pd);
+      if (!pp.entry) {
+        dfu_set_error("dfu_gemm: no kernel for a dgrad phase");
+        return DFU_E_UNSUPPORTED;
+      }
+      const int rc = launch(&pd, pp, &f, s);
+      if (rc != DFU_OK) return rc;
+    }
+  return DFU_OK;
+}
+
+namespace {
+
+int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t s) {
+  const bool acc_epi = d->epilogue == DFU_EPI_F32_ACC;
   GemmArgs a;
   const int TM = kTM[pl.tile], TN = kTN[pl.tile];
   a.M = d->M; a.N = d->N; a.K = d->K;
@@ -225,40 +337,27 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
   a.cn = d->conv_n; a.ch = d->conv_h; a.cw = d->conv_w; a.cc = d->conv_c;
   a.ck = d->conv_k; a.cr = d->conv_r; a.cs = d->conv_s;
   a.cstride = d->conv_stride; a.cpad = d->conv_pad; a.cp = d->conv_p; a.cq = d->conv_q;
+  a.cpad_w = d->conv_pad;
+  a.ph_st = a.ph_h = a.ph_w = a.ph_r0 = a.ph_s0 = a.ph_H = a.ph_W = a.ph_S = 0;
+  if (ph) {  // the phase's stride-1 equivalent geometry (GemmArgs::ph_*)
+    a.ch = ph->Hs; a.cw = ph->Ws; a.cr = ph->nr; a.cs = ph->ns;
+    a.cstride = 1; a.cpad = ph->qh; a.cpad_w = ph->qw;
+    a.ph_st = d->conv_stride; a.ph_h = ph->ph; a.ph_w = ph->pw;
+    a.ph_r0 = ph->r0; a.ph_s0 = ph->s0;
+    a.ph_H = d->conv_h; a.ph_W = d->conv_w; a.ph_S = d->conv_s;
+  }
   a.m_ld_bound = round8(d->M);
   a.n_ld_bound = round8(d->N);
-  const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
-  if (conv) {
-    DFU_CHECK_ARG(d->conv_n > 0 && d->conv_h > 0 && d->conv_w > 0 && d->conv_c > 0 &&
-                      d->conv_k > 0 && d->conv_r > 0 && d->conv_s > 0 && d->conv_stride > 0 &&
-                      d->conv_p > 0 && d->conv_q > 0,
-                  "dfu_gemm: conv geometry missing");
-    a.div_pq = make_fastdiv(d->conv_p * d->conv_q);
-    a.div_q = make_fastdiv(d->conv_q);
-    a.div_hw = make_fastdiv(d->conv_h * d->conv_w);
-    a.div_w = make_fastdiv(d->conv_w);
-    a.div_c = make_fastdiv(d->conv_c);
-    a.div_k = make_fastdiv(d->conv_k);
-    a.div_s = make_fastdiv(d->conv_s);
-    if (d->a_mode == DFU_OPND_CONV_FWD) {
-      DFU_CHECK_ARG(d->conv_c % BK == 0, "dfu_gemm: implicit conv fwd needs C %% 64 == 0");
-      DFU_CHECK_ARG(d->K == d->conv_r * d->conv_s * d->conv_c, "dfu_gemm: conv fwd K != RSC");
-      DFU_CHECK_ARG(d->M == d->conv_n * d->conv_p * d->conv_q, "dfu_gemm: conv fwd M != NPQ");
-    }
-    if (d->a_mode == DFU_OPND_CONV_DGRAD) {
-      DFU_CHECK_ARG(d->conv_k % BK == 0, "dfu_gemm: conv dgrad needs Kout %% 64 == 0");
-      DFU_CHECK_ARG(d->K == d->conv_r * d->conv_s * d->conv_k, "dfu_gemm: conv dgrad K != RSK");
-      DFU_CHECK_ARG(d->M == d->conv_n * d->conv_h * d->conv_w, "dfu_gemm: conv dgrad M != NHW");
-      DFU_CHECK_ARG(d->conv_c % 8 == 0, "dfu_gemm: conv dgrad needs C %% 8 == 0");
-    }
-    if (d->b_mode == DFU_OPND_CONV_WGRAD_X) {
-      DFU_CHECK_ARG(d->conv_c % 8 == 0, "dfu_gemm: conv wgrad needs C %% 8 == 0");
-      DFU_CHECK_ARG(d->N == d->conv_r * d->conv_s * d->conv_c, "dfu_gemm: conv wgrad N != RSC");
-      DFU_CHECK_ARG(d->K == d->conv_n * d->conv_p * d->conv_q, "dfu_gemm: conv wgrad K != NPQ");
-      a.n_ld_bound = d->N;
-    }
+  if (d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD) {
+    a.div_pq = make_fastdiv(a.cp * a.cq);
+    a.div_q = make_fastdiv(a.cq);
+    a.div_hw = make_fastdiv(a.ch * a.cw);
+    a.div_w = make_fastdiv(a.cw);
+    a.div_c = make_fastdiv(a.cc);
+    a.div_k = make_fastdiv(a.ck);
+    a.div_s = make_fastdiv(a.cs);
+    if (d->b_mode == DFU_OPND_CONV_WGRAD_X) a.n_ld_bound = d->N;
   }
-  hipStream_t s = (hipStream_t)stream;
   dim3 grid(a.tiles_m * a.tiles_n, splits);
   hipLaunchKernelGGL(pl.entry->fn, grid, dim3(NT), 0, s, a);
   DFU_LAUNCH_CHECK();
@@ -277,3 +376,5 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
   }
   return DFU_OK;
 }
+
+}  // namespace

@@ -61,6 +61,12 @@ struct GemmArgs {
   int ep_tokens;
   // conv geometry
   int cn, ch, cw, cc, ck, cr, cs, cstride, cpad, cp, cq;
+  int cpad_w;  // padding along W (== cpad except for stride-phase dgrad launches)
+  // Stride-phase dgrad (ph_st > 0): this launch computes the dX rows h = h'*st + ph_h,
+  // w = w'*st + ph_w with only the live taps r = ph_r0 + st*ri, s = ph_s0 + st*si.  The
+  // geometry above is then the phase's stride-1 equivalent (ch, cw = phase grid; cr, cs = live
+  // tap counts; cpad, cpad_w = tap origins); ph_H/ph_W/ph_S are the real dX dims / filter width.
+  int ph_st, ph_h, ph_w, ph_r0, ph_s0, ph_H, ph_W, ph_S;
   FastDiv div_pq, div_q, div_hw, div_w, div_c, div_k, div_s;
   int m_ld_bound;  // MN-contiguous operands may be read up to this column bound
   int n_ld_bound;
@@ -142,7 +148,7 @@ DFU_DEV void load_init(const GemmArgs& p, LoadState<NLD>& st, const bf16_t* base
       const uint32_t h = fdiv(rem, p.div_w);
       const uint32_t w = rem - h * p.cw;
       st.i0[i] = (int)h + p.cpad;
-      st.i1[i] = (int)w + p.cpad;
+      st.i1[i] = (int)w + p.cpad_w;
       st.bofs[i] = (int)b;
     }
   } else if constexpr (MODE == DFU_OPND_CONV_WGRAD_X) {
@@ -227,12 +233,18 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
     // B[k'=(r,s,kout)][c] = Wkrsc[kout][r][s][c];  ld = R*S*C
     const uint32_t rs = fdiv((uint32_t)k0, p.div_k);
     const int kout0 = k0 - (int)rs * p.ck;
+    int64_t tap_off = (int64_t)rs * p.cc;
+    if (p.ph_st) {  // phase launch: live tap (ri, si) -> filter tap (r0 + st ri, s0 + st si)
+      const uint32_t ri = fdiv(rs, p.div_s);
+      const int si = (int)(rs - ri * p.cs);
+      tap_off = ((int64_t)(p.ph_r0 + p.ph_st * (int)ri) * p.ph_S + p.ph_s0 + p.ph_st * si) * p.cc;
+    }
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const int kout = kout0 + (tid >> 4) + 32 * (i & 1);
       const int col = st.col + 128 * (i >> 1);
       const bool ok = col < MN_bound && k0 < kend;
-      glds16(ok ? (const void*)(base + (int64_t)kout * ld + (int64_t)rs * p.cc + col) : zero,
+      glds16(ok ? (const void*)(base + (int64_t)kout * ld + tap_off + col) : zero,
              dst + 8192 * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_WGRAD_X) {
@@ -288,6 +300,17 @@ DFU_DEV void wait_vmcnt() {
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+// Output row of GEMM row m: identity, or for a stride-phase dgrad launch the dX row
+// (b, h'*st + ph_h, w'*st + ph_w) of phase-grid row m = (b, h', w').
+DFU_DEV int64_t out_row(const GemmArgs& p, int m) {
+  if (!p.ph_st) return m;
+  const uint32_t b = fdiv((uint32_t)m, p.div_hw);
+  const uint32_t rem = (uint32_t)m - b * (uint32_t)(p.ch * p.cw);
+  const uint32_t h = fdiv(rem, p.div_w);
+  const uint32_t w = rem - h * (uint32_t)p.cw;
+  return ((int64_t)b * p.ph_H + (int)h * p.ph_st + p.ph_h) * p.ph_W + (int)w * p.ph_st + p.ph_w;
 }
 
 // ------------------------------------------------------------------------------ kernel
@@ -482,6 +505,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wr * WTM + 16 * i + lrow;
       if (m >= p.M) continue;
+      const int64_t mo = AMODE == DFU_OPND_CONV_DGRAD ? out_row(p, m) : (int64_t)m;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int n = n0 + wc * WTN + 16 * j + lcol;
@@ -503,7 +527,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
           }
-          bf16_t* C = (bf16_t*)p.C + (int64_t)m * p.ldc + n;
+          bf16_t* C = (bf16_t*)p.C + mo * p.ldc + n;
           if (full) {
             *(u32x2*)C = (u32x2){pack2(v[0], v[1]), pack2(v[2], v[3])};
           } else {
@@ -542,8 +566,8 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
               if (n + r < p.N) C[r] = v[r] + R[r];
           }
         } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
-          bf16_t* C = (bf16_t*)p.C + (int64_t)m * p.ldc + n;
-          const bf16_t* X = (const bf16_t*)p.aux + (int64_t)m * p.ldaux + n;
+          bf16_t* C = (bf16_t*)p.C + mo * p.ldc + n;
+          const bf16_t* X = (const bf16_t*)p.aux + mo * p.ldaux + n;
           float x[4];
           if (full) {
             const u32x2 xv = *(const u32x2*)X;

@@ -325,8 +325,8 @@ class BottleneckFn(torch.autograd.Function):
         dy3 = torch.empty_like(y3)
         dres = torch.empty_like(y3)
         s3.backward(g, y3, out, True, dy3, dres)
-        # downsample branch
-        dx_id = None
+        # downsample branch (its dgrad is added in place after conv1's, below)
+        dyd = None
         if yd is not None:
             dyd = torch.empty_like(yd)
             sd.backward(dres, yd, None, False, dyd, None)
@@ -334,11 +334,6 @@ class BottleneckFn(torch.autograd.Function):
             if _wants(dconv.weight):
                 conv_wgrad(dyd, xr, gd, grad_buffer(dconv.weight))
                 grads_done(dconv.weight)
-            if ctx.x_requires_grad:
-                dx_id = _empty((M1, Cin), BF16, dev)
-                conv_dgrad(dyd, gd, wd, dx_id)
-        else:
-            dx_id = dres
         # conv3
         da2 = torch.empty_like(a2)
         conv_dgrad(dy3, g3, w3, da2)
@@ -359,7 +354,11 @@ class BottleneckFn(torch.autograd.Function):
         dx = None
         if ctx.x_requires_grad:
             dxr = _empty((M1, Cin), BF16, dev)
-            conv_dgrad(dy1, g1, w1, dxr, add=dx_id)
+            if dyd is None:  # identity shortcut: its gradient rides in conv1's dgrad epilogue
+                conv_dgrad(dy1, g1, w1, dxr, add=dres)
+            else:  # downsample: conv1's dgrad, then the (strided) 1x1 dgrad added in place
+                conv_dgrad(dy1, g1, w1, dxr)
+                conv_dgrad(dyd, gd, wd, dxr, add=dxr)
             dx = from_rows(dxr, B, H, W, Cin)
         if _wants(mod.conv1.weight):
             conv_wgrad(dy1, xr, g1, grad_buffer(mod.conv1.weight))

@@ -175,6 +175,8 @@ CONV_CASES = [
     (2, 15, 15, 64, 64, 3, 3, 2, 1),
     (3, 14, 14, 128, 256, 1, 1, 2, 0),
     (2, 7, 7, 512, 512, 3, 3, 1, 1),
+    (2, 28, 28, 128, 128, 3, 3, 2, 1),   # ResNet layer2 first block conv2 (stride phases)
+    (2, 14, 14, 256, 512, 1, 1, 2, 0),   # downsample 1x1/s2: 3 of 4 phases have no tap
 ]
 
 
@@ -211,6 +213,19 @@ def test_conv_fwd_dgrad_wgrad(case, tile):
     gemm_or_auto(N * H * W, C, R * S * K, dy_nhwc, 0, w_krsc, R * S * C, dX, C,
              a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=L.EPI_BF16, conv=g, tile=tile)
     close(dX.view(N, H, W, C), _nhwc(xf.grad), atol=5e-2, rtol=1e-2, what="conv dgrad")
+    # dgrad + addend (the bottleneck's identity/downsample gradient), separate and in place
+    base = rnd(N * H * W, C, seed=23)
+    dXa = torch.empty_like(dX)
+    gemm_or_auto(N * H * W, C, R * S * K, dy_nhwc, 0, w_krsc, R * S * C, dXa, C,
+                 a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=L.EPI_BF16_ADD,
+                 aux=base, ldaux=C, conv=g, tile=tile)
+    ref_add = _nhwc(xf.grad).reshape(-1, C) + base.float()
+    close(dXa, ref_add, atol=6e-2, rtol=1e-2, what="conv dgrad + add")
+    dXi = base.clone()
+    gemm_or_auto(N * H * W, C, R * S * K, dy_nhwc, 0, w_krsc, R * S * C, dXi, C,
+                 a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=L.EPI_BF16_ADD,
+                 aux=dXi, ldaux=C, conv=g, tile=tile)
+    close(dXi, ref_add, atol=6e-2, rtol=1e-2, what="conv dgrad + add in place")
     # wgrad (OIHW fp32 accumulate)
     dW = torch.zeros(K, C, R, S, dtype=torch.float32, device=DEV)
     acc = torch.zeros(K, R * S * C, dtype=torch.float32, device=DEV)

@@ -1,0 +1,72 @@
+"""Run one GEMM of the step repeatedly (for rocprofv3 --pmc counter passes on a single kernel).
+
+  python tools/gemm_one.py <case> [--tile T] [--iters N]
+  cases: fc1_fwd (12608x3072x768, KM x KM, BF16), fc1_gelu (same, GELU epilogue),
+         fc2_dgrad (12608x3072x768, KM x MN, DGELU), fc1_wgrad (3072x768x12608, MN x MN, F32_ACC),
+         l1c3_fwd (200704x256x64 1x1 conv, STATS)
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dfu-multimodal_amd")]
+import torch  # noqa: E402
+
+from dfu_hip import _lib as L  # noqa: E402
+from dfu_hip import ops  # noqa: E402
+
+
+def T(*s, dtype=torch.bfloat16):
+    return (torch.randn(*s, device="cuda") * 0.1).to(dtype)
+
+
+def build(case, tile):
+    if case in ("fc1_fwd", "fc1_gelu"):
+        M, N, K = 12608, 3072, 768
+        A, B, C, pre = T(M, K), T(N, K), T(M, N), T(M, N)
+        epi = L.EPI_BF16_GELU if case == "fc1_gelu" else L.EPI_BF16
+        kw = dict(aux_out=pre, ldaux_out=N) if case == "fc1_gelu" else {}
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=epi, tile=tile, **kw)
+    if case == "fc2_dgrad":
+        M, N, K = 12608, 3072, 768
+        A, B, C, h = T(M, K), T(K, N), T(M, N), T(M, N)
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, N, C, N, b_mode=L.OPND_MNMAJOR,
+                                               epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N, tile=tile)
+    if case == "fc1_wgrad":
+        M, N, K = 3072, 768, 12608
+        A, B = T(K, M), T(K, N)
+        C = torch.zeros(M, N, device="cuda")
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, M, B, N, C, N, a_mode=L.OPND_MNMAJOR,
+                                               b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC,
+                                               tile=tile)
+    if case == "l1c3_fwd":
+        M, N, K = 200704, 256, 64
+        A, B, C = T(M, K), T(N, K), T(M, N)
+        st = torch.empty(ops.stats_tiles(M), 2, N, device="cuda")
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N,
+                                               epilogue=L.EPI_BF16_STATS, stats=st, tile=tile)
+    raise SystemExit(f"unknown case {case}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("case")
+    ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    flops, fn = build(a.case, a.tile)
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / a.iters
+    print(f"{a.case} tile {a.tile}: {us:.1f} us  {flops / us / 1e6:.0f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()
