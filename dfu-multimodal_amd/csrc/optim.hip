@@ -82,10 +82,12 @@ DFU_DEV void adam_update(float& p, float g, float& m, float& v, const AdamCoef& 
   p -= a.step_size * (m / denom);
 }
 
+// Optionally also writes the bf16 shadow of the updated parameters (the GEMM operand copy),
+// so no per-step cast kernels are needed.
 __global__ void k_adamw_flat(float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
                              float b1, float b2, float eps, float wd,
-                             const int64_t* __restrict__ step_dev) {
+                             const int64_t* __restrict__ step_dev, bf16_t* __restrict__ shadow) {
   const AdamCoef a = adam_coef(*step_dev, lr, b1, b2, wd);
   const int64_t n4 = n / 4;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
@@ -101,12 +103,14 @@ __global__ void k_adamw_flat(float* __restrict__ p, const float* __restrict__ g,
     ((f32x4*)p)[i] = pp;
     ((f32x4*)m)[i] = mm;
     ((f32x4*)v)[i] = vv;
+    if (shadow) ((u32x2*)shadow)[i] = (u32x2){pack2(pp[0], pp[1]), pack2(pp[2], pp[3])};
   }
   for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float pe = p[i], me = m[i], ve = v[i];
     adam_update(pe, g[i], me, ve, a, b1, b2, eps);
     p[i] = pe; m[i] = me; v[i] = ve;
+    if (shadow) shadow[i] = f2bf(pe);
   }
 }
 
@@ -166,17 +170,20 @@ extern "C" int dfu_ce_weighted_bwd(const float* saved, const float* grad_loss, i
 
 extern "C" int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                               int64_t n, float lr, float beta1, float beta2, float eps,
-                              float weight_decay, const int64_t* step_dev, void* stream) {
+                              float weight_decay, const int64_t* step_dev, void* shadow_bf16,
+                              void* stream) {
   DFU_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step_dev && n > 0,
                 "dfu_adamw_flat: bad args");
   DFU_CHECK_ARG(((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 &&
-                    ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0,
-                "dfu_adamw_flat: buffers must be 16-byte aligned");
+                    ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0 &&
+                    ((uintptr_t)shadow_bf16 & 7) == 0,
+                "dfu_adamw_flat: buffers must be 16-byte aligned (shadow 8-byte)");
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_adamw_flat, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param,
-                     grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step_dev);
+                     grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step_dev,
+                     (bf16_t*)shadow_bf16);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

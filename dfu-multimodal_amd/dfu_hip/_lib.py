@@ -107,7 +107,7 @@ PROTOTYPES = {
     "dfu_ce_weighted_fwd": [P, P, P, I32, I32, P, P, P],
     "dfu_ce_weighted_bwd": [P, P, I32, I32, P, P],
     "dfu_adamw": [P, P, P, P, P, I32, P, I32, F, F, F, F, F, P, P],
-    "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P],
+    "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P],
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
 }

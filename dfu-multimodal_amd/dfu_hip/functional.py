@@ -90,9 +90,24 @@ def from_rows(r, B, H, W, C):
 
 
 def weight_bf16_rows(w, ld=None):
-    """fp32 [N, K...] parameter -> bf16 [N, ld] (GEMM operand, re-cast every call)."""
+    """fp32 [N, K...] parameter -> bf16 [N, ld] GEMM operand.  Parameters managed by FusedAdamW
+    have a bf16 shadow the optimizer kernel keeps current (optim.FlatParams): returned as a
+    view, re-cast only if the parameter changed outside the optimizer (version counter)."""
     w2 = w.detach().reshape(w.shape[0], -1)
+    sh = getattr(w, "_dfu_shadow", None)
+    if sh is not None and (ld is None or ld == w2.shape[1]):
+        if w._version != getattr(w, "_dfu_shadow_version", -1):
+            ops.cast_rows_bf16(w2, out=sh)
+            w._dfu_shadow_version = w._version
+        return sh
     return ops.cast_rows_bf16(w2, ld_out=ld)
+
+
+def conv_weight_bf16(w):
+    """fp32 OIHW conv weight -> bf16 KRSC GEMM operand (1x1: OIHW == KRSC, the shadow view)."""
+    if w.shape[2] == 1 and w.shape[3] == 1:
+        return weight_bf16_rows(w)
+    return ops.pack_conv_weight(w.detach())
 
 
 # ---------------------------------------------------------------------- BatchNorm helper
@@ -271,9 +286,9 @@ class BottleneckFn(torch.autograd.Function):
         g1 = _geom(mod.conv1, B, H, W)
         g2 = _geom(mod.conv2, B, g1.p, g1.q)
         g3 = _geom(mod.conv3, B, g2.p, g2.q)
-        w1 = ops.pack_conv_weight(mod.conv1.weight.detach())
-        w2 = ops.pack_conv_weight(mod.conv2.weight.detach())
-        w3 = ops.pack_conv_weight(mod.conv3.weight.detach())
+        w1 = conv_weight_bf16(mod.conv1.weight)
+        w2 = conv_weight_bf16(mod.conv2.weight)
+        w3 = conv_weight_bf16(mod.conv3.weight)
         M1 = B * g1.p * g1.q
         M2 = B * g2.p * g2.q
         planes, outc = g1.k, g3.k
@@ -294,7 +309,7 @@ class BottleneckFn(torch.autograd.Function):
         if mod.downsample is not None:
             dconv, dbn = mod.downsample[0], mod.downsample[1]
             gd = _geom(dconv, B, H, W)
-            wd = ops.pack_conv_weight(dconv.weight.detach())
+            wd = conv_weight_bf16(dconv.weight)
             yd, idn, sd = conv_bn(xr, gd, wd, dbn, False)
         else:
             gd = wd = yd = sd = None

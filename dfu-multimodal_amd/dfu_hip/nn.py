@@ -30,7 +30,7 @@ class Conv2dFn(torch.autograd.Function):
         g = Fn._geom(mod, B, H, W)
         if C % 64 != 0 and not (g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0):
             raise NotImplementedError("dfu_hip.nn.Conv2d: implicit GEMM needs C % 64 == 0")
-        wk = ops.pack_conv_weight(w.detach())
+        wk = Fn.conv_weight_bf16(w)
         M = B * g.p * g.q
         y = torch.empty((M, g.k), dtype=torch.bfloat16, device=x.device)
         stats = torch.empty((ops.stats_tiles(M), 2, g.k), dtype=torch.float32, device=x.device)

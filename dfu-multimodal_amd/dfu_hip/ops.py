@@ -450,9 +450,9 @@ def ce_weighted_bwd(saved, grad_loss):
     return out
 
 
-def adamw_flat(p, g, m, v, lr, b1, b2, eps, wd, step_dev):
+def adamw_flat(p, g, m, v, lr, b1, b2, eps, wd, step_dev, shadow=None):
     check(lib().dfu_adamw_flat(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd,
-                               ptr(step_dev), stream_ptr()), "dfu_adamw_flat")
+                               ptr(step_dev), ptr(shadow), stream_ptr()), "dfu_adamw_flat")
 
 
 def step_increment(step_dev):

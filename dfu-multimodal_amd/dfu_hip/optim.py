@@ -8,7 +8,13 @@ view) and ``p.grad`` into a matching flat gradient buffer, so:
   * zero_grad is one hipMemsetAsync;
   * the weight-gradient GEMM epilogues accumulate straight into the flat buffer, whose
     contiguous slices are what data-parallel all-reduce buckets send (dfu_hip.parallel);
-  * the step counter lives on the device, so the whole step can be captured in a HIP graph.
+  * the step counter lives on the device, so the whole step can be captured in a HIP graph;
+  * the same kernel writes a bf16 shadow of every updated parameter (``FlatParams.shadow``):
+    Linear and 1x1-conv weights are consumed by the GEMMs straight from it (no cast kernels).
+    A parameter changed outside the optimizer (load_state_dict, in-place edits through the
+    parameter) bumps its version counter and is re-cast on its next use
+    (functional.weight_bf16_rows); edits through ``p.data`` bypass that counter — call
+    ``FlatParams.refresh_shadow()`` after those.
 """
 import torch
 
@@ -39,12 +45,25 @@ class FlatParams:
         self.numel = off
         self.data = torch.zeros(off, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=dev) if dev.type == "cuda" \
+            else None
         with torch.no_grad():
             for p, o in zip(self.params, self.offsets):
                 view = self.data[o:o + p.numel()].view_as(p)
                 view.copy_(p.data)
                 p.data = view
                 p.grad = self.grad[o:o + p.numel()].view_as(p)
+                if self.shadow is not None:
+                    p._dfu_shadow = self.shadow[o:o + p.numel()].view(p.shape[0], -1)
+        self.refresh_shadow()
+
+    def refresh_shadow(self):
+        """Re-cast every parameter into the bf16 shadow and mark it current."""
+        if self.shadow is None:
+            return
+        ops.cast_rows_bf16(self.data.view(1, -1), out=self.shadow.view(1, -1))
+        for p in self.params:
+            p._dfu_shadow_version = p._version
 
     def grad_view(self, i):
         p, o = self.params[i], self.offsets[i]
@@ -93,7 +112,7 @@ class FusedAdamW(torch.optim.Optimizer):
         b1, b2 = g["betas"]
         ops.step_increment(self.step_dev)
         ops.adamw_flat(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, g["lr"], b1,
-                       b2, g["eps"], g["weight_decay"], self.step_dev)
+                       b2, g["eps"], g["weight_decay"], self.step_dev, shadow=self.flat.shadow)
         return loss
 
     def state_dict(self):

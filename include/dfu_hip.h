@@ -262,10 +262,12 @@ int dfu_adamw(float* const* params, float* const* grads, float* const* exp_avg,
               float* const* exp_avg_sq, const int64_t* numels, int32_t ntensors,
               const int64_t* chunk_offsets, int32_t nchunks, float lr, float beta1,
               float beta2, float eps, float weight_decay, int64_t* step_dev, void* stream);
-/* Flat form: one contiguous buffer of n parameters (the fused flat-parameter layout). */
+/* Flat form: one contiguous buffer of n parameters (the fused flat-parameter layout).
+ * shadow_bf16 (optional, n bf16): also receives bf16(updated param) — the GEMM operand copy
+ * of every weight, so the forward pass needs no cast kernels. */
 int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float lr, float beta1, float beta2, float eps, float weight_decay,
-                   const int64_t* step_dev, void* stream);
+                   const int64_t* step_dev, void* shadow_bf16, void* stream);
 int dfu_step_increment(int64_t* step_dev, void* stream);
 /* argmax over C for each row (torch.max(outputs, 1), :384) -> int64. */
 int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t* out, void* stream);

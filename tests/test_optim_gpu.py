@@ -1,0 +1,56 @@
+"""FusedAdamW on the GPU: the flat update matches torch.optim.AdamW, and the bf16 weight shadow
+the same kernel writes stays equal to bf16(param) — after optimizer steps and after the
+parameters change outside the optimizer (load_state_dict bumps the version counter)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model():
+    from dfu_hip import nn as hnn
+    torch.manual_seed(3)
+    return torch.nn.Sequential(hnn.Linear(768, 512), hnn.ReLU(), hnn.Linear(512, 64)).to(DEV)
+
+
+def test_adamw_matches_torch_and_shadow_tracks():
+    from dfu_hip import functional as Fn
+    from dfu_hip.optim import FusedAdamW
+    m = _model()
+    ref = [p.detach().clone() for p in m.parameters()]
+    opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=1e-2)
+    ref_p = [torch.nn.Parameter(r) for r in ref]
+    ref_opt = torch.optim.AdamW(ref_p, lr=1e-3, weight_decay=1e-2)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for _ in range(4):
+        grads = [torch.randn(p.shape, generator=g).to(DEV) for p in ref_p]
+        opt.zero_grad()
+        for p, gr in zip(m.parameters(), grads):
+            p.grad.copy_(gr)
+        for p, gr in zip(ref_p, grads):
+            p.grad = gr.clone()
+        opt.step()
+        ref_opt.step()
+    for p, r in zip(m.parameters(), ref_p):
+        torch.testing.assert_close(p.detach(), r.detach(), rtol=1e-5, atol=1e-6)
+    # the shadow the forward GEMMs read is exactly bf16 of the updated fp32 weights
+    for p in m.parameters():
+        if p.dim() == 2:
+            sh = Fn.weight_bf16_rows(p)
+            assert sh.data_ptr() == p._dfu_shadow.data_ptr()
+            assert torch.equal(sh, p.detach().to(torch.bfloat16))
+    # a change outside the optimizer is picked up on the next use
+    sd = {k: torch.randn_like(v) for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    # 6000 rows: the first Linear takes the bf16 GEMM path (reads the shadow); a stale shadow
+    # would hold the old random weights and miss this reference completely
+    x = torch.randn(6000, 768, device=DEV)
+    with torch.no_grad():
+        y = m(x)
+    h = torch.relu(x.to(torch.bfloat16).float() @ sd["0.weight"].to(torch.bfloat16).float().t()
+                   + sd["0.bias"])
+    ref_y = h @ sd["2.weight"].t() + sd["2.bias"]
+    err = (y.float() - ref_y).norm() / ref_y.norm()
+    assert err < 2e-2, err.item()
+    assert torch.equal(m[0].weight._dfu_shadow, sd["0.weight"].to(torch.bfloat16))
