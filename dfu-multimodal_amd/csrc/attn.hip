@@ -313,6 +313,169 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(const bf16_t* __restrict__
   }
 }
 
+// Fused backward: one workgroup (8 waves) per (b, h).  Q, K, V, dO are staged once into LDS
+// (4 r128 images), with LSE and delta = rowsum(dO * O); then the waves share one pool of work
+// items: QT query tiles (dQ, as k_attn_bwd_dq) and QT key tiles (dK/dV, as k_attn_bwd_dkv).
+template <int KT>
+__global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict__ qkv,
+                                                        const bf16_t* __restrict__ o,
+                                                        const bf16_t* __restrict__ dout,
+                                                        const float* __restrict__ lse, int N,
+                                                        int H, float scale,
+                                                        bf16_t* __restrict__ dqkv) {
+  constexpr int NPAD = KT * 16;
+  constexpr int NTH = 512, NWAVES = 8;
+  __shared__ __attribute__((aligned(16))) char smem[4 * NPAD * 128 + 2 * NPAD * 4];
+  char* Qs = smem;
+  char* Ks = smem + NPAD * 128;
+  char* Vs = smem + 2 * NPAD * 128;
+  char* Ds = smem + 3 * NPAD * 128;
+  float* Ls = (float*)(smem + 4 * NPAD * 128);
+  float* Es = Ls + NPAD;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int64_t tok_stride = (int64_t)3 * H * 64;
+  const int64_t o_stride = (int64_t)H * 64;
+  const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
+  const bf16_t* obase = o + (int64_t)b * N * o_stride + h * 64;
+  const bf16_t* dobase = dout + (int64_t)b * N * o_stride + h * 64;
+  for (int idx = tid; idx < NPAD * 8; idx += NTH) {
+    const int row = idx >> 3, chunk = idx & 7;
+    u32x4 vq = {0u, 0u, 0u, 0u}, vk = vq, vv = vq, vd = vq, vo = vq;
+    if (row < N) {
+      const bf16_t* t = qbase + (int64_t)row * tok_stride + chunk * 8;
+      vq = *(const u32x4*)t;
+      vk = *(const u32x4*)(t + H * 64);
+      vv = *(const u32x4*)(t + 2 * H * 64);
+      vd = *(const u32x4*)(dobase + (int64_t)row * o_stride + chunk * 8);
+      vo = *(const u32x4*)(obase + (int64_t)row * o_stride + chunk * 8);
+    }
+    const int off = r128_off(row, chunk);
+    *(u32x4*)(Qs + off) = vq;
+    *(u32x4*)(Ks + off) = vk;
+    *(u32x4*)(Vs + off) = vv;
+    *(u32x4*)(Ds + off) = vd;
+    float fd[8], fo[8];
+    unpack8(vd, fd);
+    unpack8(vo, fo);
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d += fd[e] * fo[e];
+    d += __shfl_xor(d, 1, 64);  // the 8 chunks of a row are 8 consecutive lanes
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (chunk == 0) {
+      Es[row] = row < N ? d : 0.f;
+      Ls[row] = row < N ? lse[(int64_t)bh * NPAD + row] * LOG2E : 0.f;
+    }
+  }
+  __syncthreads();
+  const float c = scale * LOG2E;
+  const int QT = (N + 15) / 16;
+  for (int it = wave; it < 2 * QT; it += NWAVES) {
+    if (it < QT) {  // ---------------- dQ for query tile it
+      const int qt = it;
+      const int q = qt * 16 + (lane & 15);
+      const bool qv = q < N;
+      bf16x8 qf[2], df[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        qf[ks] = row_frag(Qs, 16 * qt, ks, lane);
+        df[ks] = row_frag(Ds, 16 * qt, ks, lane);
+      }
+      const float dsum = Es[q], lq = Ls[q];
+      f32x4 s[KT];
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * t, ks, lane), qf[ks], st, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Vs, 16 * t, ks, lane), df[ks], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = 16 * t + 4 * g + r;
+          const float pv = (qv && key < N) ? exp2f(st[r] * c - lq) : 0.f;
+          st[r] = pv * (dp[r] - dsum);
+        }
+        s[t] = st;
+      }
+      f32x4 acc[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < KT / 2; ++u) {
+        const bf16x8 dsb = pack_frag(s[2 * u], s[2 * u + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ks, u, 16 * dt, lane), dsb, acc[dt], 0, 0, 0);
+      }
+      if (qv) {
+        bf16_t* dst = dqkv + ((int64_t)b * N + q) * tok_stride + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          *(u32x2*)(dst + 16 * dt) = (u32x2){pack2(acc[dt][0] * scale, acc[dt][1] * scale),
+                                             pack2(acc[dt][2] * scale, acc[dt][3] * scale)};
+      }
+    } else {  // ---------------- dK, dV for key tile it - QT
+      const int kt = it - QT;
+      const int key = kt * 16 + (lane & 15);
+      const bool kv = key < N;
+      bf16x8 kf[2], vf[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        kf[ks] = row_frag(Ks, 16 * kt, ks, lane);
+        vf[ks] = row_frag(Vs, 16 * kt, ks, lane);
+      }
+      f32x4 dv[4], dk[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll 1
+      for (int u = 0; u < KT / 2; ++u) {
+        f32x4 ph[2], dsh[2];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int qt = 2 * u + hh;
+          f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * qt, ks, lane), kf[ks], st, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * qt, ks, lane), vf[ks], dp, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = 16 * qt + 4 * g + r;
+            const float pv = (kv && q < N) ? exp2f(st[r] * c - Ls[q]) : 0.f;
+            ph[hh][r] = pv;
+            dsh[hh][r] = pv * (dp[r] - Es[q]);
+          }
+        }
+        const bf16x8 pb = pack_frag(ph[0], ph[1]);
+        const bf16x8 db = pack_frag(dsh[0], dsh[1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ds, u, 16 * dt, lane), pb, dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Qs, u, 16 * dt, lane), db, dk[dt], 0, 0, 0);
+        }
+      }
+      if (kv) {
+        bf16_t* dst = dqkv + ((int64_t)b * N + key) * tok_stride + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          *(u32x2*)(dst + H * 64 + 16 * dt) = (u32x2){pack2(dk[dt][0] * scale, dk[dt][1] * scale),
+                                                      pack2(dk[dt][2] * scale, dk[dt][3] * scale)};
+          *(u32x2*)(dst + 2 * H * 64 + 16 * dt) = (u32x2){pack2(dv[dt][0], dv[dt][1]),
+                                                          pack2(dv[dt][2], dv[dt][3])};
+        }
+      }
+    }
+  }
+}
+
 #define DISPATCH_KT(KTV, CALL) \
   switch (KTV) {               \
     case 2: CALL(2); break;    \
@@ -353,11 +516,7 @@ extern "C" int dfu_attention_bwd(const void* qkv, const void* o, const void* dou
   DFU_CHECK_ARG(N > 0 && N <= 256, "dfu_attention_bwd: N=%d unsupported (<= 256)", N);
   const int KT = dfu_attention_npad(N) / 16;
   hipStream_t s = (hipStream_t)stream;
-#define CALL(K) hipLaunchKernelGGL(k_attn_bwd_dq<K>, dim3(B * H), dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse, N, H, scale, delta, (bf16_t*)dqkv)
-  DISPATCH_KT(KT, CALL)
-#undef CALL
-  DFU_LAUNCH_CHECK();
-#define CALL(K) hipLaunchKernelGGL(k_attn_bwd_dkv<K>, dim3(B * H), dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, N, H, scale, (bf16_t*)dqkv)
+#define CALL(K) hipLaunchKernelGGL(k_attn_bwd_fused<K>, dim3(B * H), dim3(512), 0, s, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse, N, H, scale, (bf16_t*)dqkv)
   DISPATCH_KT(KT, CALL)
 #undef CALL
   DFU_LAUNCH_CHECK();

@@ -23,7 +23,7 @@ constexpr int LDS_MAX = 160 * 1024;
 
 // OCC = workgroups per CU the variant is built for (launch bounds); OCC 2 forces a 2-stage
 // ring so two workgroups' LDS fit (their prologues/epilogues overlap each other's main loop).
-template <int TM_, int TN_, int OCC_ = 1>
+template <int TM_, int TN_, int OCC_ = 1, int NST_ = 0>
 struct Tile {
   static constexpr int TM = TM_, TN = TN_, OCC = OCC_;
   static constexpr int WGM = (TM == 256 && TN == 128) ? 4 : 2;  // wave grid
@@ -33,7 +33,9 @@ struct Tile {
   static constexpr int NLDA = TM / 64, NLDB = TN / 64;         // DMA instructions per thread
   static constexpr int A_BYTES = TM * BK * 2, B_BYTES = TN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  static constexpr int NSTAGE = (OCC == 1 && 3 * STAGE_BYTES <= LDS_MAX) ? 3 : 2;
+  // ring depth: NST_ if given, else 3 when it fits one workgroup per CU, else 2
+  static constexpr int NSTAGE =
+      NST_ ? NST_ : ((OCC == 1 && 3 * STAGE_BYTES <= LDS_MAX) ? 3 : 2);
   static constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES;
   static constexpr int DMA_PER_STAGE = NLDA + NLDB;
   static_assert(OCC * LDS_BYTES <= LDS_MAX, "LDS for the requested occupancy");
@@ -295,11 +297,23 @@ DFU_DEV bf16x8 read_frag(const char* lds, int rb, int ks, int lane) {
 
 template <int N>
 DFU_DEV void wait_vmcnt() {
-  static_assert(N == 0 || N == 4 || N == 6 || N == 8, "vmcnt literal");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Wait until at most k stages (DPS DMA instructions each) issued after the current one are
+// still in flight; k is runtime (the ring drains at the end), vmcnt needs an immediate.
+template <int DPS, int KMAX>
+DFU_DEV void wait_stages(int k) {
+  if constexpr (KMAX > 0) {
+    if (k >= KMAX) {
+      wait_vmcnt<DPS * KMAX>();
+      return;
+    }
+    wait_stages<DPS, KMAX - 1>(k);
+  } else {
+    wait_vmcnt<0>();
+  }
 }
 
 // Output row of GEMM row m: identity, or for a stride-phase dgrad launch the dX row
@@ -314,9 +328,9 @@ DFU_DEV int64_t out_row(const GemmArgs& p, int m) {
 }
 
 // ------------------------------------------------------------------------------ kernel
-template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1>
+template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0>
 __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
-  using T = Tile<TM, TN, OCC>;
+  using T = Tile<TM, TN, OCC, NST>;
   constexpr int WGM = T::WGM, WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
   constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
   __shared__ __attribute__((aligned(16))) char smem[T::LDS_BYTES];
@@ -367,21 +381,26 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
     issue_tile<BMODE, T::NLDB>(p, sb, p.B, p.ldb, p.n_ld_bound, kt, kend, tid,
                                stage + T::A_BYTES);
   };
+  // All fragment reads of the K-step (both 32-wide halves) are issued before the first MFMA,
+  // so the LDS latency overlaps MFMAs (counted lgkmcnt waits) instead of draining per group.
   auto compute = [&](const char* la) {
     const char* lb = la + T::A_BYTES;
+    bf16x8 fa[2][FM], fb[2][FN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[FM], fb[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = read_frag<AK>(la, wr * WTM + i * 16, ks, lane);
+      for (int i = 0; i < FM; ++i) fa[ks][i] = read_frag<AK>(la, wr * WTM + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
+      for (int j = 0; j < FN; ++j) fb[ks][j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][j], fa[ks][i], acc[i][j], 0, 0, 0);
   };
   // Pipeline: K-step i+NSTAGE-1 is issued (into the slot K-step i-1 vacated) right after the
   // barrier that publishes K-step i; completion is tracked with counted vmcnt (the DMA is
@@ -391,12 +410,8 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
   for (int s = 0; s < NSTAGE - 1; ++s)
     if (s < nk) issue(kt_begin + s, smem + s * T::STAGE_BYTES);
   for (int i = 0; i < nk; ++i) {
-    if constexpr (NSTAGE == 3) {
-      if (i + 1 < nk) wait_vmcnt<T::DMA_PER_STAGE>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
+    // stage i must have landed; the min(nk-i-1, NSTAGE-2) stages issued after it may fly on
+    wait_stages<T::DMA_PER_STAGE, NSTAGE - 2>(nk - i - 1);
     __builtin_amdgcn_s_barrier();
     if (i + NSTAGE - 1 < nk)
       issue(kt_begin + i + NSTAGE - 1, smem + ((i + NSTAGE - 1) % NSTAGE) * T::STAGE_BYTES);
