@@ -57,7 +57,7 @@ __global__ void k_ln_fwd(const float* __restrict__ x, int64_t ldx, int rows, int
   }
 }
 
-constexpr int LNB_ROWS = 32;  // rows per block in the backward (8 per wave)
+constexpr int LNB_ROWS = 16;  // rows per block in the backward (4 per wave): 788 blocks at B=64
 
 template <bool DY_BF>
 __global__ void k_ln_bwd(const void* __restrict__ dyv, int64_t lddy, const float* __restrict__ x,

@@ -116,16 +116,38 @@ class FusedAdamW(torch.optim.Optimizer):
         return loss
 
     def state_dict(self):
+        """torch.optim.AdamW's layout: per-parameter {'step', 'exp_avg', 'exp_avg_sq'} keyed by
+        parameter index, so checkpoints interchange with the reference's optimizer
+        (train_multimodal_fusion.py:347, 436).  The moments are views of the flat buffers."""
         sd = super().state_dict()
-        sd["dfu_flat"] = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
-                          "step": self.step_dev}
+        step = torch.tensor(float(self.step_dev.item()))
+        index = {id(p): i for i, p in enumerate(self.param_groups[0]["params"])}
+        for j, p in enumerate(self.flat.params):
+            o, n = self.flat.offsets[j], p.numel()
+            sd["state"][index[id(p)]] = {
+                "step": step.clone(),
+                "exp_avg": self.exp_avg[o:o + n].view_as(p),
+                "exp_avg_sq": self.exp_avg_sq[o:o + n].view_as(p),
+            }
         return sd
 
     def load_state_dict(self, state_dict):
-        flat = state_dict.get("dfu_flat")
-        sd = {k: v for k, v in state_dict.items() if k != "dfu_flat"}
-        super().load_state_dict(sd)
-        if flat is not None:
-            self.exp_avg.copy_(flat["exp_avg"])
-            self.exp_avg_sq.copy_(flat["exp_avg_sq"])
-            self.step_dev.copy_(flat["step"])
+        """Accepts torch.optim.AdamW state dicts (and this class's own)."""
+        state = state_dict.get("state", {})
+        super().load_state_dict({"state": {}, "param_groups": state_dict["param_groups"]})
+        params = self.param_groups[0]["params"]
+        index = {id(p): i for i, p in enumerate(params)}
+        steps = set()
+        with torch.no_grad():
+            for j, p in enumerate(self.flat.params):
+                st = state.get(index[id(p)])
+                if not st:
+                    continue
+                o, n = self.flat.offsets[j], p.numel()
+                self.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"FusedAdamW: parameters at different steps {sorted(steps)}")
+        if steps:
+            self.step_dev.fill_(steps.pop())
