@@ -183,11 +183,14 @@ def main():
     reducer = parallel.GradAllReducer(opt.flat, overlap=False) if world > 1 else None
     rgb, th, y = synthetic(args.batch, dev, seed=42 + rank)
 
+    from dfu_hip import functional as Fn
+
     def fwd_bwd():
         opt.zero_grad()
         out = fwd(model, rgb, th)
         loss = crit(out, y)
         loss.backward()
+        Fn.join_grad_streams()  # the thermal branch's side stream rejoins (graph capture needs it)
         return loss
 
     def tail():

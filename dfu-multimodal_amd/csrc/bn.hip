@@ -15,44 +15,38 @@ __global__ void k_bn_finalize(const float* __restrict__ stats, int tiles, int M,
                               float* __restrict__ rvar, int64_t* __restrict__ nbt,
                               float* __restrict__ mean_out, float* __restrict__ invstd_out,
                               float* __restrict__ scale_out, float* __restrict__ shift_out) {
-  __shared__ double sh_n[4][64], sh_mean[4][64], sh_m2[4][64];
+  // Per tile t (nb rows): sum sb and M2 qb -> sum of squares qb + sb^2/nb.  fp64 sums of x and
+  // x^2 over <= 1e6 rows of bf16-scale values keep var = E[x^2] - mean^2 exact to ~1e-12
+  // relative, and the tile loop is independent adds (no serial merge chain).
+  __shared__ double sh_s[4][64], sh_q[4][64];
   const int tl = threadIdx.x & 63, cl = threadIdx.x >> 6;
   const int c = blockIdx.x * 4 + cl;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
+  double sx = 0.0, sxx = 0.0;
   if (c < C) {
+    const int last = tiles - 1;
+    const double inv_last = 1.0 / (double)(M - last * 128);
+#pragma unroll 4
     for (int t = tl; t < tiles; t += 64) {
-      const double nb = (double)min(128, M - t * 128);
       const double sb = stats[((int64_t)t * 2 + 0) * C + c];
       const double qb = stats[((int64_t)t * 2 + 1) * C + c];
-      const double mb = sb / nb;
-      const double nt = n + nb;
-      const double d = mb - mean;
-      mean += d * nb / nt;
-      m2 += qb + d * d * n * nb / nt;
-      n = nt;
+      sx += sb;
+      sxx += qb + sb * sb * (t == last ? inv_last : (1.0 / 128.0));
     }
   }
-  sh_n[cl][tl] = n;
-  sh_mean[cl][tl] = mean;
-  sh_m2[cl][tl] = m2;
+  sh_s[cl][tl] = sx;
+  sh_q[cl][tl] = sxx;
   __syncthreads();
-  for (int s = 32; s > 0; s >>= 1) {
-    if (tl < s) {
-      const double na = sh_n[cl][tl], nb = sh_n[cl][tl + s];
-      const double nt = na + nb;
-      if (nb > 0.0) {
-        const double d = sh_mean[cl][tl + s] - sh_mean[cl][tl];
-        sh_mean[cl][tl] += d * nb / nt;
-        sh_m2[cl][tl] += sh_m2[cl][tl + s] + d * d * na * nb / nt;
-        sh_n[cl][tl] = nt;
-      }
+  for (int st = 32; st > 0; st >>= 1) {
+    if (tl < st) {
+      sh_s[cl][tl] += sh_s[cl][tl + st];
+      sh_q[cl][tl] += sh_q[cl][tl + st];
     }
     __syncthreads();
   }
   if (tl == 0 && c < C) {
-    const double nn = sh_n[cl][0];
-    const double mu = sh_mean[cl][0];
-    const double var = sh_m2[cl][0] / nn;  // biased, used to normalise
+    const double nn = (double)M;
+    const double mu = sh_s[cl][0] / nn;
+    const double var = fmax(sh_q[cl][0] / nn - mu * mu, 0.0);  // biased, used to normalise
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f;
     const float b = beta ? beta[c] : 0.f;
@@ -62,7 +56,7 @@ __global__ void k_bn_finalize(const float* __restrict__ stats, int tiles, int M,
     shift_out[c] = b - (float)mu * g * invstd;
     if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
     if (rvar) {
-      const double unb = nn > 1.0 ? sh_m2[cl][0] / (nn - 1.0) : var;
+      const double unb = nn > 1.0 ? var * nn / (nn - 1.0) : var;
       rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
     }
   }
@@ -80,22 +74,33 @@ __global__ void k_bn_eval_coeffs(const float* gamma, const float* beta, const fl
 }
 
 // ---------------------------------------------------------------- forward apply
+// Grid-stride elementwise kernels over [M][C] bf16 in 8-channel vectors.  With 256-thread
+// blocks and C/8 a power of two <= 256 (every ResNet-50 width) the stride is a multiple of C/8,
+// so a thread's channel group never changes: FIXED kernels decode it once and keep the
+// per-channel constants in registers (no per-vector 64-bit modulo, no per-element loads).
+template <bool FIXED>
 __global__ void k_bn_apply(const bf16_t* __restrict__ y, const float* __restrict__ scale,
                            const float* __restrict__ shift, const bf16_t* __restrict__ res,
                            int relu, bf16_t* __restrict__ out, int64_t M, int C) {
   const int cv = C / 8;
   const int64_t n = M * cv;
+  float sc[8], sf[8];
+  auto load_coef = [&](int c0) {
+    const f32x4 s0 = *(const f32x4*)(scale + c0), s1 = *(const f32x4*)(scale + c0 + 4);
+    const f32x4 h0 = *(const f32x4*)(shift + c0), h1 = *(const f32x4*)(shift + c0 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sc[e] = s0[e]; sc[e + 4] = s1[e]; sf[e] = h0[e]; sf[e + 4] = h1[e];
+    }
+  };
+  if (FIXED) load_coef((threadIdx.x & (cv - 1)) * 8);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * 8;
+    if (!FIXED) load_coef((int)(i % cv) * 8);
     float f[8];
     unpack8(*(const u32x4*)(y + i * 8), f);
     float r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (res) unpack8(*(const u32x4*)(res + i * 8), r);
-    const f32x4 s0 = *(const f32x4*)(scale + c0), s1 = *(const f32x4*)(scale + c0 + 4);
-    const f32x4 h0 = *(const f32x4*)(shift + c0), h1 = *(const f32x4*)(shift + c0 + 4);
-    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-    const float sf[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float v = fmaf(f[e], sc[e], sf[e]) + r[e];
@@ -103,6 +108,11 @@ __global__ void k_bn_apply(const bf16_t* __restrict__ y, const float* __restrict
     }
     *(u32x4*)(out + i * 8) = pack8(f);
   }
+}
+
+inline bool fixed_channels(int C) {
+  const int cv = C / 8;
+  return cv > 0 && cv <= 256 && (cv & (cv - 1)) == 0;
 }
 
 // ---------------------------------------------------------------- backward
@@ -201,6 +211,9 @@ __global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int blocks,
   }
 }
 
+// dy = k (g - m1 - xhat m2), xhat = (y - mean) invstd  ==  a g + b y + c per channel with
+// a = k, b = -k m2 invstd, c = k (m2 invstd mean - m1).
+template <bool FIXED>
 __global__ void k_bn_bwd_apply(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ y,
                                const bf16_t* __restrict__ out, int relu,
                                const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -208,9 +221,22 @@ __global__ void k_bn_bwd_apply(const bf16_t* __restrict__ dout, const bf16_t* __
                                bf16_t* __restrict__ dy, bf16_t* __restrict__ dres) {
   const int cv = C / 8;
   const int64_t n = M * cv;
+  float ka[8], kb[8], kc[8];
+  auto load_coef = [&](int c0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      const float k = coef[3 * c], m1 = coef[3 * c + 1], m2 = coef[3 * c + 2];
+      const float is = invstd[c];
+      ka[e] = k;
+      kb[e] = -k * m2 * is;
+      kc[e] = k * (m2 * is * mean[c] - m1);
+    }
+  };
+  if (FIXED) load_coef((threadIdx.x & (cv - 1)) * 8);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * 8;
+    if (!FIXED) load_coef((int)(i % cv) * 8);
     float g[8], yy[8];
     unpack8(*(const u32x4*)(dout + i * 8), g);
     unpack8(*(const u32x4*)(y + i * 8), yy);
@@ -223,11 +249,7 @@ __global__ void k_bn_bwd_apply(const bf16_t* __restrict__ dout, const bf16_t* __
     if (dres) *(u32x4*)(dres + i * 8) = pack8(g);
     float d[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
-      const float xh = (yy[e] - mean[c]) * invstd[c];
-      d[e] = coef[3 * c] * (g[e] - coef[3 * c + 1] - xh * coef[3 * c + 2]);
-    }
+    for (int e = 0; e < 8; ++e) d[e] = fmaf(ka[e], g[e], fmaf(kb[e], yy[e], kc[e]));
     *(u32x4*)(dy + i * 8) = pack8(d);
   }
 }
@@ -270,7 +292,8 @@ extern "C" int dfu_bn_apply(const void* y, const float* scale, const float* shif
                             const void* residual, int32_t relu, void* out, int64_t M, int32_t C,
                             void* stream) {
   DFU_CHECK_ARG(y && scale && shift && out && C % 8 == 0 && M > 0, "dfu_bn_apply: bad args");
-  hipLaunchKernelGGL(k_bn_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(fixed_channels(C) ? k_bn_apply<true> : k_bn_apply<false>,
+                     dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)y, scale, shift, (const bf16_t*)residual, relu, (bf16_t*)out,
                      M, C);
   DFU_LAUNCH_CHECK();
@@ -316,7 +339,8 @@ extern "C" int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out
   DFU_CHECK_ARG(dout && y && mean && invstd && coef && dy && C % 8 == 0 && M > 0,
                 "dfu_bn_bwd_apply: bad args");
   DFU_CHECK_ARG(!relu || out, "dfu_bn_bwd_apply: relu needs out");
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(fixed_channels(C) ? k_bn_bwd_apply<true> : k_bn_bwd_apply<false>,
+                     dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, relu, mean, invstd,
                      coef, M, C, (bf16_t*)dy, (bf16_t*)dres);
   DFU_LAUNCH_CHECK();

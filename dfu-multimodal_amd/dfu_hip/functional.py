@@ -45,14 +45,51 @@ def remove_grad_ready_hook(fn):
         _grad_ready_hooks.remove(fn)
 
 
+# Streams that wrote persistent parameter gradients since the last join.  Autograd synchronises
+# only the gradients it returns; these buffers are written in place (possibly on a branch's side
+# stream, see models.fusion), so consumers (FusedAdamW.step, GradAllReducer.finish) join first.
+_grad_streams = {}
+
+
 def grad_buffer(p):
-    """Persistent fp32 gradient buffer of parameter p (zeroed on first use)."""
+    """Persistent fp32 gradient buffer of parameter p (zeroed on first use); notes the current
+    stream as a gradient producer."""
     g = p.grad
     if g is None:
         g = torch.empty_like(p, memory_format=torch.contiguous_format)
         ops.zero_(g)
         p.grad = g
+    if g.is_cuda:
+        st = torch.cuda.current_stream(g.device)
+        _grad_streams[(st.device_index, st.stream_id)] = st
     return g
+
+
+def join_grad_streams(stream=None, clear=True):
+    """Make `stream` (default: the current stream) wait for every stream that wrote parameter
+    gradients since the last clearing join."""
+    if not _grad_streams:
+        return
+    cur = stream if stream is not None else torch.cuda.current_stream()
+    for st in _grad_streams.values():
+        if st != cur:
+            cur.wait_stream(st)
+    if clear:
+        _grad_streams.clear()
+
+
+_side_streams = {}
+
+
+def side_stream(device):
+    """One persistent side stream per device for the concurrent encoder branch."""
+    idx = torch.device(device).index
+    if idx is None:
+        idx = torch.cuda.current_device()
+    st = _side_streams.get(idx)
+    if st is None:
+        st = _side_streams[idx] = torch.cuda.Stream(device=idx)
+    return st
 
 
 def grads_done(*params):
@@ -612,6 +649,8 @@ class TokenNormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if g.is_cuda:  # produced on the fusion head's stream; the ViT may run on a side stream
+            g.record_stream(torch.cuda.current_stream())
         x, mean, rstd = ctx.saved_tensors
         norm = ctx.norm
         B, T, D = x.shape

@@ -18,6 +18,7 @@ view) and ``p.grad`` into a matching flat gradient buffer, so:
 """
 import torch
 
+from . import functional as Fn
 from . import ops
 
 _ALIGN = 4  # elements (16 B) so every tensor view starts 16-byte aligned
@@ -106,6 +107,7 @@ class FusedAdamW(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        Fn.join_grad_streams()
         if self.check_grads:
             self.flat.rebind_grads()
         g = self.param_groups[0]

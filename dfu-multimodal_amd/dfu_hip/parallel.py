@@ -86,7 +86,9 @@ class GradAllReducer:
         lo, hi, _ = self.buckets[k]
         view = self.flat.grad[lo:hi]
         if self.stream is not None:
+            # a bucket may hold gradients of both encoder branches (two streams): wait for all
             self.stream.wait_stream(torch.cuda.current_stream())
+            Fn.join_grad_streams(self.stream, clear=False)
             with torch.cuda.stream(self.stream):
                 dist.all_reduce(view, group=self.group)
                 view.mul_(1.0 / self.world)
@@ -107,6 +109,7 @@ class GradAllReducer:
                 break
 
     def finish(self):
+        Fn.join_grad_streams()
         if self.world <= 1:
             return
         if self._issued is None:

@@ -48,9 +48,10 @@ class MultimodalFusionModel(tnn.Module):
     """
 
     def __init__(self, num_classes=2, dropout=0.7, hidden_dims=(512,), layout="eval",
-                 pretrained=False):
+                 pretrained=False, concurrent_branches=True):
         super().__init__()
         self.layout = layout
+        self.concurrent_branches = concurrent_branches
         rgb = resnet50(pretrained=pretrained)
         rgb.fc = tnn.Identity()
         th = vit_base_patch16_224(pretrained=pretrained, num_classes=0)
@@ -67,10 +68,28 @@ class MultimodalFusionModel(tnn.Module):
         else:
             raise ValueError(f"layout must be 'eval' or 'train', got {layout!r}")
 
+    def _encode(self, rgb_net, th_net, rgb, thermal):
+        """Both encoders; on the GPU the thermal ViT runs on a side stream concurrently with the
+        ResNet on the current stream (their kernels fill each other's idle CUs).  Backward ops
+        run on their forward op's stream (autograd), and parameter-gradient producers are
+        joined by FusedAdamW.step / GradAllReducer.finish (functional.join_grad_streams)."""
+        if not (self.concurrent_branches and rgb.is_cuda):
+            return rgb_net(rgb), th_net(thermal)
+        main = torch.cuda.current_stream()
+        side = Fn.side_stream(rgb.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            thermal.record_stream(side)
+            th_feat = th_net(thermal)
+        rgb_feat = rgb_net(rgb)
+        main.wait_stream(side)
+        th_feat.record_stream(main)
+        return rgb_feat, th_feat
+
     def forward(self, rgb, thermal):
         if self.layout == "eval":
-            return self.fusion(self.resnet(rgb), self.vit(thermal))
-        f = Fn.ConcatFn.apply(self.rgb_branch(rgb), self.thermal_branch(thermal))
+            return self.fusion(*self._encode(self.resnet, self.vit, rgb, thermal))
+        f = Fn.ConcatFn.apply(*self._encode(self.rgb_branch, self.thermal_branch, rgb, thermal))
         return self.fusion(f)
 
 
