@@ -1,0 +1,51 @@
+"""The encoders run on two streams (models.fusion: ViT on a side stream).  Every kernel of the
+step is deterministic (split-K through fp32 slabs, BN statistics by fixed-order merges), so two
+training steps with concurrent branches must match two serialized steps BITWISE — logits, loss,
+every gradient and every updated parameter.  A missing stream join or a buffer reused across
+streams shows up here as a mismatch."""
+import pytest
+import torch
+
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _run(concurrent, steps=2):
+    from dfu_hip import nn as hnn
+    from dfu_hip.optim import FusedAdamW
+    from models.fusion import MultimodalFusionModel
+    torch.manual_seed(0)
+    ref = R.MultimodalFusionModel(num_classes=2, dropout=0.0)
+    m = MultimodalFusionModel(num_classes=2, dropout=0.0, concurrent_branches=concurrent)
+    m.load_state_dict(ref.state_dict())
+    m = m.to(DEV).train()
+    opt = FusedAdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    rgb, th, y = R.synthetic_batch(16, seed=3)
+    rgb, th, y = rgb.to(DEV), th.to(DEV), y.to(DEV)
+    crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=DEV))
+    outs, grads = [], None
+    for _ in range(steps):
+        opt.zero_grad()
+        out = m(rgb, th)
+        loss = crit(out, y)
+        loss.backward()
+        if grads is None:
+            torch.cuda.synchronize()
+            grads = {n: p.grad.clone() for n, p in m.named_parameters()}
+        opt.step()
+        outs.append((out.detach().clone(), loss.detach().clone()))
+    torch.cuda.synchronize()
+    return outs, grads, {n: p.detach().clone() for n, p in m.named_parameters()}
+
+
+def test_concurrent_branches_bitwise_equal_to_serial():
+    o1, g1, p1 = _run(True)
+    o0, g0, p0 = _run(False)
+    for (a, la), (b, lb) in zip(o1, o0):
+        assert torch.equal(a, b) and torch.equal(la, lb)
+    bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+    assert not bad, f"gradients differ: {bad[:5]}"
+    bad = [n for n in p0 if not torch.equal(p0[n], p1[n])]
+    assert not bad, f"parameters differ after two steps: {bad[:5]}"
