@@ -10,9 +10,9 @@ using namespace dfu;
 namespace {
 
 constexpr int kCUs = 256;
-constexpr int kTM[NTILES] = {128, 256, 128, 256, 128, 128};
-constexpr int kTN[NTILES] = {128, 128, 256, 256, 128, 128};
-constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 1};  // workgroups per CU
+constexpr int kTM[NTILES] = {128, 256, 128, 256, 128};
+constexpr int kTN[NTILES] = {128, 128, 256, 256, 128};
+constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2};  // workgroups per CU
 // Wave-quantisation cost model: a launch takes ceil(tiles * splits / 256) rounds (one 512-thread
 // workgroup per CU), each costing kRoundUs (prologue fill + epilogue) + k-steps * kStepUs.
 // Fitted on MI355X to tools/gemm_bench.py --sweep (ViT qkv K=768 vs fc2 K=3072 forward rows,
@@ -20,16 +20,16 @@ constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 1};  // workgroups per CU
 // 256x256 moves 1.62x more MFMA work per microsecond than 128x128.
 // The 2-per-CU 128x128 variant: two co-resident workgroups share the MFMA pipe (step cost per
 // workgroup ~doubles) but hide each other's fill and epilogue.
-constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70, 0.57};
-constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1, 5.5};
+constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70};
+constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1};
 constexpr double kSlabGBs = 5000.0;  // split-K: slab write + reduce (read slabs, RMW C)
 constexpr double kReduceLaunchUs = 2.0;
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
-                               kTable128x128o2, kTable128x128s4};
+                               kTable128x128o2};
   const int ns[NTILES] = {kTable128x128N, kTable256x128N, kTable128x256N, kTable256x256N,
-                          kTable128x128o2N, kTable128x128s4N};
+                          kTable128x128o2N};
   for (int i = 0; i < ns[tile]; ++i) {
     const Entry& en = tabs[tile][i];
     if (en.a == a && en.b == b && en.e == e) return &en;

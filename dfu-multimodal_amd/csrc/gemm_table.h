@@ -9,10 +9,7 @@ struct Entry {
   gemm_fn fn;
   int lds_bytes;
 };
-enum TileId {
-  T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, T128x128o2 = 4, T128x128s4 = 5,
-  NTILES = 6
-};
+enum TileId { T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, T128x128o2 = 4, NTILES = 5 };
 extern const Entry kTable128x128[];
 extern const int kTable128x128N;
 extern const Entry kTable256x128[];
@@ -23,8 +20,6 @@ extern const Entry kTable256x256[];
 extern const int kTable256x256N;
 extern const Entry kTable128x128o2[];
 extern const int kTable128x128o2N;
-extern const Entry kTable128x128s4[];
-extern const int kTable128x128s4N;
 }  // namespace dfu
 
 #define DFU_ENTRY(A, B, E, TMv, TNv, TID) \

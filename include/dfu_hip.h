@@ -87,8 +87,8 @@ typedef struct dfu_gemm_desc {
   int32_t conv_k, conv_r, conv_s;         /* output channels, filter R,S           */
   int32_t conv_stride, conv_pad;
   int32_t conv_p, conv_q;                 /* output H,W                            */
-  int32_t tile;        /* 0 = auto; 1..6 = 128x128, 256x128, 128x256, 256x256,
-                          128x128 at 2 workgroups/CU, 128x128 with a 4-deep ring */
+  int32_t tile;        /* 0 = auto; 1..5 = 128x128, 256x128, 128x256, 256x256,
+                          128x128 at 2 workgroups/CU                         */
   void* workspace;     /* split-K fp32 slabs (dfu_gemm_workspace_bytes); NULL =  */
   int64_t workspace_bytes; /*   split-K partials accumulate with fp32 atomics     */
 } dfu_gemm_desc;
@@ -98,7 +98,7 @@ int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
 int dfu_gemm_stats_tiles(int32_t M);
 /* Workspace bytes for deterministic split-K slabs of this descriptor (0 if not split). */
 int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* desc);
-/* The tile (1..6, as dfu_gemm_desc.tile) and split-K the cost model picks for this descriptor. */
+/* The tile (1..5, as dfu_gemm_desc.tile) and split-K the cost model picks for this descriptor. */
 int dfu_gemm_plan(const dfu_gemm_desc* desc, int32_t* tile, int32_t* split_k);
 /* Exact fp32 GEMM for the tiny fusion head (train_multimodal_fusion.py:305-313):
  * C[m][n] = accumulate*C[m][n] + sum_k A[m*sam + k*sak] * B[n*sbn + k*sbk] (+bias[n]) (relu). */

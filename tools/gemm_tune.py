@@ -1,7 +1,7 @@
 """Offline GEMM plan tuning on MI355X -> dfu-multimodal_amd/csrc/gemm_tuned.inc.
 
 Records every dfu_gemm launch of one real training step (bench.py's model and batch), and for
-each distinct descriptor times every tile shape (1..6) x split-K candidate (weight gradients),
+each distinct descriptor times every tile shape (1..5) x split-K candidate (weight gradients),
 keeping the fastest.  The generated table is compiled into libdfu_hip.so and takes precedence
 over the analytic cost model (csrc/gemm.hip), so plans are deterministic (no runtime tuning).
 
@@ -98,7 +98,7 @@ def main():
         best = (t_auto, 0, 0)
         ktiles = (d0.K + 63) // 64
         splits = [s for s in SPLITS if s <= ktiles] if d0.epilogue == L.EPI_F32_ACC else [1]
-        for tile in range(1, 7):
+        for tile in range(1, 6):
             for sk in splits:
                 d = copy_desc(d0)
                 d.tile, d.split_k = tile, sk
@@ -127,7 +127,7 @@ def main():
     with open(a.out, "w") as f:
         f.write("// Generated by tools/gemm_tune.py on MI355X (gfx950): fastest tile/split-K per GEMM of\n"
                 "// the DFU training step. Fields: a_mode, b_mode, epilogue, M, N, K, conv n,h,w,c,k,r,s,"
-                "stride,pad,\n// tile (1..6), split.\n")
+                "stride,pad,\n// tile (1..5), split.\n")
         for ln in keep + lines:
             f.write(ln + "\n")
     print(f"wrote {len(keep) + len(lines)} entries to {a.out}")
