@@ -123,7 +123,7 @@ def gemm_traffic():
     (profiles/r*_gemm_traffic.json, written by tools/prof_summary.py from separate rocprofv3
     --pmc FETCH_SIZE / WRITE_SIZE passes of this bench; bench.py cannot read counters itself)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_gemm_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_gemm_traffic.json")), key=os.path.getmtime)
     if not files:
         return None, None
     with open(files[-1]) as f:

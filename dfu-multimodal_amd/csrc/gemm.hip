@@ -134,16 +134,18 @@ __global__ void k_splitk_reduce(const float* __restrict__ slab, int splits, int 
   }
 }
 
+// Any N (e.g. the stem's 7x7x3 = 147 weight columns): one thread per (row, column); rows on
+// blockIdx.y, so no per-element 64-bit division.
 __global__ void k_splitk_reduce_scalar(const float* __restrict__ slab, int splits, int M, int N,
                                        float* __restrict__ C, int64_t ldc) {
-  const int64_t n = (int64_t)M * N;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += slab[k * n + i];
-    const int64_t m = i / N;
-    C[m * ldc + (i - m * N)] += s;
-  }
+  const int64_t plane = (int64_t)M * N;
+  for (int m = blockIdx.y; m < M; m += gridDim.y)
+    for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
+      const int64_t i = (int64_t)m * N + n;
+      float s = 0.f;
+      for (int k = 0; k < splits; ++k) s += slab[k * plane + i];
+      C[(int64_t)m * ldc + n] += s;
+    }
 }
 
 }  // namespace
@@ -370,8 +372,9 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
       hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, a.slab, splits,
                          d->M, d->N, (float*)d->C, d->ldc);
     else
-      hipLaunchKernelGGL(k_splitk_reduce_scalar, dim3((unsigned)blocks), dim3(256), 0, s, a.slab,
-                         splits, d->M, d->N, (float*)d->C, d->ldc);
+      hipLaunchKernelGGL(k_splitk_reduce_scalar,
+                         dim3((unsigned)((d->N + 255) / 256), (unsigned)(d->M < 4096 ? d->M : 4096)),
+                         dim3(256), 0, s, a.slab, splits, d->M, d->N, (float*)d->C, d->ldc);
     DFU_LAUNCH_CHECK();
   }
   return DFU_OK;

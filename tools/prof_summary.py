@@ -52,11 +52,12 @@ EPI = ["BF16", "BF16_RELU", "BF16_GELU", "F32", "F32_RESID", "BF16_DGELU", "BF16
 
 
 def gemm_label(name):
-    m = re.search(r"gemm_kernel<(\d+), (\d+), (\d+), (\d+), (\d+)>", name)
+    m = re.search(r"gemm_kernel<(\d+), (\d+), (\d+), (\d+), (\d+)(?:, (\d+))?(?:, \d+)?>", name)
     if not m:
         return short(name)
-    a, b, e, tm, tn = map(int, m.groups())
-    return f"gemm {OPND[a]} x {OPND[b]} -> {EPI[e]} {tm}x{tn}"
+    a, b, e, tm, tn = map(int, m.groups()[:5])
+    occ = f" x{m.group(6)}/CU" if m.group(6) and m.group(6) != "1" else ""
+    return f"gemm {OPND[a]} x {OPND[b]} -> {EPI[e]} {tm}x{tn}{occ}"
 
 
 def pmc_by_kernel(path, counter):
@@ -94,6 +95,8 @@ def main():
         return GS if ("gemm_kernel<" in n or "k_splitk_reduce" in n) else S
     total = sum(float(r["TotalDurationNs"]) / 1e6 / per_step(r) for r in rows)
     print(f"# {a.title}\n")
+    print("Kernel durations are summed per step; the encoders run on two streams, so the sum "
+          "exceeds the step's wall time (and the profiler itself reduces the overlap).\n")
     print(f"Source: `{a.stats}`; {S} steps executed by the profiled command "
           f"(GEMM launches: {GS:.2f} steps' worth, incl. bench.py's roofline replays); kernel time "
           f"**{total:.3f} ms per step**.\n")
