@@ -24,6 +24,10 @@ constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70};
 constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1};
 constexpr double kSlabGBs = 5000.0;  // split-K: slab write + reduce (read slabs, RMW C)
 constexpr double kReduceLaunchUs = 2.0;
+// Persistent schedule (gemm_kernel.h): a workgroup owning several work units pays one
+// prologue fill for all of them plus, per unit, the epilogue time its MFMAs do not hide.
+constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2};
+int g_persistent = 1;  // dfu_gemm_set_persistent
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
@@ -99,8 +103,11 @@ Plan plan_gemm(const dfu_gemm_desc* d) {
       const int kps = cdiv(ktiles, s);
       const int se = cdiv(ktiles, kps);
       if (se != s && s != s_lo) continue;
-      const int rounds = cdiv(tiles * se, kCUs * kOcc[t]);
-      double cost = rounds * (kRoundUs[t] + kps * kStepUs[t]);
+      const int slots = kCUs * kOcc[t];
+      const int rounds = cdiv(tiles * se, slots);
+      double cost = (g_persistent && tiles * se > slots)
+                        ? kRoundUs[t] + rounds * (kps * kStepUs[t] + kUnitUs[t])
+                        : rounds * (kRoundUs[t] + kps * kStepUs[t]);
       if (se > 1)
         cost += kReduceLaunchUs + 4.0 * (se + 2) * (double)d->M * d->N / (kSlabGBs * 1e3);
       if (cost < best.cost) {
@@ -168,6 +175,12 @@ extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* spl
   *tile = pl.tile + 1;
   *split_k = pl.split;
   return DFU_OK;
+}
+
+extern "C" int dfu_gemm_set_persistent(int32_t enable) {
+  const int old = g_persistent;
+  g_persistent = enable != 0;
+  return old;
 }
 
 namespace {
@@ -331,6 +344,10 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   a.aux_out = d->aux_out; a.ldaux_out = d->ldaux_out;
   a.stats = d->stats;
   a.split = splits;
+  a.n4 = (d->N % 4 == 0 && d->ldc % 4 == 0 && (d->aux == nullptr || d->ldaux % 4 == 0) &&
+          (d->aux_out == nullptr || d->ldaux_out % 4 == 0))
+             ? 1
+             : 0;
   a.slab = nullptr;
   if (acc_epi && splits > 1 && d->workspace != nullptr &&
       d->workspace_bytes >= (int64_t)splits * d->M * d->N * 4)
@@ -360,8 +377,24 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
     a.div_s = make_fastdiv(a.cs);
     if (d->b_mode == DFU_OPND_CONV_WGRAD_X) a.n_ld_bound = d->N;
   }
-  dim3 grid(a.tiles_m * a.tiles_n, splits);
-  hipLaunchKernelGGL(pl.entry->fn, grid, dim3(NT), 0, s, a);
+  // the epilogue addresses its outputs by 32-bit offsets within a 2 GiB buffer range
+  const bool c32 = d->epilogue == DFU_EPI_F32 || d->epilogue == DFU_EPI_F32_RESID ||
+                   d->epilogue == DFU_EPI_F32_ACC || d->epilogue == DFU_EPI_PATCH;
+  int64_t c_rows = d->M;
+  if (ph) c_rows = (int64_t)d->conv_n * d->conv_h * d->conv_w;
+  if (d->epilogue == DFU_EPI_PATCH && d->ep_tokens > 0)
+    c_rows = (int64_t)(d->M / d->ep_tokens) * (d->ep_tokens + 1);
+  DFU_CHECK_ARG(c_rows * d->ldc * (c32 ? 4 : 2) < kRsrcBytes &&
+                    (a.slab == nullptr || (int64_t)splits * d->M * d->N * 4 < kRsrcBytes),
+                "dfu_gemm: output larger than the 2 GiB epilogue buffer range");
+  // Persistent schedule: at most one wave of workgroups (CUs x occupancy), each walking its
+  // work units as one K-step stream; split-K by fp32 atomics (no workspace) keeps one unit
+  // per workgroup (its atomics have no fixed vmcnt count).
+  const int units = a.tiles_m * a.tiles_n * splits;
+  const int slots = kCUs * kOcc[pl.tile];
+  const bool atomics = acc_epi && splits > 1 && a.slab == nullptr;
+  const int nwg = (g_persistent && !atomics && units > slots) ? slots : units;
+  hipLaunchKernelGGL(pl.entry->fn, dim3(nwg), dim3(NT), 0, s, a);
   DFU_LAUNCH_CHECK();
   if (a.slab != nullptr) {
     const int64_t n = (int64_t)d->M * d->N;

@@ -13,6 +13,15 @@
 // both conflict-free; the swizzle is applied on the DMA SOURCE (the LDS write is lane-linear).
 // The MFMA is issued with the operands swapped (B fragment as "A"), so each lane ends with 4
 // consecutive output COLUMNS of one row: 8-B (bf16) / 16-B (fp32) epilogue stores.
+//
+// Persistent schedule: the grid is at most one wave of workgroups (CUs x occupancy); each
+// workgroup walks the work units u = wg, wg + G, ... (unit = output tile x K-split) as ONE
+// continuous K-step stream, so the ring never drains at a tile boundary: the next tile's first
+// stages are in flight while the current tile's epilogue runs, and the epilogue's stores drain
+// under the next tile's MFMAs.  Epilogue stores are buffer stores masked by an out-of-range
+// offset (never by a branch), so every wave issues a fixed count of them and the counted vmcnt
+// waits of the K-loop stay exact across tile boundaries (vmcnt retires loads, stores and
+// LDS-DMA of a wave in issue order; MI355X_MICROARCH.md).
 #pragma once
 #include "common.h"
 
@@ -33,12 +42,14 @@ struct Tile {
   static constexpr int NLDA = TM / 64, NLDB = TN / 64;         // DMA instructions per thread
   static constexpr int A_BYTES = TM * BK * 2, B_BYTES = TN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  // BF16_STATS epilogue scratch (per-wave column partials), after the ring in the same array
+  static constexpr int STATS_BYTES = WGM * TN * 3 * 4;
   // ring depth: NST_ if given, else 3 when it fits one workgroup per CU, else 2
   static constexpr int NSTAGE =
-      NST_ ? NST_ : ((OCC == 1 && 3 * STAGE_BYTES <= LDS_MAX) ? 3 : 2);
+      NST_ ? NST_ : ((OCC == 1 && 3 * STAGE_BYTES + STATS_BYTES <= LDS_MAX) ? 3 : 2);
   static constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES;
   static constexpr int DMA_PER_STAGE = NLDA + NLDB;
-  static_assert(OCC * LDS_BYTES <= LDS_MAX, "LDS for the requested occupancy");
+  static_assert(OCC * (LDS_BYTES + STATS_BYTES) <= LDS_MAX, "LDS for the requested occupancy");
 };
 
 struct GemmArgs {
@@ -59,7 +70,8 @@ struct GemmArgs {
   int64_t ldaux_out;
   float* stats;
   float* slab;  // split-K partial slabs [split][M][N] (F32_ACC with a workspace)
-  int split;
+  int split;    // K-splits; work units = tiles_m * tiles_n * split
+  int n4;       // N and every leading dimension % 4 == 0: one vector access per 4 columns
   int ep_tokens;
   // conv geometry
   int cn, ch, cw, cc, ck, cr, cs, cstride, cpad, cp, cq;
@@ -301,18 +313,23 @@ DFU_DEV void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// Wait until at most k stages (DPS DMA instructions each) issued after the current one are
-// still in flight; k is runtime (the ring drains at the end), vmcnt needs an immediate.
-template <int DPS, int KMAX>
-DFU_DEV void wait_stages(int k) {
-  if constexpr (KMAX > 0) {
-    if (k >= KMAX) {
-      wait_vmcnt<DPS * KMAX>();
+// Wait until at most n of this wave's youngest vector-memory operations are outstanding.  n is
+// wave-uniform but known only at run time, and vmcnt takes an immediate: wait for the largest
+// rung <= n of a ladder of immediates (a smaller count only waits longer).
+constexpr int vm_rung_below(int v) {
+  return v > 48 ? 48 : v > 40 ? 40 : v > 32 ? 32 : v > 24 ? 24 : v > 20 ? 20 : v > 16 ? 16
+         : v > 12 ? 12 : v - 1;
+}
+template <int V>
+DFU_DEV void wait_vm_le(int n) {
+  if constexpr (V <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= V) {
+      wait_vmcnt<V>();
       return;
     }
-    wait_stages<DPS, KMAX - 1>(k);
-  } else {
-    wait_vmcnt<0>();
+    wait_vm_le<vm_rung_below(V)>(n);
   }
 }
 
@@ -327,115 +344,107 @@ DFU_DEV int64_t out_row(const GemmArgs& p, int m) {
   return ((int64_t)b * p.ph_H + (int)h * p.ph_st + p.ph_h) * p.ph_W + (int)w * p.ph_st + p.ph_w;
 }
 
-// ------------------------------------------------------------------------------ kernel
-template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0>
-__global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
-  using T = Tile<TM, TN, OCC, NST>;
-  constexpr int WGM = T::WGM, WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
-  constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
-  __shared__ __attribute__((aligned(16))) char smem[T::LDS_BYTES];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wr = wave / WGN, wc = wave % WGN;
+// ------------------------------------------------------------------------------ epilogue I/O
+// Buffer descriptors with a 2 GiB range over each output / operand base: an element is masked
+// by the out-of-range offset kOOB (the store is dropped, the load reads 0), never by a branch.
+constexpr int kRsrcBytes = 0x7fffff00;
+constexpr uint32_t kOOB = 0x7fffff80u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-  // XCD-aware bijective remap (blocks b and b+8 share an XCD): each XCD gets a contiguous
-  // range of tile ids; then a grouped raster (GROUP_M x tiles_n bands walked column by
-  // column) keeps the tiles live on one XCD sharing A and B panels in its L2.
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  int wgid = bid;
-  if (nwg >= 16) {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+DFU_DEV rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, kRsrcBytes,
+                                           0x00020000);
+}
+DFU_DEV int boff(bool ok, int64_t byte_off) { return (int)(ok ? (uint32_t)byte_off : kOOB); }
+
+// Four consecutive columns n..n+3 at element index e of a row-major fp32 / bf16 matrix; okr =
+// row in range.  n4 (launch-uniform): one vector access, else four scalar accesses.
+DFU_DEV void st4_f32(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, const float* v) {
+  if (n4) {
+    const u32x4 x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                     __float_as_uint(v[3])};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, boff(okr && n < N, e * 4), 0, 0);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), r,
+                                            boff(okr && n + q < N, (e + q) * 4), 0, 0);
   }
-  constexpr int GROUP_M = 4;
-  const int band = GROUP_M * p.tiles_n;
-  const int g0 = (wgid / band) * GROUP_M;
-  const int gm = min(GROUP_M, p.tiles_m - g0);
-  const int within = wgid - (wgid / band) * band;
-  const int tm = g0 + within % gm;
-  const int tn = within / gm;
-  const int m0 = tm * TM, n0 = tn * TN;
-
-  const int kt_begin = blockIdx.y * p.kt_per_split;
-  const int kt_end = min(p.ktiles, kt_begin + p.kt_per_split);
-  const int kend = p.K;
-
-  LoadState<T::NLDA> sa;
-  LoadState<T::NLDB> sb;
-  load_init<AMODE, T::NLDA>(p, sa, p.A, p.lda, m0, p.M, tid);
-  load_init<BMODE, T::NLDB>(p, sb, p.B, p.ldb, n0, p.N, tid);
-
-  f32x4 acc[FM][FN];
+}
+DFU_DEV void st4_bf16(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, const float* v) {
+  if (n4) {
+    const u32x2 x = {pack2(v[0], v[1]), pack2(v[2], v[3])};
+    __builtin_amdgcn_raw_buffer_store_b64(x, r, boff(okr && n < N, e * 2), 0, 0);
+  } else {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  constexpr bool AK = kcontig<AMODE>();
-  constexpr bool BKc = kcontig<BMODE>();
-
-  auto issue = [&](int kt, char* stage) {
-    issue_tile<AMODE, T::NLDA>(p, sa, p.A, p.lda, p.m_ld_bound, kt, kend, tid, stage);
-    issue_tile<BMODE, T::NLDB>(p, sb, p.B, p.ldb, p.n_ld_bound, kt, kend, tid,
-                               stage + T::A_BYTES);
-  };
-  // All fragment reads of the K-step (both 32-wide halves) are issued before the first MFMA,
-  // so the LDS latency overlaps MFMAs (counted lgkmcnt waits) instead of draining per group.
-  auto compute = [&](const char* la) {
-    const char* lb = la + T::A_BYTES;
-    bf16x8 fa[2][FM], fb[2][FN];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) fa[ks][i] = read_frag<AK>(la, wr * WTM + i * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) fb[ks][j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][j], fa[ks][i], acc[i][j], 0, 0, 0);
-  };
-  // Pipeline: K-step i+NSTAGE-1 is issued (into the slot K-step i-1 vacated) right after the
-  // barrier that publishes K-step i; completion is tracked with counted vmcnt (the DMA is
-  // invisible to the compiler's waits).
-  const int nk = kt_end - kt_begin;
-#pragma unroll
-  for (int s = 0; s < NSTAGE - 1; ++s)
-    if (s < nk) issue(kt_begin + s, smem + s * T::STAGE_BYTES);
-  for (int i = 0; i < nk; ++i) {
-    // stage i must have landed; the min(nk-i-1, NSTAGE-2) stages issued after it may fly on
-    wait_stages<T::DMA_PER_STAGE, NSTAGE - 2>(nk - i - 1);
-    __builtin_amdgcn_s_barrier();
-    if (i + NSTAGE - 1 < nk)
-      issue(kt_begin + i + NSTAGE - 1, smem + ((i + NSTAGE - 1) % NSTAGE) * T::STAGE_BYTES);
-    compute(smem + (i % NSTAGE) * T::STAGE_BYTES);
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_raw_buffer_store_b16(f2bf(v[q]), r, boff(okr && n + q < N, (e + q) * 2),
+                                            0, 0);
   }
-  __syncthreads();
+}
+DFU_DEV void ld4_f32(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, float* v) {
+  if (n4) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, boff(okr && n < N, e * 4), 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = __uint_as_float(x[q]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(r, boff(okr && n + q < N, (e + q) * 4), 0, 0));
+  }
+}
+DFU_DEV void ld4_bf16(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, float* v) {
+  if (n4) {
+    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, boff(okr && n < N, e * 2), 0, 0);
+    v[0] = lo_bf(x[0]);
+    v[1] = hi_bf(x[0]);
+    v[2] = lo_bf(x[1]);
+    v[3] = hi_bf(x[1]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = bf2f(
+          __builtin_amdgcn_raw_buffer_load_b16(r, boff(okr && n + q < N, (e + q) * 2), 0, 0));
+  }
+}
 
-  // ---------------------------------------------------------------- epilogue
-  // lane holds C[m = m0 + wr*WTM + 16i + (lane&15)][n = n0 + wc*WTN + 16j + 4*(lane>>4) + r]
+// Vector-memory instructions every wave issues in one epilogue AFTER its last load (its tile
+// stores); the K-loop's waits count them.  0 = not fixed (fp32 atomics: never persistent).
+template <int EPI, class T>
+DFU_DEV int epi_stores(const GemmArgs& p) {
+  const int per = T::FM * T::FN * (p.n4 ? 1 : 4);
+  if constexpr (EPI == DFU_EPI_BF16_GELU) return 2 * per;
+  if constexpr (EPI == DFU_EPI_F32_ACC)
+    if (p.slab == nullptr && p.split > 1) return 0;
+  return per;
+}
+
+// ------------------------------------------------------------------------------ epilogue
+// lane holds C[m = m0 + wr*WTM + 16i + (lane&15)][n = n0 + wc*WTN + 16j + 4*(lane>>4) + r]
+template <int AMODE, int EPI, class T>
+DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int n0, int sidx,
+                      float* red, int tid) {
+  constexpr int FM = T::FM, FN = T::FN, WTM = T::WTM, WTN = T::WTN, WGM = T::WGM;
+  constexpr int TM = T::TM, TN = T::TN;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / T::WGN, wc = wave % T::WGN;
   const int lrow = lane & 15, lcol = 4 * (lane >> 4);
+  const bool n4 = p.n4 != 0;
+  const int M = p.M, N = p.N;
+  const rsrc_t rc = make_rsrc(p.C);
 
   if constexpr (EPI == DFU_EPI_BF16_STATS) {
-    // bf16 store + per-column (sum, M2) of this TM-row tile over the rounded values:
-    // per wave two-pass in registers, then Chan's merge across the WGM row-waves in LDS.
-    static_assert(WGM * TN * 3 * 4 <= T::LDS_BYTES, "stats scratch");
-    float* red = (float*)smem;  // [WGM][TN][3]
+    // bf16 store + per-column (sum, M2) of this TM-row tile over the rounded values: per wave
+    // two-pass in registers, then Chan's merge across the WGM row-waves in LDS.  The stats
+    // records are stored before the tile (the K-loop's waits count only the tile stores).
     float cnt = 0.f;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) cnt += (m0 + wr * WTM + 16 * i + lrow < p.M) ? 1.f : 0.f;
+    for (int i = 0; i < FM; ++i) cnt += (m0 + wr * WTM + 16 * i + lrow < M) ? 1.f : 0.f;
     cnt += __shfl_xor(cnt, 1, 64);
     cnt += __shfl_xor(cnt, 2, 64);
     cnt += __shfl_xor(cnt, 4, 64);
     cnt += __shfl_xor(cnt, 8, 64);
-    bf16_t* C = (bf16_t*)p.C;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
 #pragma unroll
@@ -446,7 +455,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
           const int m = m0 + wr * WTM + 16 * i + lrow;
           const float v = bf2f(f2bf(acc[i][j][r] * p.alpha));
           acc[i][j][r] = v;
-          s += (m < p.M) ? v : 0.f;
+          s += (m < M) ? v : 0.f;
         }
         s += __shfl_xor(s, 1, 64);
         s += __shfl_xor(s, 2, 64);
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
         for (int i = 0; i < FM; ++i) {
           const int m = m0 + wr * WTM + 16 * i + lrow;
           const float d = acc[i][j][r] - mean;
-          q += (m < p.M) ? d * d : 0.f;
+          q += (m < M) ? d * d : 0.f;
         }
         q += __shfl_xor(q, 1, 64);
         q += __shfl_xor(q, 2, 64);
@@ -472,30 +481,16 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
         }
       }
     }
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wr * WTM + 16 * i + lrow;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wc * WTN + 16 * j + lcol;
-        if (n + 3 < p.N) {
-          *(u32x2*)(C + (int64_t)m * p.ldc + n) =
-              (u32x2){pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3])};
-        } else {
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) C[(int64_t)m * p.ldc + n + r] = f2bf(acc[i][j][r]);
-        }
-      }
-    }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     // one (sum, M2) record per 128-row block: merge the row-waves that cover each block
+    const rsrc_t rs = make_rsrc(p.stats);
     constexpr int HALVES = TM / 128;
     for (int idx = tid; idx < TN * HALVES; idx += NT) {
       const int c = idx % TN, h = idx / TN;
       const int n = n0 + c;
-      if (n >= p.N || m0 + 128 * h >= p.M) continue;
       float S = 0.f, Q = 0.f, Cn = 0.f;
+#pragma unroll
       for (int w = 0; w < WGM; ++w) {
         if ((w * WTM) / 128 != h) continue;
         const float s1 = red[(w * TN + c) * 3 + 0], q1 = red[(w * TN + c) * 3 + 1];
@@ -510,133 +505,264 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
         S += s1;
         Cn += c1;
       }
+      const bool ok = n < N && m0 + 128 * h < M;
       const int64_t blk = m0 / 128 + h;
-      p.stats[(blk * 2 + 0) * p.N + n] = S;
-      p.stats[(blk * 2 + 1) * p.N + n] = Q;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(S), rs,
+                                            boff(ok, ((blk * 2 + 0) * N + n) * 4), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(Q), rs,
+                                            boff(ok, ((blk * 2 + 1) * N + n) * 4), 0, 0);
     }
-    return;
-  } else {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wr * WTM + 16 * i + lrow;
-      if (m >= p.M) continue;
-      const int64_t mo = AMODE == DFU_OPND_CONV_DGRAD ? out_row(p, m) : (int64_t)m;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int n = n0 + wc * WTN + 16 * j + lcol;
-        if (n >= p.N) continue;
-        const bool full = (n + 3 < p.N);
+        const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        st4_bf16(rc, (int64_t)m * p.ldc + n, m < M, n, N, n4, v);
+      }
+    }
+  } else {
+    constexpr bool kBias = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU || EPI == DFU_EPI_F32 ||
+                           EPI == DFU_EPI_F32_RESID || EPI == DFU_EPI_BF16_GELU ||
+                           EPI == DFU_EPI_PATCH;
+    float bias[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
+    if (kBias && p.bias) {
+      const rsrc_t rb = make_rsrc(p.bias);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wc * WTN + 16 * j + lcol;
+        ld4_f32(rb, n, true, n, N, n4, bias[j]);
+      }
+    }
+    const rsrc_t ra = make_rsrc(p.aux);
+    const rsrc_t ro = make_rsrc(EPI == DFU_EPI_F32_ACC ? (const void*)p.slab : p.aux_out);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wr * WTM + 16 * i + lrow;
+      const bool okm = m < M;
+      const int mc = okm ? m : 0;
+      const int64_t mo = AMODE == DFU_OPND_CONV_DGRAD ? out_row(p, mc) : (int64_t)mc;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wc * WTN + 16 * j + lcol;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha;
-        if constexpr (EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU || EPI == DFU_EPI_F32 ||
-                      EPI == DFU_EPI_F32_RESID || EPI == DFU_EPI_BF16_GELU ||
-                      EPI == DFU_EPI_PATCH) {
-          if (p.bias) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += (n + r < p.N) ? p.bias[n + r] : 0.f;
-          }
-        }
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha + bias[j][r];
         if constexpr (EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU) {
           if constexpr (EPI == DFU_EPI_BF16_RELU) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
           }
-          bf16_t* C = (bf16_t*)p.C + mo * p.ldc + n;
-          if (full) {
-            *(u32x2*)C = (u32x2){pack2(v[0], v[1]), pack2(v[2], v[3])};
-          } else {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) C[r] = f2bf(v[r]);
-          }
+          st4_bf16(rc, mo * p.ldc + n, okm, n, N, n4, v);
         } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
-          bf16_t* C = (bf16_t*)p.C + (int64_t)m * p.ldc + n;
-          bf16_t* Pre = (bf16_t*)p.aux_out + (int64_t)m * p.ldaux_out + n;
           float g[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) g[r] = gelu_f(v[r]);
-          if (full) {
-            *(u32x2*)Pre = (u32x2){pack2(v[0], v[1]), pack2(v[2], v[3])};
-            *(u32x2*)C = (u32x2){pack2(g[0], g[1]), pack2(g[2], g[3])};
-          } else {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) { Pre[r] = f2bf(v[r]); C[r] = f2bf(g[r]); }
-          }
+          st4_bf16(ro, mo * p.ldaux_out + n, okm, n, N, n4, v);
+          st4_bf16(rc, mo * p.ldc + n, okm, n, N, n4, g);
         } else if constexpr (EPI == DFU_EPI_F32) {
-          float* C = (float*)p.C + (int64_t)m * p.ldc + n;
-          if (full) {
-            *(f32x4*)C = (f32x4){v[0], v[1], v[2], v[3]};
-          } else {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) C[r] = v[r];
-          }
+          st4_f32(rc, mo * p.ldc + n, okm, n, N, n4, v);
         } else if constexpr (EPI == DFU_EPI_F32_RESID) {
-          float* C = (float*)p.C + (int64_t)m * p.ldc + n;
-          const float* R = (const float*)p.aux + (int64_t)m * p.ldaux + n;
-          if (full) {
-            const f32x4 rr = *(const f32x4*)R;
-            *(f32x4*)C = (f32x4){v[0] + rr[0], v[1] + rr[1], v[2] + rr[2], v[3] + rr[3]};
-          } else {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) C[r] = v[r] + R[r];
-          }
-        } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
-          bf16_t* C = (bf16_t*)p.C + mo * p.ldc + n;
-          const bf16_t* X = (const bf16_t*)p.aux + mo * p.ldaux + n;
           float x[4];
-          if (full) {
-            const u32x2 xv = *(const u32x2*)X;
-            x[0] = lo_bf(xv[0]); x[1] = hi_bf(xv[0]); x[2] = lo_bf(xv[1]); x[3] = hi_bf(xv[1]);
-          } else {
-            for (int r = 0; r < 4; ++r) x[r] = (n + r < p.N) ? bf2f(X[r]) : 0.f;
-          }
+          ld4_f32(ra, mo * p.ldaux + n, okm, n, N, n4, x);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += x[r];
+          st4_f32(rc, mo * p.ldc + n, okm, n, N, n4, v);
+        } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
+          float x[4];
+          ld4_bf16(ra, mo * p.ldaux + n, okm, n, N, n4, x);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             v[r] = (EPI == DFU_EPI_BF16_DGELU) ? v[r] * gelu_grad_f(x[r]) : v[r] + x[r];
-          if (full) {
-            *(u32x2*)C = (u32x2){pack2(v[0], v[1]), pack2(v[2], v[3])};
-          } else {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) C[r] = f2bf(v[r]);
-          }
+          st4_bf16(rc, mo * p.ldc + n, okm, n, N, n4, v);
         } else if constexpr (EPI == DFU_EPI_F32_ACC) {
           if (p.slab != nullptr) {
-            // split-K partial: plain coalesced store into this split's slab
-            float* S = p.slab + ((int64_t)blockIdx.y * p.M + m) * p.N + n;
-            if (full) {
-              *(f32x4*)S = (f32x4){v[0], v[1], v[2], v[3]};
-            } else {
-              for (int r = 0; r < 4; ++r)
-                if (n + r < p.N) S[r] = v[r];
-            }
+            // split-K partial: plain store into this split's slab
+            st4_f32(ro, ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v);
+          } else if (p.split > 1) {  // fp32 atomics: launched one unit per workgroup (host)
+            float* C = (float*)p.C + (int64_t)mc * p.ldc + n;
+            for (int r = 0; r < 4; ++r)
+              if (okm && n + r < N) atomicAdd(C + r, v[r]);
           } else {
-            float* C = (float*)p.C + (int64_t)m * p.ldc + n;
-            if (p.split > 1) {
-              for (int r = 0; r < 4; ++r)
-                if (n + r < p.N) atomicAdd(C + r, v[r]);
-            } else if (full) {
-              f32x4 c = *(f32x4*)C;
-              *(f32x4*)C = (f32x4){c[0] + v[0], c[1] + v[1], c[2] + v[2], c[3] + v[3]};
-            } else {
-              for (int r = 0; r < 4; ++r)
-                if (n + r < p.N) C[r] += v[r];
-            }
+            float c[4];
+            ld4_f32(rc, (int64_t)mc * p.ldc + n, okm, n, N, n4, c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += c[r];
+            st4_f32(rc, (int64_t)mc * p.ldc + n, okm, n, N, n4, v);
           }
         } else if constexpr (EPI == DFU_EPI_PATCH) {
-          // m = b*T + t  ->  row b*(T+1) + 1 + t of the fp32 token matrix
+          // m = b*T + t  ->  row b*(T+1) + 1 + t of the fp32 token matrix, + pos-embed row 1+t
           const int Tt = p.ep_tokens;
-          const int b = m / Tt, t = m - b * Tt;
-          float* C = (float*)p.C + ((int64_t)b * (Tt + 1) + 1 + t) * p.ldc + n;
-          const float* P = (const float*)p.aux + (int64_t)(1 + t) * p.ldaux + n;
-          if (full) {
-            const f32x4 pp = *(const f32x4*)P;
-            *(f32x4*)C = (f32x4){v[0] + pp[0], v[1] + pp[1], v[2] + pp[2], v[3] + pp[3]};
-          } else {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) C[r] = v[r] + P[r];
-          }
+          const int b = mc / Tt, t = mc - b * Tt;
+          float pe[4];
+          ld4_f32(ra, (int64_t)(1 + t) * p.ldaux + n, okm, n, N, n4, pe);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += pe[r];
+          st4_f32(rc, ((int64_t)b * (Tt + 1) + 1 + t) * p.ldc + n, okm, n, N, n4, v);
         }
       }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ kernel
+template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0>
+__global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
+  using T = Tile<TM, TN, OCC, NST>;
+  constexpr int WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
+  constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
+  constexpr int SCRATCH = EPI == DFU_EPI_BF16_STATS ? T::STATS_BYTES : 0;
+  // ALL LDS in one array: a second __shared__ object can make hipcc drain the DMA per K-step
+  __shared__ __attribute__((aligned(16))) char smem[T::LDS_BYTES + SCRATCH];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave / WGN, wc = wave % WGN;
+
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int units = tiles * p.split;
+  // XCD-aware bijective remap (blocks b and b+8 share an XCD): each XCD gets a contiguous
+  // range of workgroup ids, so the units one XCD has in flight (wg + i*G) are neighbours in
+  // the grouped raster below and share A and B panels in its L2.
+  const int nwg = gridDim.x;
+  int wg = blockIdx.x;
+  if (nwg >= 16) {
+    const int xcd = wg & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+  }
+  if (wg >= units) return;
+
+  // unit u -> split s = u / tiles and tile t = u % tiles in a grouped raster (GROUP_M x
+  // tiles_n bands walked column by column)
+  auto unit_geom = [&](int u, int& m0, int& n0, int& kb, int& nk) {
+    constexpr int GROUP_M = 4;
+    const int s = u / tiles, t = u - s * tiles;
+    const int band = GROUP_M * p.tiles_n;
+    const int g0 = (t / band) * GROUP_M;
+    const int gm = min(GROUP_M, p.tiles_m - g0);
+    const int within = t - (t / band) * band;
+    m0 = (g0 + within % gm) * TM;
+    n0 = (within / gm) * TN;
+    kb = s * p.kt_per_split;
+    nk = min(p.ktiles, kb + p.kt_per_split) - kb;
+  };
+  int total = 0;  // K-steps over all of this workgroup's units
+  for (int u = wg; u < units; u += nwg) {
+    const int kb = (u / tiles) * p.kt_per_split;
+    total += min(p.ktiles, kb + p.kt_per_split) - kb;
+  }
+
+  // issue cursor: the unit / K-step the next DMA stage loads
+  LoadState<T::NLDA> sa;
+  LoadState<T::NLDB> sb;
+  int iu = wg, ik = 0, im0, in0, ikb, ink;
+  unit_geom(iu, im0, in0, ikb, ink);
+  load_init<AMODE, T::NLDA>(p, sa, p.A, p.lda, im0, p.M, tid);
+  load_init<BMODE, T::NLDB>(p, sb, p.B, p.ldb, in0, p.N, tid);
+  auto issue_next = [&](char* stage) {
+    issue_tile<AMODE, T::NLDA>(p, sa, p.A, p.lda, p.m_ld_bound, ikb + ik, p.K, tid, stage);
+    issue_tile<BMODE, T::NLDB>(p, sb, p.B, p.ldb, p.n_ld_bound, ikb + ik, p.K, tid,
+                               stage + T::A_BYTES);
+    if (++ik == ink) {
+      ik = 0;
+      iu += nwg;
+      if (iu < units) {
+        unit_geom(iu, im0, in0, ikb, ink);
+        load_init<AMODE, T::NLDA>(p, sa, p.A, p.lda, im0, p.M, tid);
+        load_init<BMODE, T::NLDB>(p, sb, p.B, p.ldb, in0, p.N, tid);
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  constexpr bool AK = kcontig<AMODE>();
+  constexpr bool BKc = kcontig<BMODE>();
+  // All fragment reads of the K-step (both 32-wide halves) are issued before the first MFMA,
+  // so the LDS latency overlaps MFMAs (counted lgkmcnt waits) instead of draining per group.
+  auto compute = [&](const char* la) {
+    const char* lb = la + T::A_BYTES;
+    if constexpr (FM * FN >= 32) {
+      // 256x256: 128 accumulator registers leave room for one k-half of fragments at a time
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fa[FM], fb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = read_frag<AK>(la, wr * WTM + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      bf16x8 fa[2][FM], fb[2][FN];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[ks][i] = read_frag<AK>(la, wr * WTM + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[ks][j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][j], fa[ks][i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // Pipeline over the flattened K-step stream: step g+NSTAGE-1 is issued (into the slot step
+  // g-1 vacated) right after the barrier that publishes step g.  Before that barrier each wave
+  // waits until its share of step g's DMA has landed; younger than it are the
+  // min(NSTAGE-2, total-1-g) stages issued after it and the stores of every epilogue run since
+  // (bit k of `hist`: an epilogue ran k+1 steps ago).
+  const int E = epi_stores<EPI, T>(p);
+  float* red = (float*)(smem + T::LDS_BYTES);
+  unsigned hist = 0;
+  int cu = wg, ck = 0, cm0, cn0, ckb, cnk;
+  unit_geom(cu, cm0, cn0, ckb, cnk);
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < total) issue_next(smem + s * T::STAGE_BYTES);
+  int slot = 0;
+  for (int g = 0; g < total; ++g) {
+    const int later = min(NSTAGE - 2, total - 1 - g);
+    const int eps = __builtin_popcount(hist & ((1u << (NSTAGE - 1)) - 1u));
+    wait_vm_le<63>(T::DMA_PER_STAGE * later + E * eps);
+    __builtin_amdgcn_s_barrier();
+    if (g + NSTAGE - 1 < total) {
+      const int is = slot == 0 ? NSTAGE - 1 : slot - 1;  // (g + NSTAGE - 1) % NSTAGE
+      issue_next(smem + is * T::STAGE_BYTES);
+    }
+    compute(smem + slot * T::STAGE_BYTES);
+    slot = slot == NSTAGE - 1 ? 0 : slot + 1;
+    hist <<= 1;
+    if (++ck == cnk) {
+      epilogue<AMODE, EPI, T>(p, acc, cm0, cn0, cu / tiles, red, tid);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      hist |= 1u;
+      ck = 0;
+      cu += nwg;
+      if (cu < units) unit_geom(cu, cm0, cn0, ckb, cnk);
     }
   }
 }

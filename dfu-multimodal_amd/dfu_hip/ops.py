@@ -146,6 +146,11 @@ def gemm_plan(M, N, K, a_mode, b_mode, epilogue, split_k=0, tile=0):
     return t.value, sk.value
 
 
+def gemm_set_persistent(enable):
+    """Select the GEMM schedule (dfu_gemm_set_persistent); returns the previous setting."""
+    return int(lib().dfu_gemm_set_persistent(int(bool(enable))))
+
+
 def gemm_f32(M, N, K, A, sam, sak, B, sbn, sbk, C, ldc, bias=None, relu=False, accumulate=False):
     """Exact fp32 strided GEMM (fusion head); split-K slabs from the caching allocator."""
     need = lib().dfu_gemm_f32_workspace_bytes(int(M), int(N), int(K))

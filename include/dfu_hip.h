@@ -100,6 +100,10 @@ int dfu_gemm_stats_tiles(int32_t M);
 int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* desc);
 /* The tile (1..5, as dfu_gemm_desc.tile) and split-K the cost model picks for this descriptor. */
 int dfu_gemm_plan(const dfu_gemm_desc* desc, int32_t* tile, int32_t* split_k);
+/* GEMM schedule switch (tests, A/B timing): 1 (default) = persistent workgroups, each walking
+ * several work units as one continuous K-step stream; 0 = one workgroup per work unit.  The
+ * two give bitwise-identical results.  Returns the previous setting. */
+int dfu_gemm_set_persistent(int32_t enable);
 /* Exact fp32 GEMM for the tiny fusion head (train_multimodal_fusion.py:305-313):
  * C[m][n] = accumulate*C[m][n] + sum_k A[m*sam + k*sak] * B[n*sbn + k*sbk] (+bias[n]) (relu). */
 int dfu_gemm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t sam, int64_t sak,

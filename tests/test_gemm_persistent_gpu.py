@@ -1,0 +1,168 @@
+"""The persistent GEMM schedule against one workgroup per work unit.
+
+Under the persistent schedule (csrc/gemm_kernel.h) a workgroup walks several output tiles as
+one continuous K-step stream: the next tile's operands are in flight during the current tile's
+epilogue and the counted vmcnt waits of the K-loop count that epilogue's stores.  The tile's
+accumulation order does not change, so every output must be BITWISE equal to the one-unit-per-
+workgroup launch of the same plan.  Shapes are chosen so that each workgroup owns several units
+(more tiles than CUs x occupancy), with K as short as one K-step per tile (an epilogue every
+step: the hardest case for the wait counts), ragged M, and N with and without N % 4 == 0."""
+import math
+
+import pytest
+import torch
+
+from dfu_hip import _lib as L
+from dfu_hip import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TILES = [1, 2, 3, 4, 5]
+
+
+def drnd(*shape, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=DEV) * scale).to(dtype)
+
+
+def gemm_t(*args, tile=0, **kw):
+    try:
+        ops.gemm(*args, tile=tile, **kw)
+    except L.DfuError as e:
+        if tile and e.code == L.DFU_E_UNSUPPORTED:
+            pytest.skip(f"tile {tile} not instantiated for this combination")
+        raise
+
+
+def both_schedules(run):
+    """[outputs under the persistent schedule, outputs with one workgroup per unit]."""
+    res = []
+    for pers in (1, 0):
+        old = ops.gemm_set_persistent(pers)
+        try:
+            res.append([t.clone() for t in run()])
+        finally:
+            ops.gemm_set_persistent(old)
+    torch.cuda.synchronize()
+    return res
+
+
+def assert_bitwise(res, what):
+    for a, b in zip(*res):
+        assert torch.equal(a, b), f"{what}: persistent != one-shot " \
+            f"(max diff {(a.float() - b.float()).abs().max().item():.3e})"
+
+
+SHAPES = [(12608, 2304, 64), (12601, 200, 192), (6001, 198, 128)]
+EPIS = ["bf16", "gelu", "f32", "resid", "dgelu", "add", "stats", "acc", "acc_split", "patch"]
+
+
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("epi", EPIS)
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_persistent_bitwise(M, N, K, epi, tile):
+    n8, m8 = (N + 7) // 8 * 8, (M + 7) // 8 * 8
+    A = drnd(M, K, seed=1)
+    B = drnd(N, K, seed=2)
+    Bkn = drnd(K, n8, seed=3)
+    bias = drnd(N, dtype=torch.float32, seed=4)
+    h16 = drnd(M, N, seed=5)
+    r32 = drnd(M, N, dtype=torch.float32, seed=6)
+
+    def run():
+        if epi == "bf16":
+            C = torch.full((M, N), 7.0, dtype=torch.bfloat16, device=DEV)
+            gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16, bias=bias, tile=tile)
+            return [C]
+        if epi == "gelu":
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            pre = torch.empty_like(C)
+            gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_GELU, bias=bias, aux_out=pre,
+                   ldaux_out=N, tile=tile)
+            return [C, pre]
+        if epi == "f32":
+            C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            gemm_t(M, N, K, A, K, Bkn, n8, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32,
+                   tile=tile)
+            return [C]
+        if epi == "resid":
+            C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_F32_RESID, bias=bias, aux=r32,
+                   ldaux=N, tile=tile)
+            return [C]
+        if epi in ("dgelu", "add"):
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            gemm_t(M, N, K, A, K, Bkn, n8, C, N, b_mode=L.OPND_MNMAJOR,
+                   epilogue=L.EPI_BF16_DGELU if epi == "dgelu" else L.EPI_BF16_ADD, aux=h16,
+                   ldaux=N, tile=tile)
+            return [C]
+        if epi == "stats":
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            st = torch.full((ops.stats_tiles(M), 2, N), -1.0, device=DEV)
+            gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_STATS, stats=st, tile=tile)
+            return [C, st]
+        if epi in ("acc", "acc_split"):
+            Akm = drnd(K, m8, seed=7)
+            C = r32.clone()
+            gemm_t(M, N, K, Akm, m8, Bkn, n8, C, N, a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR,
+                   epilogue=L.EPI_F32_ACC, split_k=1 if epi == "acc" else 2, tile=tile)
+            return [C]
+        if epi == "patch":
+            T = 196
+            Bsz = M // T
+            Mp = Bsz * T
+            pos = drnd(T + 1, N, dtype=torch.float32, seed=8)
+            X = torch.zeros(Bsz, T + 1, N, dtype=torch.float32, device=DEV)
+            gemm_t(Mp, N, K, A, K, B, K, X, N, epilogue=L.EPI_PATCH, bias=bias, aux=pos, ldaux=N,
+                   ep_tokens=T, tile=tile)
+            return [X]
+        raise AssertionError(epi)
+
+    res = both_schedules(run)
+    assert_bitwise(res, f"{epi} {M}x{N}x{K} tile {tile}")
+    if epi == "bf16":  # and the common result is the product itself
+        ref = A.float() @ B.float().t() + bias
+        err = (res[0][0].float() - ref).abs()
+        assert (err <= 3e-2 + 1e-2 * ref.abs()).all(), err.max().item()
+    if epi == "acc":
+        Akm = drnd(K, m8, seed=7)
+        ref = r32 + Akm.float()[:, :M].t() @ Bkn.float()[:, :N]
+        assert (res[0][0] - ref).abs().max().item() < 3e-3 * math.sqrt(K)
+
+
+CONV = [  # N, H, W, C, K, R, S, stride, pad — ResNet-50 layers at B = 64
+    (64, 56, 56, 64, 64, 3, 3, 1, 1),
+    (64, 28, 28, 128, 128, 3, 3, 2, 1),
+    (64, 14, 14, 1024, 2048, 1, 1, 2, 0),
+]
+
+
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("case", CONV)
+def test_conv_persistent_bitwise(case, tile):
+    Nb, H, W, C, K, R, S, st, pad = case
+    g = ops.ConvGeom(Nb, H, W, C, K, R, S, st, pad)
+    x = drnd(Nb * H * W, C, seed=11)
+    w = drnd(K, R * S * C, seed=12, scale=0.1)
+    M = Nb * g.p * g.q
+    dy = drnd(M, K, seed=13)
+    base = drnd(Nb * H * W, C, seed=14)
+
+    def run():
+        y = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+        stt = torch.empty(ops.stats_tiles(M), 2, K, device=DEV)
+        if R == 1 and st == 1:
+            gemm_t(M, K, C, x, C, w, C, y, K, epilogue=L.EPI_BF16_STATS, stats=stt, tile=tile)
+        else:
+            gemm_t(M, K, R * S * C, x, 0, w, R * S * C, y, K, a_mode=L.OPND_CONV_FWD,
+                   epilogue=L.EPI_BF16_STATS, stats=stt, conv=g, tile=tile)
+        dx = torch.empty(Nb * H * W, C, dtype=torch.bfloat16, device=DEV)
+        gemm_t(Nb * H * W, C, R * S * K, dy, 0, w, R * S * C, dx, C, a_mode=L.OPND_CONV_DGRAD,
+               b_mode=L.OPND_CONV_DGRAD_W, epilogue=L.EPI_BF16_ADD, aux=base, ldaux=C, conv=g,
+               tile=tile)
+        acc = torch.zeros(K, R * S * C, device=DEV)
+        gemm_t(K, R * S * C, M, dy, K, x, 0, acc, R * S * C, a_mode=L.OPND_MNMAJOR,
+               b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC, conv=g, tile=tile)
+        return [y, stt, dx, acc]
+
+    assert_bitwise(both_schedules(run), f"conv {case} tile {tile}")

@@ -107,8 +107,10 @@ conv("l4ds 1x1 1024->2048 s2 14", 64, 14, 1024, 2048, 1, 2)
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 flt = args[0] if args else ""
 sweep = "--sweep" in sys.argv
+ab = "--ab" in sys.argv  # persistent vs one-workgroup-per-unit schedule, auto plan
 tiles = range(len(TILE_NAMES)) if sweep else [0]
-print(f"{'case':42s} " + " ".join(f"{TILE_NAMES[t]:>16s}" for t in tiles))
+print(f"{'case':42s} " + " ".join(f"{TILE_NAMES[t]:>16s}" for t in tiles) +
+      (f" {'one-shot':>16s}" for _ in [0]).__next__() * ab)
 tot_us = 0.0
 for name, flops, fn in cases:
     if flt and flt not in name:
@@ -122,6 +124,13 @@ for name, flops, fn in cases:
             continue
         if t == 0:
             tot_us += us
+        cells.append(f"{us:7.1f}us {flops / us / 1e6:6.0f}T")
+    if ab:
+        old = ops.gemm_set_persistent(0)
+        try:
+            us = timeit(lambda: fn(0))
+        finally:
+            ops.gemm_set_persistent(old)
         cells.append(f"{us:7.1f}us {flops / us / 1e6:6.0f}T")
     print(f"{name:42s} " + " ".join(cells), flush=True)
 print(f"total (auto) {tot_us:.1f} us")
