@@ -2,6 +2,7 @@
 // shape and split-K by a wave-quantisation cost model (one 512-thread workgroup per CU),
 // launches the kernel, and for split-K with a caller workspace reduces the fp32 slabs.
 #include <math.h>
+#include <stdlib.h>
 
 #include "gemm_table.h"
 
@@ -348,6 +349,10 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
           (d->aux_out == nullptr || d->ldaux_out % 4 == 0))
              ? 1
              : 0;
+  a.n8 = (a.n4 && d->N % 8 == 0 && d->ldc % 8 == 0 && ((uintptr_t)d->C & 15) == 0 &&
+          (d->aux_out == nullptr || (d->ldaux_out % 8 == 0 && ((uintptr_t)d->aux_out & 15) == 0)))
+             ? 1
+             : 0;
   a.slab = nullptr;
   if (acc_epi && splits > 1 && d->workspace != nullptr &&
       d->workspace_bytes >= (int64_t)splits * d->M * d->N * 4)
@@ -365,6 +370,8 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
     a.ph_r0 = ph->r0; a.ph_s0 = ph->s0;
     a.ph_H = d->conv_h; a.ph_W = d->conv_w; a.ph_S = d->conv_s;
   }
+  static const int dbg = getenv("DFU_GEMM_DEBUG") ? atoi(getenv("DFU_GEMM_DEBUG")) : 0;
+  a.dbg = dbg;
   a.m_ld_bound = round8(d->M);
   a.n_ld_bound = round8(d->N);
   if (d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD) {

@@ -72,6 +72,7 @@ struct GemmArgs {
   float* slab;  // split-K partial slabs [split][M][N] (F32_ACC with a workspace)
   int split;    // K-splits; work units = tiles_m * tiles_n * split
   int n4;       // N and every leading dimension % 4 == 0: one vector access per 4 columns
+  int n8;       // N, ldc (, ldaux_out) % 8 == 0 and 16-B aligned bf16 outputs: paired stores
   int ep_tokens;
   // conv geometry
   int cn, ch, cw, cc, ck, cr, cs, cstride, cpad, cp, cq;
@@ -84,6 +85,7 @@ struct GemmArgs {
   FastDiv div_pq, div_q, div_hw, div_w, div_c, div_k, div_s;
   int m_ld_bound;  // MN-contiguous operands may be read up to this column bound
   int n_ld_bound;
+  int dbg;  // timing experiments only (DFU_GEMM_DEBUG): 1 no epilogue, 2 no MFMA, 4 no DMA
 };
 
 // ------------------------------------------------------------------------------ LDS maps
@@ -409,11 +411,87 @@ DFU_DEV void ld4_bf16(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, floa
   }
 }
 
+// Sum over the 16 lanes of a DPP row (the 16 rows of one MFMA fragment column), result in every
+// lane: quad swaps, then half-row and row mirrors — four DPP adds instead of ds_bpermute
+// shuffles, pairing the lanes as xor 1, 2, 4, 8 would (the same additions, bitwise).
+template <int CTRL>
+DFU_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+DFU_DEV float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
+}
+
+// Bias of the 4 columns n0w + 16j + 4*(lane>>4) + r (j < FN) by SCALAR loads (lgkmcnt, not
+// vmcnt: a vector load here would make hipcc drain the in-flight DMA of the next tile), then a
+// per-lane select among the 16 columns of each fragment.
+template <int FN>
+DFU_DEV void load_bias(const float* bias, int n0w, int N, int lane, float (&b)[FN][4]) {
+  typedef const __attribute__((address_space(4))) float cfloat;
+  const cfloat* bp = (const cfloat*)bias;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nb = n0w + 16 * j;
+    float s[16];
+    if (nb + 16 <= N) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s[q] = bp[nb + q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s[q] = nb + q < N ? bp[nb + q] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      b[j][r] = g == 0 ? s[r] : g == 1 ? s[4 + r] : g == 2 ? s[8 + r] : s[12 + r];
+  }
+}
+
+// One 16-row block of bf16 outputs (row element offset rowe; fragment j holds columns
+// n0w + 16j + 4*(lane>>4) + r).  With n8, fragments j and j+1 are merged by one
+// v_permlane16_swap per dword so every lane stores 8 consecutive columns (16 B): lane group g
+// takes columns 16j + 16(g&1) + 8(g>>1) .. +7, the 4 lanes of a row cover 64 contiguous bytes,
+// and one dwordx4 replaces two dwordx2 (HIP guide T21, for the 16x16 accumulator layout).
+template <int FN>
+DFU_DEV void st_row_bf16(rsrc_t r, int64_t rowe, bool okm, int n0w, int N, bool n8, bool n4,
+                         int lane, const float (&v)[FN][4]) {
+  static_assert(FN % 2 == 0, "fragment pairs");
+  if (n8) {
+    const int g = lane >> 4;
+    const int cofs = ((g & 1) << 4) + ((g >> 1) << 3);
+#pragma unroll
+    for (int j = 0; j < FN; j += 2) {
+      const uint32_t a0 = pack2(v[j][0], v[j][1]), a1 = pack2(v[j][2], v[j][3]);
+      const uint32_t b0 = pack2(v[j + 1][0], v[j + 1][1]), b1 = pack2(v[j + 1][2], v[j + 1][3]);
+      const auto rx = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+      const u32x4 q = {rx[0], ry[0], rx[1], ry[1]};
+      const int col = n0w + 16 * j + cofs;
+      __builtin_amdgcn_raw_buffer_store_b128(q, r, boff(okm && col < N, (rowe + col) * 2), 0, 0);
+    }
+  } else {
+    const int lcol = 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0w + 16 * j + lcol;
+      st4_bf16(r, rowe + n, okm, n, N, n4, v[j]);
+    }
+  }
+}
+
 // Vector-memory instructions every wave issues in one epilogue AFTER its last load (its tile
 // stores); the K-loop's waits count them.  0 = not fixed (fp32 atomics: never persistent).
 template <int EPI, class T>
 DFU_DEV int epi_stores(const GemmArgs& p) {
-  const int per = T::FM * T::FN * (p.n4 ? 1 : 4);
+  constexpr bool bf16_out = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU ||
+                            EPI == DFU_EPI_BF16_GELU || EPI == DFU_EPI_BF16_DGELU ||
+                            EPI == DFU_EPI_BF16_ADD || EPI == DFU_EPI_BF16_STATS;
+  const int per = bf16_out && p.n8 ? T::FM * T::FN / 2 : T::FM * T::FN * (p.n4 ? 1 : 4);
   if constexpr (EPI == DFU_EPI_BF16_GELU) return 2 * per;
   if constexpr (EPI == DFU_EPI_F32_ACC)
     if (p.slab == nullptr && p.split > 1) return 0;
@@ -441,10 +519,7 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
     float cnt = 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i) cnt += (m0 + wr * WTM + 16 * i + lrow < M) ? 1.f : 0.f;
-    cnt += __shfl_xor(cnt, 1, 64);
-    cnt += __shfl_xor(cnt, 2, 64);
-    cnt += __shfl_xor(cnt, 4, 64);
-    cnt += __shfl_xor(cnt, 8, 64);
+    cnt = row16_sum(cnt);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
 #pragma unroll
@@ -457,10 +532,7 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
           acc[i][j][r] = v;
           s += (m < M) ? v : 0.f;
         }
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
+        s = row16_sum(s);
         const float mean = cnt > 0.f ? s / cnt : 0.f;
         float q = 0.f;
 #pragma unroll
@@ -469,10 +541,7 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
           const float d = acc[i][j][r] - mean;
           q += (m < M) ? d * d : 0.f;
         }
-        q += __shfl_xor(q, 1, 64);
-        q += __shfl_xor(q, 2, 64);
-        q += __shfl_xor(q, 4, 64);
-        q += __shfl_xor(q, 8, 64);
+        q = row16_sum(q);
         if (lrow == 0) {
           const int c = wc * WTN + 16 * j + lcol + r;
           red[(wr * TN + c) * 3 + 0] = s;
@@ -515,12 +584,12 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wr * WTM + 16 * i + lrow;
+      float v[FN][4];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wc * WTN + 16 * j + lcol;
-        const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        st4_bf16(rc, (int64_t)m * p.ldc + n, m < M, n, N, n4, v);
-      }
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[j][r] = acc[i][j][r];
+      st_row_bf16<FN>(rc, (int64_t)m * p.ldc, m < M, n0 + wc * WTN, N, p.n8, n4, lane, v);
     }
   } else {
     constexpr bool kBias = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU || EPI == DFU_EPI_F32 ||
@@ -531,14 +600,7 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
-    if (kBias && p.bias) {
-      const rsrc_t rb = make_rsrc(p.bias);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wc * WTN + 16 * j + lcol;
-        ld4_f32(rb, n, true, n, N, n4, bias[j]);
-      }
-    }
+    if (kBias && p.bias) load_bias<FN>(p.bias, n0 + wc * WTN, N, lane, bias);
     const rsrc_t ra = make_rsrc(p.aux);
     const rsrc_t ro = make_rsrc(EPI == DFU_EPI_F32_ACC ? (const void*)p.slab : p.aux_out);
 #pragma unroll
@@ -547,63 +609,76 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
       const bool okm = m < M;
       const int mc = okm ? m : 0;
       const int64_t mo = AMODE == DFU_OPND_CONV_DGRAD ? out_row(p, mc) : (int64_t)mc;
+      const int n0w = n0 + wc * WTN;
+      float v[FN][4];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wc * WTN + 16 * j + lcol;
-        float v[4];
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha + bias[j][r];
-        if constexpr (EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU) {
-          if constexpr (EPI == DFU_EPI_BF16_RELU) {
+        for (int r = 0; r < 4; ++r) v[j][r] = acc[i][j][r] * p.alpha + bias[j][r];
+      if constexpr (EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU) {
+        if constexpr (EPI == DFU_EPI_BF16_RELU) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-          }
-          st4_bf16(rc, mo * p.ldc + n, okm, n, N, n4, v);
-        } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
-          float g[4];
+          for (int j = 0; j < FN; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) g[r] = gelu_f(v[r]);
-          st4_bf16(ro, mo * p.ldaux_out + n, okm, n, N, n4, v);
-          st4_bf16(rc, mo * p.ldc + n, okm, n, N, n4, g);
-        } else if constexpr (EPI == DFU_EPI_F32) {
-          st4_f32(rc, mo * p.ldc + n, okm, n, N, n4, v);
-        } else if constexpr (EPI == DFU_EPI_F32_RESID) {
-          float x[4];
-          ld4_f32(ra, mo * p.ldaux + n, okm, n, N, n4, x);
+            for (int r = 0; r < 4; ++r) v[j][r] = fmaxf(v[j][r], 0.f);
+        }
+        st_row_bf16<FN>(rc, mo * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+      } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
+        float g[FN][4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += x[r];
-          st4_f32(rc, mo * p.ldc + n, okm, n, N, n4, v);
-        } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g[j][r] = gelu_f(v[j][r]);
+        st_row_bf16<FN>(ro, mo * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, v);
+        st_row_bf16<FN>(rc, mo * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+      } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = n0w + 16 * j + lcol;
           float x[4];
           ld4_bf16(ra, mo * p.ldaux + n, okm, n, N, n4, x);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            v[r] = (EPI == DFU_EPI_BF16_DGELU) ? v[r] * gelu_grad_f(x[r]) : v[r] + x[r];
-          st4_bf16(rc, mo * p.ldc + n, okm, n, N, n4, v);
-        } else if constexpr (EPI == DFU_EPI_F32_ACC) {
-          if (p.slab != nullptr) {
-            // split-K partial: plain store into this split's slab
-            st4_f32(ro, ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v);
-          } else if (p.split > 1) {  // fp32 atomics: launched one unit per workgroup (host)
-            float* C = (float*)p.C + (int64_t)mc * p.ldc + n;
-            for (int r = 0; r < 4; ++r)
-              if (okm && n + r < N) atomicAdd(C + r, v[r]);
-          } else {
-            float c[4];
-            ld4_f32(rc, (int64_t)mc * p.ldc + n, okm, n, N, n4, c);
+            v[j][r] = (EPI == DFU_EPI_BF16_DGELU) ? v[j][r] * gelu_grad_f(x[r]) : v[j][r] + x[r];
+        }
+        st_row_bf16<FN>(rc, mo * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+      } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += c[r];
-            st4_f32(rc, (int64_t)mc * p.ldc + n, okm, n, N, n4, v);
+        for (int j = 0; j < FN; ++j) {
+          const int n = n0w + 16 * j + lcol;
+          if constexpr (EPI == DFU_EPI_F32) {
+            st4_f32(rc, mo * p.ldc + n, okm, n, N, n4, v[j]);
+          } else if constexpr (EPI == DFU_EPI_F32_RESID) {
+            float x[4];
+            ld4_f32(ra, mo * p.ldaux + n, okm, n, N, n4, x);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][r] += x[r];
+            st4_f32(rc, mo * p.ldc + n, okm, n, N, n4, v[j]);
+          } else if constexpr (EPI == DFU_EPI_F32_ACC) {
+            if (p.slab != nullptr) {
+              // split-K partial: plain store into this split's slab
+              st4_f32(ro, ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v[j]);
+            } else if (p.split > 1) {  // fp32 atomics: launched one unit per workgroup (host)
+              float* C = (float*)p.C + (int64_t)mc * p.ldc + n;
+              for (int r = 0; r < 4; ++r)
+                if (okm && n + r < N) atomicAdd(C + r, v[j][r]);
+            } else {
+              float c[4];
+              ld4_f32(rc, (int64_t)mc * p.ldc + n, okm, n, N, n4, c);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[j][r] += c[r];
+              st4_f32(rc, (int64_t)mc * p.ldc + n, okm, n, N, n4, v[j]);
+            }
+          } else if constexpr (EPI == DFU_EPI_PATCH) {
+            // m = b*T + t -> row b*(T+1) + 1 + t of the fp32 token matrix, + pos-embed row 1+t
+            const int Tt = p.ep_tokens;
+            const int b = mc / Tt, t = mc - b * Tt;
+            float pe[4];
+            ld4_f32(ra, (int64_t)(1 + t) * p.ldaux + n, okm, n, N, n4, pe);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][r] += pe[r];
+            st4_f32(rc, ((int64_t)b * (Tt + 1) + 1 + t) * p.ldc + n, okm, n, N, n4, v[j]);
           }
-        } else if constexpr (EPI == DFU_EPI_PATCH) {
-          // m = b*T + t  ->  row b*(T+1) + 1 + t of the fp32 token matrix, + pos-embed row 1+t
-          const int Tt = p.ep_tokens;
-          const int b = mc / Tt, t = mc - b * Tt;
-          float pe[4];
-          ld4_f32(ra, (int64_t)(1 + t) * p.ldaux + n, okm, n, N, n4, pe);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += pe[r];
-          st4_f32(rc, ((int64_t)b * (Tt + 1) + 1 + t) * p.ldc + n, okm, n, N, n4, v);
         }
       }
     }
@@ -626,16 +701,22 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
 
   const int tiles = p.tiles_m * p.tiles_n;
   const int units = tiles * p.split;
-  // XCD-aware bijective remap (blocks b and b+8 share an XCD): each XCD gets a contiguous
-  // range of workgroup ids, so the units one XCD has in flight (wg + i*G) are neighbours in
-  // the grouped raster below and share A and B panels in its L2.
+  // Units by rounds: in round i workgroup b takes unit i*G + w(b).  In complete rounds w is
+  // the XCD-aware bijective remap (blocks b and b+8 share an XCD): each XCD gets a contiguous
+  // range of units, neighbours in the grouped raster below that share A and B panels in its
+  // L2.  In the last, partial round w(b) = b, so its units spread over all XCDs and CUs (the
+  // dispatcher places block b on XCD b % 8) instead of piling onto the first XCDs.
   const int nwg = gridDim.x;
-  int wg = blockIdx.x;
+  const int bid = blockIdx.x;
+  int wg = bid;
   if (nwg >= 16) {
-    const int xcd = wg & 7, q = nwg >> 3, r = nwg & 7;
-    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blockIdx.x >> 3);
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  if (wg >= units) return;
+  const int full = units / nwg;
+  const int rounds = full + (bid < units - full * nwg ? 1 : 0);
+  if (rounds == 0) return;
+  auto unit_at = [&](int i) { return i * nwg + (i < full ? wg : bid); };
 
   // unit u -> split s = u / tiles and tile t = u % tiles in a grouped raster (GROUP_M x
   // tiles_n bands walked column by column)
@@ -652,27 +733,28 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
     nk = min(p.ktiles, kb + p.kt_per_split) - kb;
   };
   int total = 0;  // K-steps over all of this workgroup's units
-  for (int u = wg; u < units; u += nwg) {
-    const int kb = (u / tiles) * p.kt_per_split;
+  for (int i = 0; i < rounds; ++i) {
+    const int kb = (unit_at(i) / tiles) * p.kt_per_split;
     total += min(p.ktiles, kb + p.kt_per_split) - kb;
   }
 
-  // issue cursor: the unit / K-step the next DMA stage loads
+  // issue cursor: the round / K-step the next DMA stage loads
   LoadState<T::NLDA> sa;
   LoadState<T::NLDB> sb;
-  int iu = wg, ik = 0, im0, in0, ikb, ink;
-  unit_geom(iu, im0, in0, ikb, ink);
+  int iu = 0, ik = 0, im0, in0, ikb, ink;
+  unit_geom(unit_at(0), im0, in0, ikb, ink);
   load_init<AMODE, T::NLDA>(p, sa, p.A, p.lda, im0, p.M, tid);
   load_init<BMODE, T::NLDB>(p, sb, p.B, p.ldb, in0, p.N, tid);
   auto issue_next = [&](char* stage) {
+    if (!(p.dbg & 4)) {
     issue_tile<AMODE, T::NLDA>(p, sa, p.A, p.lda, p.m_ld_bound, ikb + ik, p.K, tid, stage);
     issue_tile<BMODE, T::NLDB>(p, sb, p.B, p.ldb, p.n_ld_bound, ikb + ik, p.K, tid,
                                stage + T::A_BYTES);
+    }
     if (++ik == ink) {
       ik = 0;
-      iu += nwg;
-      if (iu < units) {
-        unit_geom(iu, im0, in0, ikb, ink);
+      if (++iu < rounds) {
+        unit_geom(unit_at(iu), im0, in0, ikb, ink);
         load_init<AMODE, T::NLDA>(p, sa, p.A, p.lda, im0, p.M, tid);
         load_init<BMODE, T::NLDB>(p, sb, p.B, p.ldb, in0, p.N, tid);
       }
@@ -732,10 +814,10 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
   // waits until its share of step g's DMA has landed; younger than it are the
   // min(NSTAGE-2, total-1-g) stages issued after it and the stores of every epilogue run since
   // (bit k of `hist`: an epilogue ran k+1 steps ago).
-  const int E = epi_stores<EPI, T>(p);
+  const int E = (p.dbg & 1) ? 0 : epi_stores<EPI, T>(p);
   float* red = (float*)(smem + T::LDS_BYTES);
   unsigned hist = 0;
-  int cu = wg, ck = 0, cm0, cn0, ckb, cnk;
+  int ci = 0, cu = unit_at(0), ck = 0, cm0, cn0, ckb, cnk;
   unit_geom(cu, cm0, cn0, ckb, cnk);
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
@@ -743,26 +825,31 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
   int slot = 0;
   for (int g = 0; g < total; ++g) {
     const int later = min(NSTAGE - 2, total - 1 - g);
-    const int eps = __builtin_popcount(hist & ((1u << (NSTAGE - 1)) - 1u));
-    wait_vm_le<63>(T::DMA_PER_STAGE * later + E * eps);
+    const unsigned win = hist & ((1u << (NSTAGE - 1)) - 1u);
+    if (win == 0 && later == NSTAGE - 2)  // steady state: a fixed count, no ladder
+      wait_vmcnt<T::DMA_PER_STAGE * (NSTAGE - 2)>();
+    else
+      wait_vm_le<63>(T::DMA_PER_STAGE * later + E * __builtin_popcount(win));
     __builtin_amdgcn_s_barrier();
     if (g + NSTAGE - 1 < total) {
       const int is = slot == 0 ? NSTAGE - 1 : slot - 1;  // (g + NSTAGE - 1) % NSTAGE
       issue_next(smem + is * T::STAGE_BYTES);
     }
-    compute(smem + slot * T::STAGE_BYTES);
+    if (!(p.dbg & 2)) compute(smem + slot * T::STAGE_BYTES);
     slot = slot == NSTAGE - 1 ? 0 : slot + 1;
     hist <<= 1;
     if (++ck == cnk) {
-      epilogue<AMODE, EPI, T>(p, acc, cm0, cn0, cu / tiles, red, tid);
+      if (!(p.dbg & 1)) epilogue<AMODE, EPI, T>(p, acc, cm0, cn0, cu / tiles, red, tid);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
       hist |= 1u;
       ck = 0;
-      cu += nwg;
-      if (cu < units) unit_geom(cu, cm0, cn0, ckb, cnk);
+      if (++ci < rounds) {
+        cu = unit_at(ci);
+        unit_geom(cu, cm0, cn0, ckb, cnk);
+      }
     }
   }
 }

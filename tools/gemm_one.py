@@ -22,6 +22,13 @@ def T(*s, dtype=torch.bfloat16):
 
 
 def build(case, tile):
+    if case in ("qkv_fwd", "proj_fwd", "fc2_fwd"):
+        M, N, K = {"qkv_fwd": (12608, 2304, 768), "proj_fwd": (12608, 768, 768),
+                   "fc2_fwd": (12608, 768, 3072)}[case]
+        A, B, C = T(M, K), T(N, K), T(M, N)
+        bias = T(N, dtype=torch.float32)
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16,
+                                               bias=bias, tile=tile)
     if case in ("fc1_fwd", "fc1_gelu"):
         M, N, K = 12608, 3072, 768
         A, B, C, pre = T(M, K), T(N, K), T(M, N), T(M, N)

@@ -114,6 +114,13 @@ def main():
                 f"{d0.M}x{d0.N}x{d0.K} (x{n}/step)")
         print(f"{name:62s} auto {t_auto:8.1f} us  best {best[0]:8.1f} us tile {best[1]} "
               f"split {best[2]}  {flops / best[0] / 1e6:6.0f} TFLOP/s", flush=True)
+        if not best[1]:  # the current plan won: record it too, so the table is complete
+            d = copy_desc(d0)
+            d.tile, d.split_k = 0, 0
+            tt, ss = ctypes.c_int32(), ctypes.c_int32()
+            ops.check(ops.lib().dfu_gemm_plan(ctypes.byref(d), ctypes.byref(tt), ctypes.byref(ss)),
+                      "dfu_gemm_plan")
+            best = (best[0], tt.value, ss.value if d0.epilogue == L.EPI_F32_ACC else 0)
         if best[1]:
             lines.append("    {" + ", ".join(str(v) for v in k) + f", {best[1]}, {best[2]}}},"
                          f"  // {name}: {best[0]:.1f} us (model {t_auto:.1f} us)")
