@@ -2,7 +2,7 @@
 // epilogues.  One kernel body serves every contraction of the DFU training step
 // (SURVEY.md §2.2): ViT Linear fwd/dgrad/wgrad, NHWC conv fwd/dgrad/wgrad, patch-embed.
 //
-// Geometry: 512 threads = 8 waves (2 per SIMD), one workgroup per CU, output tile TM x TN
+// Geometry: 512 threads = 8 waves (2 per SIMD) or 256 threads = 4 waves, output tile TM x TN
 // (128x128, 256x128, 128x256 or 256x256), K-step 64, v_mfma_f32_16x16x32_bf16 with fp32
 // accumulators.  Operands move global -> LDS by LDS-DMA (global_load_lds_dwordx4) into an
 // NSTAGE-deep ring (3 stages when they fit in 160 KiB, else 2), tracked by counted vmcnt and
@@ -27,19 +27,21 @@
 
 namespace dfu {
 
-constexpr int BK = 64, NT = 512, NWAVE = 8;
+constexpr int BK = 64;
 constexpr int LDS_MAX = 160 * 1024;
 
 // OCC = workgroups per CU the variant is built for (launch bounds); OCC 2 forces a 2-stage
 // ring so two workgroups' LDS fit (their prologues/epilogues overlap each other's main loop).
-template <int TM_, int TN_, int OCC_ = 1, int NST_ = 0>
+// NW = waves per workgroup: 8 (2x4 or 4x2 wave grid) or 4 (2x2: 64x64 per wave on a 128x128
+// tile, a third less LDS read traffic per MFMA than 64x32).
+template <int TM_, int TN_, int OCC_ = 1, int NST_ = 0, int NW_ = 8>
 struct Tile {
-  static constexpr int TM = TM_, TN = TN_, OCC = OCC_;
-  static constexpr int WGM = (TM == 256 && TN == 128) ? 4 : 2;  // wave grid
-  static constexpr int WGN = NWAVE / WGM;
+  static constexpr int TM = TM_, TN = TN_, OCC = OCC_, NW = NW_, NT = 64 * NW_;
+  static constexpr int WGM = NW == 4 ? 2 : (TM == 256 && TN == 128) ? 4 : 2;  // wave grid
+  static constexpr int WGN = NW / WGM;
   static constexpr int WTM = TM / WGM, WTN = TN / WGN;         // per-wave sub-tile
   static constexpr int FM = WTM / 16, FN = WTN / 16;           // MFMA accumulators per wave
-  static constexpr int NLDA = TM / 64, NLDB = TN / 64;         // DMA instructions per thread
+  static constexpr int NLDA = TM / (8 * NW), NLDB = TN / (8 * NW);  // DMA instrs per thread
   static constexpr int A_BYTES = TM * BK * 2, B_BYTES = TN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   // BF16_STATS epilogue scratch (per-wave column partials), after the ring in the same array
@@ -100,12 +102,13 @@ constexpr bool kcontig() {
 
 // ------------------------------------------------------------------------------ loaders
 // One DMA wave-instruction writes 1 KiB of LDS at a wave-uniform base, lane l at base+16*l.
-// Instruction i of wave w lands at byte 1024*(w + 8*i) of the operand tile.
-//   K-contiguous tile: that is rows 8*(w+8i) .. +7, i.e. thread row (tid>>3) + 64*i, and the
-//     lane at LDS slot (lane&7) of its row fetches chunk (lane&7) ^ (row&7) = kc_lane_chunk.
-//   MN-contiguous tile (128-column sub-images of 16 KiB): 1-KiB piece q = w + 8*i is k-rows
-//     4*(q&15) .. +3 of sub-image q>>4, i.e. k-row (tid>>4) + 32*(i&1), columns
-//     128*(i>>1) + 8*chunk with chunk = (lane&15) ^ f(k-row) (same f for every i).
+// Instruction i of wave w (of NW) lands at byte 1024*(w + NW*i) of the operand tile.
+//   K-contiguous tile: that is rows 8*(w+NW*i) .. +7, i.e. thread row (tid>>3) + 8*NW*i, and
+//     the lane at LDS slot (lane&7) of its row fetches chunk (lane&7) ^ (row&7).
+//   MN-contiguous tile (128-column sub-images of 16 KiB = 16 pieces, PPS = 16/NW pieces per
+//     wave): piece q = w + NW*(i%PPS) of sub-image i/PPS is k-rows 4q .. 4q+3, i.e. k-row
+//     (tid>>4) + 4*NW*(i%PPS), columns 128*(i/PPS) + 8*chunk with chunk = (lane&15) ^ f(k-row)
+//     (the same f for every i: f reads k-row bits 0, 1 and 3 only).
 // Out-of-range lanes fetch 16 zero bytes from g_zero16.
 __device__ __attribute__((aligned(16))) const uint32_t g_zero16[4] = {0u, 0u, 0u, 0u};
 
@@ -123,7 +126,7 @@ struct LoadState {
   int col;                 // MN-contiguous: first column (sub-image 0) of this lane's chunk
 };
 
-template <int MODE, int NLD>
+template <int MODE, int NLD, int NW>
 DFU_DEV void load_init(const GemmArgs& p, LoadState<NLD>& st, const bf16_t* base, int64_t ld,
                        int mn0, int MN, int tid) {
   const int lane = tid & 63;
@@ -135,14 +138,14 @@ DFU_DEV void load_init(const GemmArgs& p, LoadState<NLD>& st, const bf16_t* base
   if constexpr (MODE == DFU_OPND_KMAJOR) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const int row = mn0 + (tid >> 3) + 64 * i;
+      const int row = mn0 + (tid >> 3) + 8 * NW * i;
       st.valid[i] = row < MN;
       st.ptr[i] = base + (int64_t)(st.valid[i] ? row : 0) * ld + st.kc;
     }
   } else if constexpr (MODE == DFU_OPND_CONV_FWD) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {  // rows = output positions (b, oh, ow)
-      const int m = mn0 + (tid >> 3) + 64 * i;
+      const int m = mn0 + (tid >> 3) + 8 * NW * i;
       st.valid[i] = m < MN;
       const uint32_t mm = st.valid[i] ? m : 0;
       const uint32_t b = fdiv(mm, p.div_pq);
@@ -156,7 +159,7 @@ DFU_DEV void load_init(const GemmArgs& p, LoadState<NLD>& st, const bf16_t* base
   } else if constexpr (MODE == DFU_OPND_CONV_DGRAD) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {  // rows = input positions (b, h, w) of dX
-      const int m = mn0 + (tid >> 3) + 64 * i;
+      const int m = mn0 + (tid >> 3) + 8 * NW * i;
       st.valid[i] = m < MN;
       const uint32_t mm = st.valid[i] ? m : 0;
       const uint32_t b = fdiv(mm, p.div_hw);
@@ -168,7 +171,8 @@ DFU_DEV void load_init(const GemmArgs& p, LoadState<NLD>& st, const bf16_t* base
       st.bofs[i] = (int)b;
     }
   } else if constexpr (MODE == DFU_OPND_CONV_WGRAD_X) {
-    constexpr int NSUB = NLD >= 2 ? NLD / 2 : 1;
+    constexpr int PPS = 16 / NW;
+    constexpr int NSUB = NLD >= PPS ? NLD / PPS : 1;
 #pragma unroll
     for (int sub = 0; sub < NSUB; ++sub) {  // n' = (r, s, c) per sub-image
       const uint32_t n = st.col + 128 * sub;
@@ -189,9 +193,11 @@ DFU_DEV void glds16(const void* src, char* lds_dst) {
 }
 
 // Issue this thread's NLD LDS-DMA instructions for K-step kt into `tile`.
-template <int MODE, int NLD>
+template <int MODE, int NLD, int NW>
 DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_t* base,
                         int64_t ld, int MN_bound, int kt, int kend, int tid, char* tile) {
+  constexpr int PPS = 16 / NW;  // MN-contiguous pieces per wave and 128-column sub-image
+  constexpr int STEP = 1024 * NW;
   const int k0 = kt * BK;
   char* dst = tile + 1024 * (tid >> 6);
   const void* zero = (const void*)g_zero16;
@@ -200,7 +206,7 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const bool ok = st.valid[i] && kin;
-      glds16(ok ? (const void*)(st.ptr[i] + k0) : zero, dst + 8192 * i);
+      glds16(ok ? (const void*)(st.ptr[i] + k0) : zero, dst + STEP * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_FWD) {
     // whole K-step lies in one filter tap (C % 64 == 0, host-checked)
@@ -214,7 +220,7 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
       const int ih = st.i0[i] + (int)r, iw = st.i1[i] + sx;
       const bool ok = kin && st.valid[i] && (unsigned)ih < (unsigned)p.ch && (unsigned)iw < (unsigned)p.cw;
       const int64_t off = (((int64_t)st.bofs[i] * p.ch + ih) * p.cw + iw) * p.cc + c0;
-      glds16(ok ? (const void*)(base + off) : zero, dst + 8192 * i);
+      glds16(ok ? (const void*)(base + off) : zero, dst + STEP * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_DGRAD) {
     // K' = (r, s, kout); gather dY[b][(h+pad-r)/st][(w+pad-s)/st][kout]
@@ -235,15 +241,15 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
       }
       ok = ok && oh < p.cp && ow < p.cq;
       const int64_t off = (((int64_t)st.bofs[i] * p.cp + oh) * p.cq + ow) * p.ck + k_0;
-      glds16(ok ? (const void*)(base + off) : zero, dst + 8192 * i);
+      glds16(ok ? (const void*)(base + off) : zero, dst + STEP * i);
     }
   } else if constexpr (MODE == DFU_OPND_MNMAJOR) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const int k = k0 + (tid >> 4) + 32 * (i & 1);
-      const int col = st.col + 128 * (i >> 1);
+      const int k = k0 + (tid >> 4) + 4 * NW * (i % PPS);
+      const int col = st.col + 128 * (i / PPS);
       const bool ok = col < MN_bound && k < kend;
-      glds16(ok ? (const void*)(base + (int64_t)k * ld + col) : zero, dst + 8192 * i);
+      glds16(ok ? (const void*)(base + (int64_t)k * ld + col) : zero, dst + STEP * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_DGRAD_W) {
     // B[k'=(r,s,kout)][c] = Wkrsc[kout][r][s][c];  ld = R*S*C
@@ -257,18 +263,18 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
     }
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const int kout = kout0 + (tid >> 4) + 32 * (i & 1);
-      const int col = st.col + 128 * (i >> 1);
+      const int kout = kout0 + (tid >> 4) + 4 * NW * (i % PPS);
+      const int col = st.col + 128 * (i / PPS);
       const bool ok = col < MN_bound && k0 < kend;
       glds16(ok ? (const void*)(base + (int64_t)kout * ld + tap_off + col) : zero,
-             dst + 8192 * i);
+             dst + STEP * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_WGRAD_X) {
     // B[k'=m (b,oh,ow)][n'=(r,s,c)] = X[b][oh*st-pad+r][ow*st-pad+s][c]
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const int sub = i >> 1;
-      const int m = k0 + (tid >> 4) + 32 * (i & 1);
+      const int sub = i / PPS;
+      const int m = k0 + (tid >> 4) + 4 * NW * (i % PPS);
       bool ok = (st.col + 128 * sub) < MN_bound && m < kend;
       const uint32_t mm = ok ? m : 0;
       const uint32_t b = fdiv(mm, p.div_pq);
@@ -279,7 +285,7 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
       const int iw = (int)ow * p.cstride - p.cpad + st.i1[sub];
       ok = ok && (unsigned)ih < (unsigned)p.ch && (unsigned)iw < (unsigned)p.cw;
       const int64_t off = (((int64_t)b * p.ch + ih) * p.cw + iw) * p.cc + st.cin[sub];
-      glds16(ok ? (const void*)(base + off) : zero, dst + 8192 * i);
+      glds16(ok ? (const void*)(base + off) : zero, dst + STEP * i);
     }
   }
 }
@@ -555,7 +561,7 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
     // one (sum, M2) record per 128-row block: merge the row-waves that cover each block
     const rsrc_t rs = make_rsrc(p.stats);
     constexpr int HALVES = TM / 128;
-    for (int idx = tid; idx < TN * HALVES; idx += NT) {
+    for (int idx = tid; idx < TN * HALVES; idx += T::NT) {
       const int c = idx % TN, h = idx / TN;
       const int n = n0 + c;
       float S = 0.f, Q = 0.f, Cn = 0.f;
@@ -686,9 +692,9 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
 }
 
 // ------------------------------------------------------------------------------ kernel
-template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0>
-__global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
-  using T = Tile<TM, TN, OCC, NST>;
+template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0, int NW = 8>
+__global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
+  using T = Tile<TM, TN, OCC, NST, NW>;
   constexpr int WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
   constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
   constexpr int SCRATCH = EPI == DFU_EPI_BF16_STATS ? T::STATS_BYTES : 0;
@@ -743,20 +749,20 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(const GemmArgs p) {
   LoadState<T::NLDB> sb;
   int iu = 0, ik = 0, im0, in0, ikb, ink;
   unit_geom(unit_at(0), im0, in0, ikb, ink);
-  load_init<AMODE, T::NLDA>(p, sa, p.A, p.lda, im0, p.M, tid);
-  load_init<BMODE, T::NLDB>(p, sb, p.B, p.ldb, in0, p.N, tid);
+  load_init<AMODE, T::NLDA, NW>(p, sa, p.A, p.lda, im0, p.M, tid);
+  load_init<BMODE, T::NLDB, NW>(p, sb, p.B, p.ldb, in0, p.N, tid);
   auto issue_next = [&](char* stage) {
     if (!(p.dbg & 4)) {
-    issue_tile<AMODE, T::NLDA>(p, sa, p.A, p.lda, p.m_ld_bound, ikb + ik, p.K, tid, stage);
-    issue_tile<BMODE, T::NLDB>(p, sb, p.B, p.ldb, p.n_ld_bound, ikb + ik, p.K, tid,
+    issue_tile<AMODE, T::NLDA, NW>(p, sa, p.A, p.lda, p.m_ld_bound, ikb + ik, p.K, tid, stage);
+    issue_tile<BMODE, T::NLDB, NW>(p, sb, p.B, p.ldb, p.n_ld_bound, ikb + ik, p.K, tid,
                                stage + T::A_BYTES);
     }
     if (++ik == ink) {
       ik = 0;
       if (++iu < rounds) {
         unit_geom(unit_at(iu), im0, in0, ikb, ink);
-        load_init<AMODE, T::NLDA>(p, sa, p.A, p.lda, im0, p.M, tid);
-        load_init<BMODE, T::NLDB>(p, sb, p.B, p.ldb, in0, p.N, tid);
+        load_init<AMODE, T::NLDA, NW>(p, sa, p.A, p.lda, im0, p.M, tid);
+        load_init<BMODE, T::NLDB, NW>(p, sb, p.B, p.ldb, in0, p.N, tid);
       }
     }
   };

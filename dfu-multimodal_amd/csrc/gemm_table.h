@@ -8,8 +8,12 @@ struct Entry {
   int a, b, e, tile;
   gemm_fn fn;
   int lds_bytes;
+  int threads;
 };
-enum TileId { T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, T128x128o2 = 4, NTILES = 5 };
+enum TileId {
+  T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, T128x128o2 = 4, T128x128w4 = 5,
+  NTILES = 6
+};
 extern const Entry kTable128x128[];
 extern const int kTable128x128N;
 extern const Entry kTable256x128[];
@@ -20,17 +24,28 @@ extern const Entry kTable256x256[];
 extern const int kTable256x256N;
 extern const Entry kTable128x128o2[];
 extern const int kTable128x128o2N;
+extern const Entry kTable128x128w4[];
+extern const int kTable128x128w4N;
 }  // namespace dfu
 
-#define DFU_ENTRY(A, B, E, TMv, TNv, TID) \
-  { A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv>, dfu::Tile<TMv, TNv>::LDS_BYTES }
+#define DFU_ENTRY(A, B, E, TMv, TNv, TID)                                             \
+  {                                                                                   \
+    A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv>, dfu::Tile<TMv, TNv>::LDS_BYTES, \
+        dfu::Tile<TMv, TNv>::NT                                                       \
+  }
 #define DFU_ENTRY_OCC(A, B, E, TMv, TNv, OCCv, TID)                       \
   {                                                                       \
     A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv, OCCv>,             \
-        dfu::Tile<TMv, TNv, OCCv>::LDS_BYTES                              \
+        dfu::Tile<TMv, TNv, OCCv>::LDS_BYTES, dfu::Tile<TMv, TNv, OCCv>::NT   \
   }
 #define DFU_ENTRY_NST(A, B, E, TMv, TNv, NSTv, TID)                       \
   {                                                                       \
     A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv, 1, NSTv>,          \
-        dfu::Tile<TMv, TNv, 1, NSTv>::LDS_BYTES                           \
+        dfu::Tile<TMv, TNv, 1, NSTv>::LDS_BYTES, dfu::Tile<TMv, TNv, 1, NSTv>::NT \
+  }
+// 4-wave workgroups (2x2 waves of 64x64), OCCv per CU
+#define DFU_ENTRY_W4(A, B, E, TMv, TNv, OCCv, TID)                              \
+  {                                                                             \
+    A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv, OCCv, 0, 4>,             \
+        dfu::Tile<TMv, TNv, OCCv, 0, 4>::LDS_BYTES, dfu::Tile<TMv, TNv, OCCv, 0, 4>::NT \
   }
