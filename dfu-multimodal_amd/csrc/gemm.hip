@@ -28,7 +28,8 @@ constexpr double kReduceLaunchUs = 2.0;
 // Persistent schedule (gemm_kernel.h): a workgroup owning several work units pays one
 // prologue fill for all of them plus, per unit, the epilogue time its MFMAs do not hide.
 constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2};
-int g_persistent = 1;  // dfu_gemm_set_persistent
+int g_persistent = 1;       // dfu_gemm_set_persistent
+int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
@@ -181,6 +182,12 @@ extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* spl
 extern "C" int dfu_gemm_set_persistent(int32_t enable) {
   const int old = g_persistent;
   g_persistent = enable != 0;
+  return old;
+}
+
+extern "C" int dfu_gemm_set_inkernel_reduce(int32_t enable) {
+  const int old = g_inkernel_reduce;
+  g_inkernel_reduce = enable != 0;
   return old;
 }
 
@@ -357,6 +364,11 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   if (acc_epi && splits > 1 && d->workspace != nullptr &&
       d->workspace_bytes >= (int64_t)splits * d->M * d->N * 4)
     a.slab = (float*)d->workspace;
+  // in-kernel split-K reduction: the last split of a tile to finish adds the slabs into C
+  a.counters = nullptr;
+  if (a.slab != nullptr && g_inkernel_reduce && splits <= 8 && d->tile_counters != nullptr &&
+      d->tile_counters_len >= a.tiles_m * a.tiles_n)
+    a.counters = d->tile_counters;
   a.ep_tokens = d->ep_tokens;
   a.cn = d->conv_n; a.ch = d->conv_h; a.cw = d->conv_w; a.cc = d->conv_c;
   a.ck = d->conv_k; a.cr = d->conv_r; a.cs = d->conv_s;
@@ -403,7 +415,7 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   const int nwg = (g_persistent && !atomics && units > slots) ? slots : units;
   hipLaunchKernelGGL(pl.entry->fn, dim3(nwg), dim3(pl.entry->threads), 0, s, a);
   DFU_LAUNCH_CHECK();
-  if (a.slab != nullptr) {
+  if (a.slab != nullptr && a.counters == nullptr) {
     const int64_t n = (int64_t)d->M * d->N;
     const bool vec = d->N % 4 == 0 && d->ldc % 4 == 0 && ((uintptr_t)d->C & 15) == 0;
     int64_t blocks = (vec ? n / 4 : n) / 256 + 1;

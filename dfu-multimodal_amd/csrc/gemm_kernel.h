@@ -72,6 +72,7 @@ struct GemmArgs {
   int64_t ldaux_out;
   float* stats;
   float* slab;  // split-K partial slabs [split][M][N] (F32_ACC with a workspace)
+  int* counters;  // per-tile arrival counters: in-kernel slab reduction (zero in, zero out)
   int split;    // K-splits; work units = tiles_m * tiles_n * split
   int n4;       // N and every leading dimension % 4 == 0: one vector access per 4 columns
   int n8;       // N, ldc (, ldaux_out) % 8 == 0 and 16-B aligned bf16 outputs: paired stores
@@ -367,16 +368,19 @@ DFU_DEV int boff(bool ok, int64_t byte_off) { return (int)(ok ? (uint32_t)byte_o
 
 // Four consecutive columns n..n+3 at element index e of a row-major fp32 / bf16 matrix; okr =
 // row in range.  n4 (launch-uniform): one vector access, else four scalar accesses.
+// AUX = cache-policy bits of the buffer instruction (16 = sc1: write-through stores / loads
+// that bypass non-coherent caches, for data handed between workgroups; HIP guide G16 R1).
+template <int AUX = 0>
 DFU_DEV void st4_f32(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, const float* v) {
   if (n4) {
     const u32x4 x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                      __float_as_uint(v[3])};
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, boff(okr && n < N, e * 4), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, boff(okr && n < N, e * 4), 0, AUX);
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), r,
-                                            boff(okr && n + q < N, (e + q) * 4), 0, 0);
+                                            boff(okr && n + q < N, (e + q) * 4), 0, AUX);
   }
 }
 DFU_DEV void st4_bf16(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, const float* v) {
@@ -390,16 +394,17 @@ DFU_DEV void st4_bf16(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, cons
                                             0, 0);
   }
 }
+template <int AUX = 0>
 DFU_DEV void ld4_f32(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, float* v) {
   if (n4) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, boff(okr && n < N, e * 4), 0, 0);
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, boff(okr && n < N, e * 4), 0, AUX);
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = __uint_as_float(x[q]);
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       v[q] = __uint_as_float(
-          __builtin_amdgcn_raw_buffer_load_b32(r, boff(okr && n + q < N, (e + q) * 4), 0, 0));
+          __builtin_amdgcn_raw_buffer_load_b32(r, boff(okr && n + q < N, (e + q) * 4), 0, AUX));
   }
 }
 DFU_DEV void ld4_bf16(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, float* v) {
@@ -500,8 +505,76 @@ DFU_DEV int epi_stores(const GemmArgs& p) {
   const int per = bf16_out && p.n8 ? T::FM * T::FN / 2 : T::FM * T::FN * (p.n4 ? 1 : 4);
   if constexpr (EPI == DFU_EPI_BF16_GELU) return 2 * per;
   if constexpr (EPI == DFU_EPI_F32_ACC)
-    if (p.slab == nullptr && p.split > 1) return 0;
+    if ((p.slab == nullptr && p.split > 1) || p.counters != nullptr) return 0;
   return per;
+}
+
+// C += slab 0 + ... + slab S-1 over this workgroup's tile (the last split to arrive).
+template <class T, int S>
+DFU_DEV void splitk_sum(const GemmArgs& p, int m0, int n0, int tid) {
+  constexpr int FM = T::FM, FN = T::FN, WTM = T::WTM, WTN = T::WTN;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / T::WGN, wc = wave % T::WGN;
+  const int lrow = lane & 15, lcol = 4 * (lane >> 4);
+  const int M = p.M, N = p.N;
+  const bool n4 = p.n4 != 0;
+  const rsrc_t rs = make_rsrc(p.slab);
+  const rsrc_t rc = make_rsrc(p.C);
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wr * WTM + 16 * i + lrow;
+    const bool okm = m < M;
+    const int mc = okm ? m : 0;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wc * WTN + 16 * j + lcol;
+      float x[S][4], c[4];
+#pragma unroll
+      for (int k = 0; k < S; ++k) ld4_f32<16>(rs, ((int64_t)k * M + mc) * N + n, okm, n, N, n4, x[k]);
+      ld4_f32(rc, (int64_t)mc * p.ldc + n, okm, n, N, n4, c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sum = x[0][r];
+#pragma unroll
+        for (int k = 1; k < S; ++k) sum += x[k][r];
+        c[r] += sum;
+      }
+      st4_f32(rc, (int64_t)mc * p.ldc + n, okm, n, N, n4, c);
+    }
+  }
+}
+
+// In-kernel split-K reduction (after this split's slab tile is stored, write-through): count the
+// tile's arrivals; the last split to arrive adds slab 0 + ... + slab S-1 (that order, as the
+// separate reduce kernel) into C and resets the counter.  No workgroup ever waits for another
+// (the publish is: own stores drained -> barrier -> one agent-scope atomic), so it is correct
+// for any placement of the splits over XCDs and CUs (HIP guide G16 R1: sc1 stores and loads).
+template <class T>
+DFU_DEV void splitk_finish(const GemmArgs& p, int m0, int n0, float* red, int tid) {
+  const int t = (m0 / T::TM) * p.tiles_n + n0 / T::TN;
+  int* flag = (int*)red;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.counters + t, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == p.split - 1;
+    if (last) __hip_atomic_store(p.counters + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int last = *flag;
+  if (!last) return;
+  switch (p.split) {  // compile-time split counts: every slab load of the tile issued up front
+    case 2: splitk_sum<T, 2>(p, m0, n0, tid); break;
+    case 3: splitk_sum<T, 3>(p, m0, n0, tid); break;
+    case 4: splitk_sum<T, 4>(p, m0, n0, tid); break;
+    case 5: splitk_sum<T, 5>(p, m0, n0, tid); break;
+    case 6: splitk_sum<T, 6>(p, m0, n0, tid); break;
+    case 7: splitk_sum<T, 7>(p, m0, n0, tid); break;
+    default: splitk_sum<T, 8>(p, m0, n0, tid); break;
+  }
 }
 
 // ------------------------------------------------------------------------------ epilogue
@@ -662,8 +735,11 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
             st4_f32(rc, mo * p.ldc + n, okm, n, N, n4, v[j]);
           } else if constexpr (EPI == DFU_EPI_F32_ACC) {
             if (p.slab != nullptr) {
-              // split-K partial: plain store into this split's slab
-              st4_f32(ro, ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v[j]);
+              // split-K partial into this split's slab (write-through when reduced in-kernel)
+              if (p.counters != nullptr)
+                st4_f32<16>(ro, ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v[j]);
+              else
+                st4_f32(ro, ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v[j]);
             } else if (p.split > 1) {  // fp32 atomics: launched one unit per workgroup (host)
               float* C = (float*)p.C + (int64_t)mc * p.ldc + n;
               for (int r = 0; r < 4; ++r)
@@ -688,6 +764,9 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
         }
       }
     }
+    if constexpr (EPI == DFU_EPI_F32_ACC) {
+      if (p.slab != nullptr && p.counters != nullptr) splitk_finish<T>(p, m0, n0, red, tid);
+    }
   }
 }
 
@@ -697,7 +776,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   using T = Tile<TM, TN, OCC, NST, NW>;
   constexpr int WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
   constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
-  constexpr int SCRATCH = EPI == DFU_EPI_BF16_STATS ? T::STATS_BYTES : 0;
+  constexpr int SCRATCH =
+      EPI == DFU_EPI_BF16_STATS ? T::STATS_BYTES : EPI == DFU_EPI_F32_ACC ? 16 : 0;
   // ALL LDS in one array: a second __shared__ object can make hipcc drain the DMA per K-step
   __shared__ __attribute__((aligned(16))) char smem[T::LDS_BYTES + SCRATCH];
   const int tid = threadIdx.x;

@@ -49,6 +49,7 @@ class GemmDesc(ctypes.Structure):
         ("conv_p", c_int32), ("conv_q", c_int32),
         ("tile", c_int32),
         ("workspace", c_void_p), ("workspace_bytes", c_int64),
+        ("tile_counters", c_void_p), ("tile_counters_len", c_int32),
     ]
 
 
@@ -67,6 +68,7 @@ PROTOTYPES = {
     "dfu_gemm_workspace_bytes": [ctypes.POINTER(GemmDesc)],
     "dfu_gemm_plan": [ctypes.POINTER(GemmDesc), ctypes.POINTER(c_int32), ctypes.POINTER(c_int32)],
     "dfu_gemm_set_persistent": [I32],
+    "dfu_gemm_set_inkernel_reduce": [I32],
     "dfu_gemm_f32": [I32, I32, I32, P, I64, I64, P, I64, I64, P, I64, P, I32, I32, P, I64, P],
     "dfu_gemm_f32_workspace_bytes": [I32, I32, I32],
     "dfu_pack_conv_weight": [P, P, I32, I32, I32, I32, P],

@@ -116,6 +116,8 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
                 workspace = torch.empty(need, dtype=torch.uint8, device=C.device)
             d.workspace = workspace.data_ptr()
             d.workspace_bytes = int(need)
+            cnt = tile_counters(C.device)
+            d.tile_counters, d.tile_counters_len = cnt.data_ptr(), cnt.numel()
     check(lib().dfu_gemm(ctypes.byref(d), stream_ptr()), "dfu_gemm")
     if gemm_record is not None:
         flops = 2.0 * M * N * K
@@ -123,6 +125,26 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
             flops /= conv.stride * conv.stride  # algorithmic: only the 1/stride^2 live taps
         gemm_record.append((d, flops, _algorithmic_bytes(d, conv),
                             (A, B, C, bias, aux, aux_out, stats, workspace)))
+
+
+_COUNTERS = {}
+TILE_COUNTERS = 1 << 16
+
+
+def tile_counters(device):
+    """Per-stream zeroed int32 tile counters for the in-kernel split-K reduction (every launch
+    returns them zeroed; launches on one stream never overlap)."""
+    st = torch.cuda.current_stream(device)
+    key = (st.device_index, st.cuda_stream)
+    t = _COUNTERS.get(key)
+    if t is None:
+        t = _COUNTERS[key] = torch.zeros(TILE_COUNTERS, dtype=torch.int32, device=device)
+    return t
+
+
+def gemm_set_inkernel_reduce(enable):
+    """Split-K reduction inside the GEMM (1) or by the separate reduce kernel (0)."""
+    return int(lib().dfu_gemm_set_inkernel_reduce(int(bool(enable))))
 
 
 def _plan_desc(M, N, K, a_mode, b_mode, epilogue, split_k, tile):

@@ -91,6 +91,12 @@ typedef struct dfu_gemm_desc {
                           128x128 at 2 workgroups/CU (8 waves, 4 waves)      */
   void* workspace;     /* split-K fp32 slabs (dfu_gemm_workspace_bytes); NULL =  */
   int64_t workspace_bytes; /*   split-K partials accumulate with fp32 atomics     */
+  /* Split-K with slabs: NULL = a second kernel adds the slabs into C.  Otherwise a zeroed
+   * int32[tile_counters_len] the launch returns zeroed: the last of a tile's splits to finish
+   * adds all its slabs into C inside the GEMM (same order, bitwise the same result).  One
+   * buffer per stream (launches on one stream never overlap). */
+  int32_t* tile_counters;
+  int32_t tile_counters_len;
 } dfu_gemm_desc;
 
 int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
@@ -104,6 +110,10 @@ int dfu_gemm_plan(const dfu_gemm_desc* desc, int32_t* tile, int32_t* split_k);
  * several work units as one continuous K-step stream; 0 = one workgroup per work unit.  The
  * two give bitwise-identical results.  Returns the previous setting. */
 int dfu_gemm_set_persistent(int32_t enable);
+/* Split-K reduction switch: 1 = inside the GEMM when the descriptor carries tile
+ * counters, 0 (default: measured faster) = the separate reduce kernel.  Bitwise-identical; returns the
+ * previous setting. */
+int dfu_gemm_set_inkernel_reduce(int32_t enable);
 /* Exact fp32 GEMM for the tiny fusion head (train_multimodal_fusion.py:305-313):
  * C[m][n] = accumulate*C[m][n] + sum_k A[m*sam + k*sak] * B[n*sbn + k*sbk] (+bias[n]) (relu). */
 int dfu_gemm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t sam, int64_t sak,

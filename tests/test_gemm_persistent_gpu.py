@@ -166,3 +166,35 @@ def test_conv_persistent_bitwise(case, tile):
         return [y, stt, dx, acc]
 
     assert_bitwise(both_schedules(run), f"conv {case} tile {tile}")
+
+
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("M,N,K,split", [(768, 3072, 12608, 3), (2304, 768, 12608, 4),
+                                         (64, 147, 802816 // 16, 0), (300, 200, 4000, 7)])
+def test_gemm_splitk_inkernel_bitwise(M, N, K, split, tile):
+    """Split-K slabs reduced by the last-arriving split inside the GEMM (tile counters) equal the
+    separate reduce kernel bitwise (same summation order), under both schedules; the counters
+    come back zeroed (graph replays and the next launch rely on it)."""
+    m8, n8 = (M + 7) // 8 * 8, (N + 7) // 8 * 8
+    Akm = drnd(K, m8, seed=21)
+    Bkn = drnd(K, n8, seed=22)
+    C0 = drnd(M, N, dtype=torch.float32, seed=23)
+    res = []
+    for ink in (1, 0):
+        old = ops.gemm_set_inkernel_reduce(ink)
+        try:
+            C = C0.clone()
+            gemm_t(M, N, K, Akm, m8, Bkn, n8, C, N, a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR,
+                   epilogue=L.EPI_F32_ACC, split_k=split, tile=tile)
+            C2 = C0.clone()  # twice: counters must have been left zeroed
+            gemm_t(M, N, K, Akm, m8, Bkn, n8, C2, N, a_mode=L.OPND_MNMAJOR,
+                   b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC, split_k=split, tile=tile)
+            res.append((C, C2))
+        finally:
+            ops.gemm_set_inkernel_reduce(old)
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert torch.equal(res[0][0], res[0][1])
+    assert int(ops.tile_counters(C0.device).abs().sum().item()) == 0
+    ref = C0 + Akm.float()[:, :M].t() @ Bkn.float()[:, :N]
+    assert (res[0][0] - ref).abs().max().item() < 3e-3 * math.sqrt(K)
