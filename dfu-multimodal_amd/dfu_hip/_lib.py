@@ -77,6 +77,10 @@ PROTOTYPES = {
     "dfu_cast_rows_f32": [P, I64, P, I64, I32, I32, P],
     "dfu_im2col_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],
     "dfu_patchify_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
+    "dfu_col2im_f32": [P, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P],
+    "dfu_unpatchify_f32": [P, I32, I32, I32, I32, I32, P, P],
+    "dfu_gradcam": [P, I32, I64, I64, I64, P, I32, I64, I64, I64, I32, I32, I32, P, P],
+    "dfu_saliency": [P, I32, I32, I32, P, P],
     "dfu_bn_finalize": [P, I32, I32, I32, P, P, F, F, P, P, P, P, P, P, P, P],
     "dfu_bn_eval_coeffs": [P, P, P, P, F, I32, P, P, P],
     "dfu_bn_apply": [P, P, P, P, I32, P, I64, I32, P],

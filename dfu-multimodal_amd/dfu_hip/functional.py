@@ -291,25 +291,24 @@ class StemFn(torch.autograd.Function):
             grads_done(w)
         dx = None
         if ctx.x_requires_grad:
-            # Grad-CAM path (grad_cam_visualization.py:374): dcol = dy W, then col2im.
+            # Grad-CAM path (grad_cam_visualization.py:374): fp32 dcol = dy W (MFMA GEMM),
+            # then its col2im adjoint (a gather kernel) -> fp32 NCHW input gradient.
             wkn = wb  # [Cout][Kp] viewed as B[k=cout][n=kp]
-            dcol = _empty((M, Kp), BF16, y.device)
+            dcol = _empty((M, Kp), F32, y.device)
             ops.gemm(M, Kp, Cout, dy, Cout, wkn, Kp, dcol, Kp, b_mode=L.OPND_MNMAJOR,
-                     epilogue=L.EPI_BF16)
-            dx = col2im_f32(dcol, B, C, H, W, R, S, st, pad, P, Q, Kp)
+                     epilogue=L.EPI_F32)
+            dx = ops.col2im_f32(dcol, B, C, H, W, R, S, st, pad, P, Q, Kp)
         return dx, None, None, None, None
 
 
-def col2im_f32(dcol, B, C, H, W, R, S, st, pad, P, Q, Kp):
-    """Adjoint of dfu_im2col_f32 (used only for input gradients, Grad-CAM)."""
-    # Expressed with the patch GEMM identity: input gradient of the explicit im2col is the sum
-    # of the column entries that read each pixel; done with F.fold over fp32 columns.
-    import torch.nn.functional as F
-    cols = dcol[:, :C * R * S].float().view(B, P * Q, C * R * S).transpose(1, 2)
-    return F.fold(cols, (H, W), (R, S), padding=pad, stride=st)
-
-
 # ---------------------------------------------------------------------------- Bottleneck
+def _fire_grad_hooks(probe, grad):
+    """Call the gradient hooks registered (Tensor.register_hook) on a probe leaf with the
+    gradient the fused backward computed for the tensor it stands for."""
+    for hook in list((probe._backward_hooks or {}).values()):
+        hook(grad)
+
+
 class BottleneckFn(torch.autograd.Function):
     """torchvision Bottleneck: relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1 x))))))) + id)."""
 
@@ -357,6 +356,14 @@ class BottleneckFn(torch.autograd.Function):
         ctx.bns = (s1, s2, s3, sd)
         ctx.shape = (B, Cin, H, W)
         ctx.x_requires_grad = ctx.needs_input_grad[0]
+        ctx.probes = None
+        if getattr(mod, "_probe", False):
+            # Hooked `relu` (Grad-CAM): torchvision calls it after bn1 and bn2 as well, so hand
+            # the block the two inner ReLU outputs as leaf tensors whose gradient hooks
+            # backward fires with da2 / da1 (models/resnet.py Bottleneck.forward).
+            ctx.probes = (from_rows(a1, B, g1.p, g1.q, planes).detach().requires_grad_(True),
+                          from_rows(a2, B, g2.p, g2.q, planes).detach().requires_grad_(True))
+            mod._probes = ctx.probes
         ctx.save_for_backward(xr, y1, a1, y2, a2, y3, out, w1, w2, w3,
                               *( (yd, wd) if yd is not None else ()))
         return from_rows(out, B, g3.p, g3.q, outc)
@@ -389,6 +396,8 @@ class BottleneckFn(torch.autograd.Function):
         # conv3
         da2 = torch.empty_like(a2)
         conv_dgrad(dy3, g3, w3, da2)
+        if ctx.probes is not None:
+            _fire_grad_hooks(ctx.probes[1], from_rows(da2, B, g2.p, g2.q, g2.k))
         if _wants(mod.conv3.weight):
             conv_wgrad(dy3, a2, g3, grad_buffer(mod.conv3.weight))
             grads_done(mod.conv3.weight)
@@ -397,6 +406,8 @@ class BottleneckFn(torch.autograd.Function):
         s2.backward(da2, y2, a2, True, dy2, None)
         da1 = torch.empty_like(a1)
         conv_dgrad(dy2, g2, w2, da1)
+        if ctx.probes is not None:
+            _fire_grad_hooks(ctx.probes[0], from_rows(da1, B, g1.p, g1.q, g1.k))
         if _wants(mod.conv2.weight):
             conv_wgrad(dy2, a1, g2, grad_buffer(mod.conv2.weight))
             grads_done(mod.conv2.weight)
@@ -458,15 +469,16 @@ class PatchEmbedFn(torch.autograd.Function):
                  ldaux=D, ep_tokens=T)
         ops.vit_cls_rows(cls.detach().reshape(D), pos.detach().reshape(T + 1, D), X, B, T + 1, D)
         ctx.params = (w, b, cls, pos)
-        ctx.dims = (B, T, D, K)
-        ctx.save_for_backward(patches)
+        ctx.dims = (B, T, D, K, C, H, W, ps)
+        ctx.x_requires_grad = ctx.needs_input_grad[0]
+        ctx.save_for_backward(patches, wb)
         return X
 
     @staticmethod
     def backward(ctx, gX):
-        (patches,) = ctx.saved_tensors
+        patches, wb = ctx.saved_tensors
         w, b, cls, pos = ctx.params
-        B, T, D, K = ctx.dims
+        B, T, D, K, C, H, W, ps = ctx.dims
         gX = gX.contiguous()
         gpatch = ops.vit_embed_bwd(gX, B, T + 1, D,
                                    grad_buffer(cls) if _wants(cls) else None,
@@ -477,7 +489,15 @@ class PatchEmbedFn(torch.autograd.Function):
             ops.gemm(D, K, B * T, gpatch, D, patches, K, dw, K, a_mode=L.OPND_MNMAJOR,
                      b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
         grads_done(w, b, cls, pos)
-        return None, None, None, None, None, None
+        dx = None
+        if ctx.x_requires_grad:
+            # Grad-CAM input saliency (grad_cam_visualization.py:374, 401-413): fp32
+            # d patches = gpatch W (MFMA GEMM), then the unpatchify permutation.
+            dpatch = _empty((B * T, K), F32, gX.device)
+            ops.gemm(B * T, K, D, gpatch, D, wb, K, dpatch, K, b_mode=L.OPND_MNMAJOR,
+                     epilogue=L.EPI_F32)
+            dx = ops.unpatchify_f32(dpatch, B, C, H, W, ps)
+        return dx, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------- ViT block

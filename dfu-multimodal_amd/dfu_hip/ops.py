@@ -252,6 +252,58 @@ def patchify_f32(x, ps):
     return out
 
 
+# ------------------------------------------------------------------------------ Grad-CAM
+def col2im_f32(dcol, B, C, H, W, R, S, stride, pad, P, Q, Kp):
+    """Adjoint of im2col_f32: fp32 [B*P*Q][Kp] column gradients -> fp32 NCHW input gradient."""
+    _req(dcol, F32, "col2im_f32")
+    dx = torch.empty((B, C, H, W), dtype=F32, device=dcol.device)
+    check(lib().dfu_col2im_f32(ptr(dcol), B, C, H, W, R, S, stride, pad, P, Q, Kp, ptr(dx),
+                               stream_ptr()), "dfu_col2im_f32")
+    return dx
+
+
+def unpatchify_f32(dpatch, B, C, H, W, ps):
+    """Adjoint of patchify_f32: fp32 [B*(H/ps)*(W/ps)][C*ps*ps] -> fp32 NCHW."""
+    _req(dpatch, F32, "unpatchify_f32")
+    dx = torch.empty((B, C, H, W), dtype=F32, device=dpatch.device)
+    check(lib().dfu_unpatchify_f32(ptr(dpatch), B, C, H, W, ps, ptr(dx), stream_ptr()),
+          "dfu_unpatchify_f32")
+    return dx
+
+
+def gradcam(act, grad):
+    """Grad-CAM maps (B, h, w) fp32 from a hooked activation (B, Ca, h, w) and a gradient
+    (B, Cg, h, w): weights from the Cg gradient channels, the map over the first min(Ca, Cg)
+    activation channels (grad_cam_visualization.py:415-429).  NCHW or channels_last views."""
+    if act.dtype not in (BF16, F32) or not act.is_cuda or not grad.is_cuda:
+        raise TypeError("gradcam: bf16/fp32 CUDA tensors expected")
+    grad = grad.to(act.dtype)
+    B, Ca, h, w = act.shape
+    Bg, Cg, hg, wg = grad.shape
+    if (B, h, w) != (Bg, hg, wg):
+        raise ValueError(f"gradcam: activation {tuple(act.shape)} vs gradient {tuple(grad.shape)}")
+    views = []
+    for t in (act, grad):
+        if t.stride(2) != w * t.stride(3):  # the spatial dims must be one dense position axis
+            t = t.contiguous(memory_format=torch.channels_last)
+        views.append((t, t.stride(0), t.stride(3), t.stride(1)))
+    (a, sab, sap, sac), (g, sgb, sgp, sgc) = views
+    cam = torch.empty((B, h, w), dtype=F32, device=act.device)
+    check(lib().dfu_gradcam(ptr(a), Ca, sab, sap, sac, ptr(g), Cg, sgb, sgp, sgc,
+                            int(a.dtype == BF16), B, h * w, ptr(cam), stream_ptr()), "dfu_gradcam")
+    return cam
+
+
+def saliency(dx):
+    """mean_c |dx| per pixel, normalised by its per-image max: (B, H, W) fp32."""
+    _req(dx, F32, "saliency")
+    dx = dx.contiguous()
+    B, C, H, W = dx.shape
+    out = torch.empty((B, H, W), dtype=F32, device=dx.device)
+    check(lib().dfu_saliency(ptr(dx), B, C, H * W, ptr(out), stream_ptr()), "dfu_saliency")
+    return out
+
+
 # ----------------------------------------------------------------------------- BatchNorm
 def bn_finalize(stats, M, C, gamma, beta, eps, momentum, running_mean, running_var, nbt,
                 mean_out, invstd_out, scale_out, shift_out):

@@ -48,11 +48,20 @@ class Bottleneck(tnn.Module):
         return ps
 
     def forward(self, x):
+        hooked = bool(self.relu._forward_hooks or self.relu._forward_pre_hooks)
+        self._probe = hooked and torch.is_grad_enabled()
         out = Fn.BottleneckFn.apply(x, *self._params(), self)
-        # The block output already is relu(...): calling the (idempotent) ReLU module again
-        # is exact and only happens when someone hooks it (Grad-CAM target 'layer4.2.relu',
-        # grad_cam_visualization.py:355-357, 389-392).
-        if self.relu._forward_hooks or self.relu._forward_pre_hooks:
+        if hooked:
+            # Someone hooks `relu` (Grad-CAM target 'layer4.2.relu',
+            # grad_cam_visualization.py:355-357, 389-392).  torchvision calls it three times per
+            # block — after bn1, after bn2, after the residual add — and the reference's CAM
+            # depends on that (its stored gradient is the first call's, its activation the
+            # last's).  Replay the two inner calls to the forward hooks with probe leaves that
+            # BottleneckFn.backward feeds their gradients to, then call the module on the
+            # block output (already relu(...), so the idempotent ReLU is exact).
+            for probe in self.__dict__.pop("_probes", ()):
+                for hook in list(self.relu._forward_hooks.values()):
+                    hook(self.relu, (probe,), probe)
             out = self.relu(out)
         return out
 

@@ -149,6 +149,28 @@ int dfu_im2col_f32(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t s
 int dfu_patchify_f32(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
                      int32_t C, int32_t H, int32_t W, int32_t ps, void* out, void* stream);
 
+/* ---------------------------------------------------------------- Grad-CAM (C5) ----- */
+/* Input gradients of the two stems, which Grad-CAM needs (grad_cam_visualization.py:374-386:
+ * the input requires grad) and the training step does not.
+ * col2im: adjoint of dfu_im2col_f32 (resnet conv1): fp32 dcol [B*P*Q][Kp] -> fp32 NCHW dx. */
+int dfu_col2im_f32(const float* dcol, int32_t B, int32_t C, int32_t H, int32_t W, int32_t R,
+                   int32_t S, int32_t stride, int32_t pad, int32_t P, int32_t Q, int32_t Kp,
+                   float* dx, void* stream);
+/* unpatchify: adjoint of dfu_patchify_f32 (timm patch_embed.proj): fp32
+ * [B*(H/ps)*(W/ps)][C*ps*ps] -> fp32 NCHW dx. */
+int dfu_unpatchify_f32(const float* dpatch, int32_t B, int32_t C, int32_t H, int32_t W,
+                       int32_t ps, float* dx, void* stream);
+/* Grad-CAM map per image (grad_cam_visualization.py:415-429): w_c = mean_p grad[b][p][c] over
+ * the Cg gradient channels, cam[b][p] = relu(sum_{c < min(Ca, Cg)} w_c act[b][p][c]) / max_p
+ * (when > 0).  Per-tensor element strides (batch, position, channel): NCHW or channels_last
+ * views; both bf16 or both fp32; cam fp32 [B][HW]. */
+int dfu_gradcam(const void* act, int32_t Ca, int64_t sab, int64_t sap, int64_t sac,
+                const void* grad, int32_t Cg, int64_t sgb, int64_t sgp, int64_t sgc,
+                int32_t is_bf16, int32_t B, int32_t HW, float* cam, void* stream);
+/* Input-gradient saliency (grad_cam_visualization.py:401-413, the ViT fallback):
+ * out[b][p] = mean_c |dx[b][c][p]|, divided by its per-image max when that is > 0. */
+int dfu_saliency(const float* dx, int32_t B, int32_t C, int32_t HW, float* out, void* stream);
+
 /* ---------------------------------------------------------------- BatchNorm (train) -- */
 /* torchvision BatchNorm2d(eps 1e-5, momentum 0.1) in training mode over NHWC [M][C].
  * finalize: combine the (sum, M2) tile slab of the producing GEMM into mean / invstd,

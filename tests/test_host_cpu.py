@@ -124,3 +124,19 @@ def test_flat_params_layout():
         assert p.data.data_ptr() == fp.data.data_ptr() + 4 * o
         assert p.grad.data_ptr() == fp.grad.data_ptr() + 4 * o
     assert fp.numel == 4 + 8 + 8 + 4
+
+
+def test_gradcam_target_layer_rule():
+    """grad_cam_visualization.py:389-392: the target is the LAST module name containing the
+    target string — the block output ReLU of layer4 and the ViT's last drop_path2 (a 3-D token
+    tensor, hence the input-saliency fallback); both are called by our forward when hooked."""
+    from models.fusion import MultimodalFusionModel
+    from models.gradcam import GradCAM
+    m = MultimodalFusionModel()
+    rc, tc = GradCAM(m.resnet, ["layer4"]), GradCAM(m.vit, ["blocks"])
+    assert rc.target_name() == "layer4.2.relu"
+    assert tc.target_name() == "blocks.11.drop_path2"
+    assert len(rc.handles) > 0 and len(tc.handles) > 0
+    rc.remove()
+    tc.remove()
+    assert not m.resnet.layer4[-1].relu._forward_hooks
