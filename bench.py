@@ -7,6 +7,7 @@ pairs already resident in HBM (BASELINE.json config C3; C4 = the same per GPU ov
 launched by torch.distributed.run, RCCL gradient all-reduce).  Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--config fusion|thermal|rgb]
+  python bench.py --config gradcam [--batch 32]   # C5: fusion predict + Grad-CAM maps per sample
 """
 import argparse
 import json
@@ -24,7 +25,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 # Algorithmic GEMM/conv FLOPs per unit of work (fwd + dgrad + wgrad), SURVEY.md §8(d)
-FLOPS_PER_UNIT = {"fusion": 129.44e9, "thermal": 105.15e9, "rgb": 24.29e9}
+FLOPS_PER_UNIT = {"fusion": 129.44e9, "thermal": 105.15e9, "rgb": 24.29e9, "gradcam": 173.20e9}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 RGB_MEAN = (0.485, 0.456, 0.406)
 RGB_STD = (0.229, 0.224, 0.225)
@@ -35,12 +36,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--config", default="fusion", choices=["fusion", "thermal", "rgb"])
+    ap.add_argument("--batch", type=int, default=None, help="per GPU (default 64; gradcam 32)")
+    ap.add_argument("--config", default="fusion", choices=["fusion", "thermal", "rgb", "gradcam"])
     ap.add_argument("--no-graph", action="store_true", help="eager step instead of a HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 32 if args.config == "gradcam" else 64
+    return args
 
 
 def synthetic(B, device, seed):
@@ -118,6 +122,37 @@ def cpu_baseline(config, threads, budget_s=10.0):
                       f"torch.set_num_threads({threads})"}
 
 
+def cpu_baseline_gradcam(threads, budget_s=10.0):
+    """The oracle's restatement of the reference Grad-CAM (oracle/gradcam_ref.py) timed on the host
+    cores, sample by sample as the reference runs it (bs=1, grad_cam_visualization.py:686): fusion
+    forward under no_grad, the ResNet 'layer4' CAM and the ViT input saliency."""
+    from oracle import gradcam_ref as G
+    from oracle import torch_ref as R
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    model = R.MultimodalFusionModel(num_classes=2, dropout=0.7).eval()
+    rgb, th, _ = R.synthetic_batch(4, seed=42)
+    cam = G.GradCAMRef(model.resnet, ["layer4"])
+
+    def sample(i):
+        with torch.no_grad():
+            torch.softmax(model(rgb[i:i + 1], th[i:i + 1]), 1).argmax(1)
+        cam.generate_cam(rgb[i:i + 1])
+        G.saliency_ref(model.vit, th[i:i + 1])
+
+    sample(0)
+    t0 = time.perf_counter()
+    n = 0
+    while n < 8 and (n == 0 or time.perf_counter() - t0 < budget_s):
+        sample(n % 4)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "samples/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 eager Grad-CAM (fusion predict + ResNet layer4 CAM + ViT "
+                      f"input saliency), bs=1 as the reference, {n} samples ({dt:.1f} s) after 1 "
+                      f"warm-up, torch.set_num_threads({threads})"}
+
+
 def gemm_traffic():
     """HBM bytes per GEMM launch from the latest committed PMC measurement
     (profiles/r*_gemm_traffic.json, written by tools/prof_summary.py from separate rocprofv3
@@ -164,6 +199,120 @@ def gemm_roofline(fwd_bwd, tail, replays=3):
             "achieved": flops / (us * 1e-6) / 1e12}
 
 
+def main_gradcam(args, rank, world, dev):
+    """C5 (grad_cam_visualization.py visualize_multimodal :561-632, batched): per batch of B
+    samples resident in HBM, one eval fusion forward under no_grad (softmax, argmax), then
+    GradCAM(model.resnet, ['layer4']) -> (B, 7, 7) CAMs and GradCAM(model.vit, ['blocks']) ->
+    (B, 224, 224) input saliency, each one forward + backward with input gradients.  Replicas
+    over ranks (each its own samples; no data-path collective)."""
+    from models.fusion import MultimodalFusionModel
+    from models.gradcam import GradCAM
+    model = MultimodalFusionModel(num_classes=2, dropout=0.7).to(dev).eval()
+    rgb, th, _ = synthetic(args.batch, dev, seed=42 + rank)
+    cam_rgb = GradCAM(model.resnet, ["layer4"])
+    cam_th = GradCAM(model.vit, ["blocks"])
+    outs = {}
+
+    def step():
+        with torch.no_grad():
+            probs = torch.softmax(model(rgb, th), dim=1)
+        outs["pred"] = probs.argmax(1)
+        outs["cam"] = cam_rgb.generate_cams(rgb)
+        outs["sal"] = cam_th.generate_cams(th)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(max(1, args.warmup)):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    assert outs["cam"].shape == (args.batch, 7, 7) and outs["sal"].shape == (args.batch, 224, 224)
+    ref_cam = outs["cam"].clone()
+    graph = None
+    if not args.no_graph:
+        try:  # the hooks' Python runs once, at capture; replays rewrite the same buffers
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            graph.replay()
+            torch.cuda.synchronize()
+            if not torch.allclose(outs["cam"], ref_cam, atol=1e-2):
+                raise RuntimeError("graph replay changed the CAMs")
+        except Exception as e:
+            if rank == 0:
+                print(f"[bench] graph capture failed ({type(e).__name__}: {e}); eager",
+                      file=sys.stderr)
+            graph = None
+            torch.cuda.synchronize()
+    run = graph.replay if graph is not None else step
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        run()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        t = torch.tensor([elapsed, gpu_ms / 1000.0], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gpu_s = t.tolist()
+        gpu_ms = gpu_s * 1000.0
+    gr = gemm_roofline(step, lambda: None)
+    value = args.batch * args.gpus * args.steps / elapsed
+    per_step_s = gpu_ms / 1000.0 / args.steps
+    achieved = args.batch * FLOPS_PER_UNIT["gradcam"] / per_step_s / 1e12
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline_gradcam(min(args.cpu_threads, os.cpu_count() or 1))
+            except Exception as e:
+                cpu = {"error": f"{type(e).__name__}: {e}"}
+        traffic, traffic_src = gemm_traffic()
+        line = {
+            "metric": "samples/sec (fusion predict + Grad-CAM maps, bs=32/GPU)",
+            "value": round(value, 2), "unit": "samples/sec", "n_gpus": args.gpus,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1000.0 / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic 224x224 RGB+thermal pairs (uint8 U{0..255}, reference "
+                    "normalisation), random-init weights (seed 42), resident in HBM",
+            "config": {"workload": "C5 fusion eval predict + ResNet 'layer4' Grad-CAM + ViT "
+                                   "'blocks' input saliency (fwd+bwd with input grads)",
+                       "model": "resnet50+vit_base_patch16_224 late fusion",
+                       "global_batch": args.batch * args.gpus, "per_gpu_batch": args.batch,
+                       "image": 224, "parallelism": f"replicas{args.gpus}",
+                       "hip_graph": graph is not None},
+            "roofline": {"bound": "mfma", "achieved": round(gr["achieved"], 1),
+                         "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(gr["achieved"] / PEAK_BF16_TFLOPS, 4),
+                         "traffic": None, "traffic_note": "PMC traffic measured on the C3 bench "
+                                                          f"({traffic_src}: {traffic} B/launch)",
+                         "algorithmic_bytes_per_launch": round(gr["bytes_per_launch"]),
+                         "kernel": "dfu gemm_kernel (MFMA bf16 GEMM template)",
+                         "launches_per_step": gr["launches_per_step"],
+                         "avg_launch_us": round(gr["avg_launch_us"], 2),
+                         "gemm_ms_per_step": round(gr["gemm_ms_per_step"], 3),
+                         "step": {"achieved": round(achieved, 1),
+                                  "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                                  "basis": f"173.20 GFLOP per sample (SURVEY 8d) x {args.batch} / "
+                                           f"HIP-event step time {per_step_s * 1e3:.3f} ms"}},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     from dfu_hip import parallel
@@ -173,6 +322,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     torch.manual_seed(42)
+    if args.config == "gradcam":
+        return main_gradcam(args, rank, world, dev)
 
     from dfu_hip import nn as hnn
     from dfu_hip.optim import FusedAdamW
