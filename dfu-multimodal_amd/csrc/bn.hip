@@ -8,45 +8,41 @@
 namespace {
 
 // ---------------------------------------------------------------- forward finalize
-// Block = 64 tile-lanes x 4 channels; Chan-merge of (count, mean, M2) in fp64.
-__global__ void k_bn_finalize(const float* __restrict__ stats, int tiles, int M, int C,
-                              const float* __restrict__ gamma, const float* __restrict__ beta,
-                              float eps, float momentum, float* __restrict__ rmean,
-                              float* __restrict__ rvar, int64_t* __restrict__ nbt,
-                              float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                              float* __restrict__ scale_out, float* __restrict__ shift_out) {
-  // Per tile t (nb rows): sum sb and M2 qb -> sum of squares qb + sb^2/nb.  fp64 sums of x and
-  // x^2 over <= 1e6 rows of bf16-scale values keep var = E[x^2] - mean^2 exact to ~1e-12
-  // relative, and the tile loop is independent adds (no serial merge chain).
-  __shared__ double sh_s[4][64], sh_q[4][64];
-  const int tl = threadIdx.x & 63, cl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 4 + cl;
+// Block = 16 waves x 64 channel-lanes: a lane owns one channel (the 64 lanes of a wave read one
+// contiguous 256-B row segment of the slab per tile), the waves stride the tiles; fp64 sums,
+// then a 16-way LDS reduction.  Per tile t (nb rows): sum sb and M2 qb -> sum of squares
+// qb + sb^2/nb.  fp64 sums of x and x^2 over <= 1e6 rows of bf16-scale values keep
+// var = E[x^2] - mean^2 exact to ~1e-12 relative, and the tile loop is independent adds.
+constexpr int FIN_WAVES = 16;
+
+__global__ __launch_bounds__(1024) void k_bn_finalize(
+    const float* __restrict__ stats, int tiles, int M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ rmean,
+    float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  __shared__ double sh_s[FIN_WAVES][64], sh_q[FIN_WAVES][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   double sx = 0.0, sxx = 0.0;
   if (c < C) {
     const int last = tiles - 1;
     const double inv_last = 1.0 / (double)(M - last * 128);
 #pragma unroll 4
-    for (int t = tl; t < tiles; t += 64) {
+    for (int t = w; t < tiles; t += FIN_WAVES) {
       const double sb = stats[((int64_t)t * 2 + 0) * C + c];
       const double qb = stats[((int64_t)t * 2 + 1) * C + c];
       sx += sb;
       sxx += qb + sb * sb * (t == last ? inv_last : (1.0 / 128.0));
     }
   }
-  sh_s[cl][tl] = sx;
-  sh_q[cl][tl] = sxx;
+  sh_s[w][lane] = sx;
+  sh_q[w][lane] = sxx;
   __syncthreads();
-  for (int st = 32; st > 0; st >>= 1) {
-    if (tl < st) {
-      sh_s[cl][tl] += sh_s[cl][tl + st];
-      sh_q[cl][tl] += sh_q[cl][tl + st];
-    }
-    __syncthreads();
-  }
-  if (tl == 0 && c < C) {
+  if (w == 0 && c < C) {
+    for (int k = 1; k < FIN_WAVES; ++k) { sx += sh_s[k][lane]; sxx += sh_q[k][lane]; }
     const double nn = (double)M;
-    const double mu = sh_s[cl][0] / nn;
-    const double var = fmax(sh_q[cl][0] / nn - mu * mu, 0.0);  // biased, used to normalise
+    const double mu = sx / nn;
+    const double var = fmax(sxx / nn - mu * mu, 0.0);  // biased, used to normalise
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f;
     const float b = beta ? beta[c] : 0.f;
@@ -129,8 +125,24 @@ inline int bwd_rows_per_block(int64_t M, int C) {
   return (int)rpb;
 }
 
+// RELU: 0 none; 1 mask = out > 0 (the stored output: BN + residual + ReLU); 2 mask =
+// fma(y, scale, shift) > 0, the forward's own pre-ReLU value recomputed from y (BN + ReLU with
+// no residual: the same fp32 value k_bn_apply rounded, so the same mask, without reading out).
+// A compile-time mode: every load of an iteration is issued before any of them is used.
+template <int RELU>
+DFU_DEV void relu_mask8(const float* oo, const float* yy, const float* sc, const float* sf,
+                        float* g) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if constexpr (RELU == 1) g[e] = oo[e] > 0.f ? g[e] : 0.f;
+    if constexpr (RELU == 2) g[e] = (fmaf(yy[e], sc[e], sf[e]) + 0.f) > 0.f ? g[e] : 0.f;
+  }
+}
+
+template <int RELU>
 __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ y,
-                                const bf16_t* __restrict__ out, int relu,
+                                const bf16_t* __restrict__ out,
+                                const float* __restrict__ scale, const float* __restrict__ shift,
                                 const float* __restrict__ mean, const float* __restrict__ invstd,
                                 int64_t M, int C, int rows_per_block, float* __restrict__ partial) {
   __shared__ float red[2][256][8];
@@ -143,20 +155,23 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float mu[8], is[8];
+  float mu[8], is[8], sc[8] = {}, sf[8] = {};
 #pragma unroll
   for (int e = 0; e < 8; ++e) { mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e]; }
+  if constexpr (RELU == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; }
+  }
   for (int64_t r = r0 + rl; r < r1; r += rl_n) {
     const int64_t o = r * C + c0;
-    float g[8], yy[8];
-    unpack8(*(const u32x4*)(dout + o), g);
-    unpack8(*(const u32x4*)(y + o), yy);
-    if (relu) {
-      float oo[8];
-      unpack8(*(const u32x4*)(out + o), oo);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] = oo[e] > 0.f ? g[e] : 0.f;
-    }
+    float g[8], yy[8], oo[8];
+    const u32x4 gv = *(const u32x4*)(dout + o), yv = *(const u32x4*)(y + o);
+    u32x4 ov = {};
+    if constexpr (RELU == 1) ov = *(const u32x4*)(out + o);
+    unpack8(gv, g);
+    unpack8(yv, yy);
+    unpack8(ov, oo);
+    relu_mask8<RELU>(oo, yy, sc, sf, g);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       sg[e] += g[e];
@@ -181,27 +196,28 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
   }
 }
 
-// 32 block-lanes x 8 channels per workgroup; fp64 sums.
-__global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int blocks, int64_t M, int C,
-                                  const float* __restrict__ gamma,
-                                  const float* __restrict__ invstd, int batch_stats,
-                                  float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                  float* __restrict__ coef) {
-  __shared__ double red[2][32][8];
-  const int cl = threadIdx.x & 7, bl = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + cl;
+// 16 waves x 64 channel-lanes per workgroup (coalesced 256-B row segments of the partials, the
+// waves stride the row-blocks); fp64 sums, 16-way LDS reduction.
+__global__ __launch_bounds__(1024) void k_bn_bwd_finalize(
+    const float* __restrict__ partial, int blocks, int64_t M, int C,
+    const float* __restrict__ gamma, const float* __restrict__ invstd, int batch_stats,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef) {
+  __shared__ double red[2][FIN_WAVES][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   double sg = 0.0, sgx = 0.0;
   if (c < C) {
-    for (int b = bl; b < blocks; b += 32) {
+#pragma unroll 4
+    for (int b = w; b < blocks; b += FIN_WAVES) {
       sg += partial[((int64_t)b * 2 + 0) * C + c];
       sgx += partial[((int64_t)b * 2 + 1) * C + c];
     }
   }
-  red[0][bl][cl] = sg;
-  red[1][bl][cl] = sgx;
+  red[0][w][lane] = sg;
+  red[1][w][lane] = sgx;
   __syncthreads();
-  if (bl == 0 && c < C) {
-    for (int l = 1; l < 32; ++l) { sg += red[0][l][cl]; sgx += red[1][l][cl]; }
+  if (w == 0 && c < C) {
+    for (int k = 1; k < FIN_WAVES; ++k) { sg += red[0][k][lane]; sgx += red[1][k][lane]; }
     if (dbeta) dbeta[c] += (float)sg;
     if (dgamma) dgamma[c] += (float)sgx;
     const float g = gamma ? gamma[c] : 1.f;
@@ -213,15 +229,16 @@ __global__ void k_bn_bwd_finalize(const float* __restrict__ partial, int blocks,
 
 // dy = k (g - m1 - xhat m2), xhat = (y - mean) invstd  ==  a g + b y + c per channel with
 // a = k, b = -k m2 invstd, c = k (m2 invstd mean - m1).
-template <bool FIXED>
+template <int RELU, bool FIXED>
 __global__ void k_bn_bwd_apply(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ y,
-                               const bf16_t* __restrict__ out, int relu,
+                               const bf16_t* __restrict__ out,
+                               const float* __restrict__ scale, const float* __restrict__ shift,
                                const float* __restrict__ mean, const float* __restrict__ invstd,
                                const float* __restrict__ coef, int64_t M, int C,
                                bf16_t* __restrict__ dy, bf16_t* __restrict__ dres) {
   const int cv = C / 8;
   const int64_t n = M * cv;
-  float ka[8], kb[8], kc[8];
+  float ka[8], kb[8], kc[8], sc[8] = {}, sf[8] = {};
   auto load_coef = [&](int c0) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -231,21 +248,21 @@ __global__ void k_bn_bwd_apply(const bf16_t* __restrict__ dout, const bf16_t* __
       ka[e] = k;
       kb[e] = -k * m2 * is;
       kc[e] = k * (m2 * is * mean[c] - m1);
+      if constexpr (RELU == 2) { sc[e] = scale[c]; sf[e] = shift[c]; }
     }
   };
   if (FIXED) load_coef((threadIdx.x & (cv - 1)) * 8);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if (!FIXED) load_coef((int)(i % cv) * 8);
-    float g[8], yy[8];
-    unpack8(*(const u32x4*)(dout + i * 8), g);
-    unpack8(*(const u32x4*)(y + i * 8), yy);
-    if (relu) {
-      float oo[8];
-      unpack8(*(const u32x4*)(out + i * 8), oo);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] = oo[e] > 0.f ? g[e] : 0.f;
-    }
+    float g[8], yy[8], oo[8];
+    const u32x4 gv = *(const u32x4*)(dout + i * 8), yv = *(const u32x4*)(y + i * 8);
+    u32x4 ov = {};
+    if constexpr (RELU == 1) ov = *(const u32x4*)(out + i * 8);
+    unpack8(gv, g);
+    unpack8(yv, yy);
+    unpack8(ov, oo);
+    relu_mask8<RELU>(oo, yy, sc, sf, g);
     if (dres) *(u32x4*)(dres + i * 8) = pack8(g);
     float d[8];
 #pragma unroll
@@ -270,7 +287,8 @@ extern "C" int dfu_bn_finalize(const float* stats, int32_t tiles, int32_t M, int
   DFU_CHECK_ARG(stats && tiles == (M + 127) / 128 && C > 0 && mean_out && invstd_out &&
                     scale_out && shift_out,
                 "dfu_bn_finalize: bad args (tiles=%d M=%d)", tiles, M);
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 3) / 4), dim3(256), 0, (hipStream_t)stream, stats,
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0,
+                     (hipStream_t)stream, stats,
                      tiles, M, C, gamma, beta, eps, momentum, running_mean, running_var,
                      num_batches, mean_out, invstd_out, scale_out, shift_out);
   DFU_LAUNCH_CHECK();
@@ -306,19 +324,23 @@ extern "C" int dfu_bn_bwd_blocks(int64_t M, int32_t C) {
 }
 
 extern "C" int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* out, int32_t relu,
-                                 const float* mean, const float* invstd, int64_t M, int32_t C,
-                                 float* partial, void* stream) {
-  DFU_CHECK_ARG(dout && y && mean && invstd && partial && C % 8 == 0 && M > 0,
+                                 const float* scale, const float* shift, const float* mean,
+                                 const float* invstd, int64_t M, int32_t C, float* partial,
+                                 void* stream) {
+  DFU_CHECK_ARG(dout && y && mean && invstd && partial && C % 8 == 0 && M > 0 && relu >= 0 &&
+                    relu <= 2,
                 "dfu_bn_bwd_reduce: bad args");
-  DFU_CHECK_ARG(!relu || out, "dfu_bn_bwd_reduce: relu needs out");
+  DFU_CHECK_ARG(relu != 1 || out, "dfu_bn_bwd_reduce: relu=1 needs out");
+  DFU_CHECK_ARG(relu != 2 || (scale && shift), "dfu_bn_bwd_reduce: relu=2 needs scale/shift");
   const int cv = C / 8;
   const int ct_n = cv < 64 ? cv : 64;
   DFU_CHECK_ARG(256 % ct_n == 0 && cv % ct_n == 0, "dfu_bn_bwd_reduce: C=%d unsupported", C);
   const int rpb = bwd_rows_per_block(M, C);
   dim3 grid(cv / ct_n, dfu_bn_bwd_blocks(M, C));
-  hipLaunchKernelGGL(k_bn_bwd_reduce, grid, dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, relu, mean, invstd,
-                     M, C, rpb, partial);
+  auto kern = relu == 1 ? k_bn_bwd_reduce<1> : relu == 2 ? k_bn_bwd_reduce<2> : k_bn_bwd_reduce<0>;
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dout,
+                     (const bf16_t*)y, (const bf16_t*)out, scale, shift, mean, invstd, M, C, rpb,
+                     partial);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
@@ -327,22 +349,29 @@ extern "C" int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t
                                    const float* gamma, const float* invstd, int32_t batch_stats,
                                    float* dgamma, float* dbeta, float* coef, void* stream) {
   DFU_CHECK_ARG(partial && invstd && coef && blocks > 0 && C > 0, "dfu_bn_bwd_finalize: bad args");
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 7) / 8), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0,
+                     (hipStream_t)stream,
                      partial, blocks, M, C, gamma, invstd, batch_stats, dgamma, dbeta, coef);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
 
 extern "C" int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t relu,
-                                const float* mean, const float* invstd, const float* coef,
-                                int64_t M, int32_t C, void* dy, void* dres, void* stream) {
-  DFU_CHECK_ARG(dout && y && mean && invstd && coef && dy && C % 8 == 0 && M > 0,
+                                const float* scale, const float* shift, const float* mean,
+                                const float* invstd, const float* coef, int64_t M, int32_t C,
+                                void* dy, void* dres, void* stream) {
+  DFU_CHECK_ARG(dout && y && mean && invstd && coef && dy && C % 8 == 0 && M > 0 && relu >= 0 &&
+                    relu <= 2,
                 "dfu_bn_bwd_apply: bad args");
-  DFU_CHECK_ARG(!relu || out, "dfu_bn_bwd_apply: relu needs out");
-  hipLaunchKernelGGL(fixed_channels(C) ? k_bn_bwd_apply<true> : k_bn_bwd_apply<false>,
-                     dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, relu, mean, invstd,
-                     coef, M, C, (bf16_t*)dy, (bf16_t*)dres);
+  DFU_CHECK_ARG(relu != 1 || out, "dfu_bn_bwd_apply: relu=1 needs out");
+  DFU_CHECK_ARG(relu != 2 || (scale && shift), "dfu_bn_bwd_apply: relu=2 needs scale/shift");
+  const bool fx = fixed_channels(C);
+  auto kern = relu == 1   ? (fx ? k_bn_bwd_apply<1, true> : k_bn_bwd_apply<1, false>)
+              : relu == 2 ? (fx ? k_bn_bwd_apply<2, true> : k_bn_bwd_apply<2, false>)
+                          : (fx ? k_bn_bwd_apply<0, true> : k_bn_bwd_apply<0, false>);
+  hipLaunchKernelGGL(kern, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, scale, shift, mean,
+                     invstd, coef, M, C, (bf16_t*)dy, (bf16_t*)dres);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

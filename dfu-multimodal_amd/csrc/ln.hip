@@ -59,102 +59,127 @@ __global__ void k_ln_fwd(const float* __restrict__ x, int64_t ldx, int rows, int
 
 constexpr int LNB_ROWS = 16;  // rows per block in the backward (4 per wave): 788 blocks at B=64
 
-template <bool DY_BF>
-__global__ void k_ln_bwd(const void* __restrict__ dyv, int64_t lddy, const float* __restrict__ x,
-                         int64_t ldx, const float* __restrict__ mean_in,
-                         const float* __restrict__ rstd_in, const float* __restrict__ gamma,
-                         int rows, int D, float* __restrict__ gx, int64_t ldg,
-                         bf16_t* __restrict__ gx_bf, float* __restrict__ partial,
-                         float* __restrict__ gsum_partial) {
-  __shared__ float red[3][4][1024];
+// Backward, one wave per row, 4 rows per wave processed two at a time: all loads of a row pair
+// (x, dy, and the residual gradient gx it adds into) are issued before either row's
+// reductions, so each pair costs one memory round trip.  NV = float4 chunks per lane
+// (D <= 256 * NV).  dgamma / dbeta / column sums of the updated gx are reduced over the 4
+// waves through one LDS buffer reused per quantity.
+template <bool DY_BF, int NV>
+__global__ __launch_bounds__(256) void k_ln_bwd(
+    const void* __restrict__ dyv, int64_t lddy, const float* __restrict__ x, int64_t ldx,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const float* __restrict__ gamma, int rows, int D, float* __restrict__ gx, int64_t ldg,
+    bf16_t* __restrict__ gx_bf, float* __restrict__ partial, float* __restrict__ gsum_partial) {
+  __shared__ float red[4][256 * NV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = D / 4;
-  float dg[MAXV][4], db[MAXV][4], gs[MAXV][4];
+  float dg[NV][4], db[NV][4], gs[NV][4];
+  f32x4 gm[NV];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { dg[i][e] = 0.f; db[i][e] = 0.f; gs[i][e] = 0.f; }
-  f32x4 gm[MAXV];
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int j = lane + 64 * i;
     gm[i] = j < nv ? *(const f32x4*)(gamma + 4 * j) : (f32x4){0, 0, 0, 0};
-  }
-  for (int rr = 0; rr < LNB_ROWS / 4; ++rr) {
-    const int row = blockIdx.x * LNB_ROWS + wave * (LNB_ROWS / 4) + rr;
-    if (row >= rows) break;
-    const float mu = mean_in[row], rs = rstd_in[row];
-    float xh[MAXV][4], dy[MAXV][4];
-    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const int j = lane + 64 * i;
-      if (j < nv) {
-        const f32x4 xv = *(const f32x4*)(x + (int64_t)row * ldx + 4 * j);
-        if constexpr (DY_BF) {
-          const u32x2 w = *(const u32x2*)((const bf16_t*)dyv + (int64_t)row * lddy + 4 * j);
-          dy[i][0] = lo_bf(w[0]); dy[i][1] = hi_bf(w[0]); dy[i][2] = lo_bf(w[1]); dy[i][3] = hi_bf(w[1]);
+    for (int e = 0; e < 4; ++e) { dg[i][e] = 0.f; db[i][e] = 0.f; gs[i][e] = 0.f; }
+  }
+  const int row0 = blockIdx.x * LNB_ROWS + wave * (LNB_ROWS / 4);
+#pragma unroll 1
+  for (int rp = 0; rp < LNB_ROWS / 4; rp += 2) {
+    f32x4 xv[2][NV], gv[2][NV];
+    float dy[2][NV][4], mu[2], rs[2];
+    bool ok[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // load phase: both rows
+      const int row = row0 + rp + h;
+      ok[h] = row < rows;
+      mu[h] = ok[h] ? mean_in[row] : 0.f;
+      rs[h] = ok[h] ? rstd_in[row] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int j = lane + 64 * i;
+        if (ok[h] && j < nv) {
+          xv[h][i] = *(const f32x4*)(x + (int64_t)row * ldx + 4 * j);
+          gv[h][i] = *(const f32x4*)(gx + (int64_t)row * ldg + 4 * j);
+          if constexpr (DY_BF) {
+            const u32x2 w = *(const u32x2*)((const bf16_t*)dyv + (int64_t)row * lddy + 4 * j);
+            dy[h][i][0] = lo_bf(w[0]); dy[h][i][1] = hi_bf(w[0]);
+            dy[h][i][2] = lo_bf(w[1]); dy[h][i][3] = hi_bf(w[1]);
+          } else {
+            const f32x4 w = *(const f32x4*)((const float*)dyv + (int64_t)row * lddy + 4 * j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dy[h][i][e] = w[e];
+          }
         } else {
-          const f32x4 w = *(const f32x4*)((const float*)dyv + (int64_t)row * lddy + 4 * j);
-          dy[i][0] = w[0]; dy[i][1] = w[1]; dy[i][2] = w[2]; dy[i][3] = w[3];
+          xv[h][i] = (f32x4){0, 0, 0, 0};
+          gv[h][i] = (f32x4){0, 0, 0, 0};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dy[h][i][e] = 0.f;
         }
+      }
+    }
+    float s1[2], s2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      s1[h] = 0.f;
+      s2[h] = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          xh[i][e] = (xv[e] - mu) * rs;
-          const float dxh = dy[i][e] * gm[i][e];
-          s1 += dxh;
-          s2 += dxh * xh[i][e];
-          dg[i][e] += dy[i][e] * xh[i][e];
-          db[i][e] += dy[i][e];
+          const float xh = (xv[h][i][e] - mu[h]) * rs[h];
+          const float dxh = dy[h][i][e] * gm[i][e];
+          s1[h] += dxh;
+          s2[h] += dxh * xh;
+          dg[i][e] += dy[h][i][e] * xh;
+          db[i][e] += dy[h][i][e];
         }
-      } else {
+    }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { xh[i][e] = 0.f; dy[i][e] = 0.f; }
+    for (int h = 0; h < 2; ++h) {
+      s1[h] = wave_sum(s1[h]) / (float)D;
+      s2[h] = wave_sum(s2[h]) / (float)D;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!ok[h]) continue;
+      const int row = row0 + rp + h;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int j = lane + 64 * i;
+        if (j >= nv) continue;
+        f32x4 g = gv[h][i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (xv[h][i][e] - mu[h]) * rs[h];
+          g[e] += rs[h] * (dy[h][i][e] * gm[i][e] - s1[h] - xh * s2[h]);
+          gs[i][e] += g[e];
+        }
+        *(f32x4*)(gx + (int64_t)row * ldg + 4 * j) = g;
+        if (gx_bf) {
+          bf16_t* gb = gx_bf + (int64_t)row * ldg + 4 * j;
+          *(u32x2*)gb = (u32x2){pack2(g[0], g[1]), pack2(g[2], g[3])};
+        }
       }
     }
-    s1 = wave_sum(s1) / (float)D;
-    s2 = wave_sum(s2) / (float)D;
+  }
+  // reduce dgamma, dbeta (and the gx column sums) over the 4 waves, one quantity at a time
+  auto wave_reduce = [&](float (&q)[NV][4], float* dst) {
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int j = lane + 64 * i;
-      if (j >= nv) continue;
-      float* g = gx + (int64_t)row * ldg + 4 * j;
-      f32x4 gv = *(f32x4*)g;
+      if (j < nv)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        gv[e] += rs * (dy[i][e] * gm[i][e] - s1 - xh[i][e] * s2);
-        gs[i][e] += gv[e];
-      }
-      *(f32x4*)g = gv;
-      if (gx_bf) {
-        bf16_t* gb = gx_bf + (int64_t)row * ldg + 4 * j;
-        *(u32x2*)gb = (u32x2){pack2(gv[0], gv[1]), pack2(gv[2], gv[3])};
-      }
+        for (int e = 0; e < 4; ++e) red[wave][4 * j + e] = q[i][e];
     }
-  }
-  // reduce dgamma/dbeta over the 4 waves
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int j = lane + 64 * i;
-    if (j < nv)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        red[0][wave][4 * j + e] = dg[i][e];
-        red[1][wave][4 * j + e] = db[i][e];
-        red[2][wave][4 * j + e] = gs[i][e];
-      }
-  }
-  __syncthreads();
-  if (gsum_partial)  // column sums of the updated residual gradient (the upstream bias grad)
+    __syncthreads();
     for (int d = threadIdx.x; d < D; d += blockDim.x)
-      gsum_partial[(int64_t)blockIdx.x * D + d] =
-          red[2][0][d] + red[2][1][d] + red[2][2][d] + red[2][3][d];
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    partial[((int64_t)blockIdx.x * 2 + 0) * D + d] =
-        red[0][0][d] + red[0][1][d] + red[0][2][d] + red[0][3][d];
-    partial[((int64_t)blockIdx.x * 2 + 1) * D + d] =
-        red[1][0][d] + red[1][1][d] + red[1][2][d] + red[1][3][d];
-  }
+      dst[d] = red[0][d] + red[1][d] + red[2][d] + red[3][d];
+    __syncthreads();
+  };
+  wave_reduce(dg, partial + ((int64_t)blockIdx.x * 2 + 0) * D);
+  wave_reduce(db, partial + ((int64_t)blockIdx.x * 2 + 1) * D);
+  if (gsum_partial)  // column sums of the updated residual gradient (the upstream bias grad)
+    wave_reduce(gs, gsum_partial + (int64_t)blockIdx.x * D);
 }
 
 }  // namespace
@@ -189,12 +214,10 @@ extern "C" int dfu_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_bf16, 
                 "dfu_layernorm_bwd: bad args");
   DFU_CHECK_ARG(lddy % 4 == 0 && ldx % 4 == 0 && ldg % 4 == 0, "dfu_layernorm_bwd: bad ld");
   dim3 grid(dfu_ln_bwd_blocks(rows));
-  if (dy_bf16)
-    hipLaunchKernelGGL(k_ln_bwd<true>, grid, dim3(256), 0, (hipStream_t)stream, dy, lddy, x, ldx,
-                       mean, rstd, gamma, rows, D, gx, ldg, (bf16_t*)gx_bf16, partial, gsum_partial);
-  else
-    hipLaunchKernelGGL(k_ln_bwd<false>, grid, dim3(256), 0, (hipStream_t)stream, dy, lddy, x, ldx,
-                       mean, rstd, gamma, rows, D, gx, ldg, (bf16_t*)gx_bf16, partial, gsum_partial);
+  auto kern = D <= 768 ? (dy_bf16 ? k_ln_bwd<true, 3> : k_ln_bwd<false, 3>)
+                       : (dy_bf16 ? k_ln_bwd<true, 4> : k_ln_bwd<false, 4>);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, dy, lddy, x, ldx, mean, rstd,
+                     gamma, rows, D, gx, ldg, (bf16_t*)gx_bf16, partial, gsum_partial);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -178,11 +178,15 @@ class _BN:
                                self.invstd, _empty((self.C,), F32, self.mean.device))
 
     def backward(self, dout, y, out, relu, dy, dres):
+        """relu: False; True (mask from `out`, the BN + residual + ReLU case); or 2 (BN + ReLU
+        with no residual: the mask is recomputed from y with the forward's scale/shift, so
+        `out` is not read)."""
         bn = self.bn
         dgamma = grad_buffer(bn.weight) if _wants(bn.weight) else None
         dbeta = grad_buffer(bn.bias) if _wants(bn.bias) else None
         ops.bn_bwd(dout, y, out, relu, self.mean, self.invstd, bn.weight, self.M, self.C, dy,
-                   dres, dgamma, dbeta, batch_stats=self.training)
+                   dres, dgamma, dbeta, batch_stats=self.training, scale=self.scale,
+                   shift=self.shift)
         grads_done(bn.weight, bn.bias)
 
 
@@ -281,7 +285,7 @@ class StemFn(torch.autograd.Function):
         da = ops.maxpool_bwd(g, am, B, P, Q, Cout, P2, Q2).view(B * P * Q, Cout)
         M = B * P * Q
         dy = torch.empty_like(y)
-        ctx.bns.backward(da, y, a, True, dy, None)
+        ctx.bns.backward(da, y, None, 2, dy, None)
         w = mod.conv1.weight
         if _wants(w):
             dw = grad_buffer(w).view(Cout, -1)
@@ -403,7 +407,7 @@ class BottleneckFn(torch.autograd.Function):
             grads_done(mod.conv3.weight)
         # bn2 + relu, conv2
         dy2 = torch.empty_like(y2)
-        s2.backward(da2, y2, a2, True, dy2, None)
+        s2.backward(da2, y2, None, 2, dy2, None)
         da1 = torch.empty_like(a1)
         conv_dgrad(dy2, g2, w2, da1)
         if ctx.probes is not None:
@@ -413,7 +417,7 @@ class BottleneckFn(torch.autograd.Function):
             grads_done(mod.conv2.weight)
         # bn1 + relu, conv1 (+ identity gradient fused in the dgrad epilogue)
         dy1 = torch.empty_like(y1)
-        s1.backward(da1, y1, a1, True, dy1, None)
+        s1.backward(da1, y1, None, 2, dy1, None)
         dx = None
         if ctx.x_requires_grad:
             dxr = _empty((M1, Cin), BF16, dev)

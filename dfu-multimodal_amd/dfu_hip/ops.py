@@ -326,19 +326,26 @@ def bn_apply(y, scale, shift, residual, relu, out, M, C):
 
 
 def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta,
-           batch_stats=True):
-    """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply."""
+           batch_stats=True, scale=None, shift=None):
+    """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply.  relu: False/0 none;
+    True/1 mask from the stored output `out`; 2 mask recomputed from y with the forward's
+    scale/shift (BN + ReLU without residual; `out` is not read)."""
+    relu = int(relu)
+    if relu == 2 and (scale is None or shift is None):
+        raise ValueError("bn_bwd: relu=2 needs the forward scale/shift")
     blocks = lib().dfu_bn_bwd_blocks(M, C)
     partial = torch.empty((blocks, 2, C), dtype=F32, device=y.device)
     coef = torch.empty((C, 3), dtype=F32, device=y.device)
     s = stream_ptr()
-    check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), int(relu), ptr(mean), ptr(invstd),
-                                  M, C, ptr(partial), s), "dfu_bn_bwd_reduce")
+    check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
+                                  ptr(mean), ptr(invstd), M, C, ptr(partial), s),
+          "dfu_bn_bwd_reduce")
     check(lib().dfu_bn_bwd_finalize(ptr(partial), blocks, M, C, ptr(gamma), ptr(invstd),
                                     int(batch_stats), ptr(dgamma), ptr(dbeta), ptr(coef), s),
           "dfu_bn_bwd_finalize")
-    check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), int(relu), ptr(mean), ptr(invstd),
-                                 ptr(coef), M, C, ptr(dy), ptr(dres), s), "dfu_bn_bwd_apply")
+    check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
+                                 ptr(mean), ptr(invstd), ptr(coef), M, C, ptr(dy), ptr(dres), s),
+          "dfu_bn_bwd_apply")
 
 
 # ------------------------------------------------------------------------------- pooling

@@ -188,11 +188,13 @@ int dfu_bn_eval_coeffs(const float* gamma, const float* beta, const float* runni
 int dfu_bn_apply(const void* y, const float* scale, const float* shift, const void* residual,
                  int32_t relu, void* out, int64_t M, int32_t C, void* stream);
 /* Backward of out = act(bn(y) (+res)).  reduce: per-channel partial sums of g and g*xhat,
- * g = dout * [out > 0 if relu]; written as [blocks][2][C] (dfu_bn_bwd_blocks(M, C)). */
+ * g = dout * mask; written as [blocks][2][C] (dfu_bn_bwd_blocks(M, C)).  relu: 0 no mask;
+ * 1 mask = out > 0 (BN + residual + ReLU: reads out); 2 mask = y*scale + shift > 0 with the
+ * forward's scale/shift (BN + ReLU, no residual: recomputed from y, out not read). */
 int dfu_bn_bwd_blocks(int64_t M, int32_t C);
 int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* out, int32_t relu,
-                      const float* mean, const float* invstd, int64_t M, int32_t C,
-                      float* partial, void* stream);
+                      const float* scale, const float* shift, const float* mean,
+                      const float* invstd, int64_t M, int32_t C, float* partial, void* stream);
 /* finalize: sums -> dgamma, dbeta (accumulated into grad buffers, may be NULL) and the
  * per-channel coefficients used by apply.  batch_stats = 0 for eval-mode BN (running
  * statistics are constants: dy = gamma*invstd*g). */
@@ -201,8 +203,9 @@ int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t M, int32_t
                         float* dgamma, float* dbeta, float* coef, void* stream);
 /* dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); optionally dres = g (bf16). */
 int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t relu,
-                     const float* mean, const float* invstd, const float* coef, int64_t M,
-                     int32_t C, void* dy, void* dres, void* stream);
+                     const float* scale, const float* shift, const float* mean,
+                     const float* invstd, const float* coef, int64_t M, int32_t C, void* dy,
+                     void* dres, void* stream);
 
 /* ---------------------------------------------------------------- pooling ----------- */
 /* resnet maxpool 3x3/s2/p1 on NHWC bf16; argmax (0..8 window index) saved as uint8. */

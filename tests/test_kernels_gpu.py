@@ -299,6 +299,34 @@ def test_batchnorm_train_fwd_bwd():
     close(dbeta, bf.grad, atol=0.5, rtol=1e-2, what="dbeta")
 
 
+@pytest.mark.parametrize("M,C", [(5000, 128), (3136, 2048), (200704, 64)])
+def test_batchnorm_bwd_mask_from_y_is_bitwise(M, C):
+    """relu=2 (mask recomputed from y with the forward scale/shift, `out` not read) equals relu=1
+    (mask from the stored BN+ReLU output) bit for bit."""
+    y = rnd(M, C, seed=50, scale=2.0)
+    stats = torch.empty(ops.stats_tiles(M), 2, C, dtype=torch.float32, device=DEV)
+    Y = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(M, C, C, y, C, torch.eye(C, dtype=torch.bfloat16, device=DEV), C, Y, C,
+             epilogue=L.EPI_BF16_STATS, stats=stats)
+    gamma = rnd(C, dtype=torch.float32, seed=51) * 0.5 + 1
+    beta = rnd(C, dtype=torch.float32, seed=52)
+    mean, invstd, scale, shift = (torch.empty(C, device=DEV) for _ in range(4))
+    ops.bn_finalize(stats, M, C, gamma, beta, 1e-5, 0.1, None, None, None, mean, invstd, scale,
+                    shift)
+    out = torch.empty_like(Y)
+    ops.bn_apply(Y, scale, shift, None, True, out, M, C)
+    dout = rnd(M, C, seed=53)
+    res = []
+    for mode, o in ((1, out), (2, None)):
+        dy = torch.empty_like(Y)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        ops.bn_bwd(dout, Y, o, mode, mean, invstd, gamma, M, C, dy, None, dg, db,
+                   scale=scale, shift=shift)
+        res.append((dy, dg, db))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_layernorm_fwd_bwd():
     rows, D = 1000, 768
     x = (torch.randn(rows, D, device=DEV) * 3 + 1).float()
