@@ -14,6 +14,7 @@ constexpr int kCUs = 256;
 constexpr int kTM[NTILES] = {128, 256, 128, 256, 128, 128};
 constexpr int kTN[NTILES] = {128, 128, 256, 256, 128, 128};
 constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 2};  // workgroups per CU
+constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false};  // gemm_kernel kTail
 // Wave-quantisation cost model: a launch takes ceil(tiles * splits / 256) rounds (one 512-thread
 // workgroup per CU), each costing kRoundUs (prologue fill + epilogue) + k-steps * kStepUs.
 // Fitted on MI355X to tools/gemm_bench.py --sweep (ViT qkv K=768 vs fc2 K=3072 forward rows,
@@ -30,6 +31,7 @@ constexpr double kReduceLaunchUs = 2.0;
 constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2};
 int g_persistent = 1;       // dfu_gemm_set_persistent
 int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
+int g_tail_split = 1;       // dfu_gemm_set_tail_split
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
@@ -157,14 +159,77 @@ __global__ void k_splitk_reduce_scalar(const float* __restrict__ slab, int split
     }
 }
 
+// Tail split (GemmArgs::tail_*) for an unsplit launch of `tiles` tiles over `slots`
+// workgroup slots: the R = tiles mod slots tiles of the last, partial round are each split
+// S ways along K, S = as many as the idle slots allow (<= 8, >= 2 K-steps per split).
+struct Tail {
+  int full = 0, r = 0, s = 0, kps = 0;
+  int64_t bytes = 0;  // fp32 slab workspace
+};
+
+// The split count maximises the K-step time it takes off the tail round minus the slab hand-off,
+// which all the tail workgroups do at once at the end of the launch: each stores its fp32 tile
+// and the last of each tile reads them all back, ~2 x R x S x TM x TN x 4 bytes at ~5 TB/s, plus
+// ~3 us (fitted on MI355X with tools/gemm_step_profile.py --tail-ab: K >= ~2304 launches gain
+// 7-40 us, K <= 1024 ones would lose up to 11).  Used only if the net gain is positive.
+Tail tail_plan(int tiles, int slots, int ktiles, int tm, int tn, double step_us) {
+  Tail best;
+  if (!g_tail_split) return best;
+  const int R = tiles % slots;
+  if (R == 0) return best;
+  int smax = slots / R;
+  if (smax > 8) smax = 8;
+  if (smax > ktiles / 2) smax = ktiles / 2;
+  double best_gain = 0.0;
+  for (int S = 2; S <= smax; ++S) {
+    const int kps = cdiv(ktiles, S);
+    const int se = cdiv(ktiles, kps);
+    if (se != S) continue;
+    const double bytes = (double)R * S * tm * tn * 4;
+    const double gain = (ktiles - kps) * step_us - (3.0 + 2.0 * bytes / 5e6);
+    if (gain > best_gain) {
+      best_gain = gain;
+      best.s = S;
+      best.kps = kps;
+    }
+  }
+  if (best.s < 2) return Tail();
+  best.full = tiles - R;
+  best.r = R;
+  best.bytes = (int64_t)best.s * R * tm * tn * 4;
+  return best;
+}
+
+Tail tail_for(const dfu_gemm_desc* d, const Plan& pl) {
+  if (!pl.entry || d->epilogue == DFU_EPI_F32_ACC || !kTailOK[pl.tile]) return Tail();
+  const int tiles = cdiv(d->M, kTM[pl.tile]) * cdiv(d->N, kTN[pl.tile]);
+  return tail_plan(tiles, kCUs * kOcc[pl.tile], cdiv(d->K, BK), kTM[pl.tile], kTN[pl.tile],
+                   kStepUs[pl.tile]);
+}
+
 }  // namespace
 
 extern "C" int dfu_gemm_stats_tiles(int32_t M) { return (M + 127) / 128; }
 
 extern "C" int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* d) {
-  if (!d || d->epilogue != DFU_EPI_F32_ACC) return 0;
+  if (!d) return 0;
   const Plan pl = plan_gemm(d);
-  return pl.entry && pl.split > 1 ? (int64_t)pl.split * d->M * d->N * 4 : 0;
+  if (!pl.entry) return 0;
+  if (d->epilogue != DFU_EPI_F32_ACC) {
+    // tail-split slabs (at most one split per workgroup slot); a strided dgrad's phase launches
+    // re-plan their own tiles: the bound over every tile shape
+    if (!g_tail_split) return 0;
+    if (d->a_mode == DFU_OPND_CONV_DGRAD && d->conv_stride > 1) {
+      int64_t b = 0;
+      for (int t = 0; t < NTILES; ++t) {
+        const int64_t bt = kTailOK[t] ? (int64_t)kCUs * kOcc[t] * kTM[t] * kTN[t] * 4 : 0;
+        if (bt > b) b = bt;
+      }
+      return b;
+    }
+    return tail_for(d, pl).bytes;
+  }
+  return pl.split > 1 ? (int64_t)pl.split * d->M * d->N * 4 : 0;
 }
 
 extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* split_k) {
@@ -182,6 +247,12 @@ extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* spl
 extern "C" int dfu_gemm_set_persistent(int32_t enable) {
   const int old = g_persistent;
   g_persistent = enable != 0;
+  return old;
+}
+
+extern "C" int dfu_gemm_set_tail_split(int32_t enable) {
+  const int old = g_tail_split;
+  g_tail_split = enable != 0;
   return old;
 }
 
@@ -409,8 +480,19 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   // Persistent schedule: at most one wave of workgroups (CUs x occupancy), each walking its
   // work units as one K-step stream; split-K by fp32 atomics (no workspace) keeps one unit
   // per workgroup (its atomics have no fixed vmcnt count).
-  const int units = a.tiles_m * a.tiles_n * splits;
   const int slots = kCUs * kOcc[pl.tile];
+  a.tail_full = a.tail_r = a.tail_s = a.tail_kps = 0;
+  a.tslab = nullptr;
+  if (!acc_epi && splits == 1 && kTailOK[pl.tile]) {
+    const Tail t = tail_plan(a.tiles_m * a.tiles_n, slots, a.ktiles, TM, TN, kStepUs[pl.tile]);
+    if (t.r > 0 && d->workspace != nullptr && d->workspace_bytes >= t.bytes &&
+        d->tile_counters != nullptr && d->tile_counters_len >= t.r) {
+      a.tail_full = t.full; a.tail_r = t.r; a.tail_s = t.s; a.tail_kps = t.kps;
+      a.tslab = (float*)d->workspace;
+      a.counters = d->tile_counters;
+    }
+  }
+  const int units = a.tail_r ? a.tail_full + a.tail_r * a.tail_s : a.tiles_m * a.tiles_n * splits;
   const bool atomics = acc_epi && splits > 1 && a.slab == nullptr;
   const int nwg = (g_persistent && !atomics && units > slots) ? slots : units;
   hipLaunchKernelGGL(pl.entry->fn, dim3(nwg), dim3(pl.entry->threads), 0, s, a);

@@ -74,6 +74,13 @@ struct GemmArgs {
   float* slab;  // split-K partial slabs [split][M][N] (F32_ACC with a workspace)
   int* counters;  // per-tile arrival counters: in-kernel slab reduction (zero in, zero out)
   int split;    // K-splits; work units = tiles_m * tiles_n * split
+  // Tail split (tail_r > 0, split == 1): units [0, tail_full) are whole tiles; the tail_r tiles
+  // left over after the last complete round of workgroups are each split over tail_s
+  // workgroups along K (tail_kps K-steps each) instead of leaving most CUs idle for a whole
+  // round.  Each split stores its fp32 accumulators to tslab; the last to arrive on the tile's
+  // counter sums the slabs in split order and runs the normal epilogue.
+  int tail_full, tail_r, tail_s, tail_kps;
+  float* tslab;  // [tail_s][tail_r][FM*FN][threads] f32x4, lane-linear
   int n4;       // N and every leading dimension % 4 == 0: one vector access per 4 columns
   int n8;       // N, ldc (, ldaux_out) % 8 == 0 and 16-B aligned bf16 outputs: paired stores
   int ep_tokens;
@@ -577,6 +584,65 @@ DFU_DEV void splitk_finish(const GemmArgs& p, int m0, int n0, float* red, int ti
   }
 }
 
+// Tail-split hand-off (GemmArgs::tail_*): store this split's accumulators (write-through),
+// count the tile's arrivals, and in the last split to arrive replace acc by the sum of all the
+// tile's splits in split order (its own from registers: the same values it stored), so the
+// result does not depend on arrival order.  Returns whether this workgroup runs the epilogue.
+// Same publish protocol as splitk_finish (no workgroup waits for another).
+template <class T>
+DFU_DEV bool tail_reduce(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int v, float* red,
+                         int tid) {
+  constexpr int NF = T::FM * T::FN, NT = T::NT;
+  const int R = p.tail_r, S = p.tail_s;
+  const int s = v / R, r = v - s * R;
+  const rsrc_t rs = make_rsrc(p.tslab);
+  auto off = [&](int k, int f) { return (int)(((((int64_t)k * R + r) * NF + f) * NT + tid) * 16); };
+#pragma unroll
+  for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::FN; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                             off(s, i * T::FN + j), 0, 16);
+  int* flag = (int*)red;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.counters + r, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == S - 1;
+    if (last) __hip_atomic_store(p.counters + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (!*flag) return false;
+  // acc = slab 0 + slab 1 + ... in split order (this split's own slab re-read: the same
+  // values); two slabs' loads in flight per round trip (an odd count reads slab S-1 twice and
+  // adds it once: the out-of-range partner is clamped, not added).
+  for (int k = 0; k < S; k += 2) {
+    const int k1 = k + 1 < S ? k + 1 : k;
+    f32x4 x0[T::FM][T::FN], x1[T::FM][T::FN];
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::FN; ++j) {
+        x0[i][j] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off(k, i * T::FN + j), 0, 16));
+        x1[i][j] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off(k1, i * T::FN + j), 0, 16));
+      }
+#pragma unroll
+    for (int i = 0; i < T::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::FN; ++j) {
+        f32x4 a = k == 0 ? x0[i][j] : acc[i][j] + x0[i][j];
+        if (k1 != k) a = a + x1[i][j];
+        acc[i][j] = a;
+      }
+  }
+  return true;
+}
+
 // ------------------------------------------------------------------------------ epilogue
 // lane holds C[m = m0 + wr*WTM + 16i + (lane&15)][n = n0 + wc*WTN + 16j + 4*(lane>>4) + r]
 template <int AMODE, int EPI, class T>
@@ -776,8 +842,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   using T = Tile<TM, TN, OCC, NST, NW>;
   constexpr int WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
   constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
-  constexpr int SCRATCH =
-      EPI == DFU_EPI_BF16_STATS ? T::STATS_BYTES : EPI == DFU_EPI_F32_ACC ? 16 : 0;
+  constexpr int SCRATCH = EPI == DFU_EPI_BF16_STATS ? T::STATS_BYTES : 16;  // stats / flag
   // ALL LDS in one array: a second __shared__ object can make hipcc drain the DMA per K-step
   __shared__ __attribute__((aligned(16))) char smem[T::LDS_BYTES + SCRATCH];
   const int tid = threadIdx.x;
@@ -785,8 +850,12 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   const int wave = tid >> 6;
   const int wr = wave / WGN, wc = wave % WGN;
 
+  // Tail split (GemmArgs::tail_*) is built into the 8-wave 128x128 variants only (8 accumulator
+  // fragments per lane); in the larger ones its code costs register spills, and the host never
+  // requests it from them (gemm.hip kTailOK).
+  constexpr bool kTail = NW == 8 && FM * FN <= 8 && EPI != DFU_EPI_F32_ACC;
   const int tiles = p.tiles_m * p.tiles_n;
-  const int units = tiles * p.split;
+  const int units = kTail && p.tail_r ? p.tail_full + p.tail_r * p.tail_s : tiles * p.split;
   // Units by rounds: in round i workgroup b takes unit i*G + w(b).  In complete rounds w is
   // the XCD-aware bijective remap (blocks b and b+8 share an XCD): each XCD gets a contiguous
   // range of units, neighbours in the grouped raster below that share A and B panels in its
@@ -806,22 +875,34 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
 
   // unit u -> split s = u / tiles and tile t = u % tiles in a grouped raster (GROUP_M x
   // tiles_n bands walked column by column)
+  // (tail units: v = u - tail_full -> split v / tail_r of tail tile tail_full + v % tail_r)
   auto unit_geom = [&](int u, int& m0, int& n0, int& kb, int& nk) {
     constexpr int GROUP_M = 4;
-    const int s = u / tiles, t = u - s * tiles;
+    int s, t, kps;
+    if (kTail && p.tail_r && u >= p.tail_full) {
+      const int v = u - p.tail_full;
+      s = v / p.tail_r;
+      t = p.tail_full + (v - s * p.tail_r);
+      kps = p.tail_kps;
+    } else {
+      s = u / tiles;
+      t = u - s * tiles;
+      kps = p.kt_per_split;
+    }
     const int band = GROUP_M * p.tiles_n;
     const int g0 = (t / band) * GROUP_M;
     const int gm = min(GROUP_M, p.tiles_m - g0);
     const int within = t - (t / band) * band;
     m0 = (g0 + within % gm) * TM;
     n0 = (within / gm) * TN;
-    kb = s * p.kt_per_split;
-    nk = min(p.ktiles, kb + p.kt_per_split) - kb;
+    kb = s * kps;
+    nk = min(p.ktiles, kb + kps) - kb;
   };
   int total = 0;  // K-steps over all of this workgroup's units
   for (int i = 0; i < rounds; ++i) {
-    const int kb = (unit_at(i) / tiles) * p.kt_per_split;
-    total += min(p.ktiles, kb + p.kt_per_split) - kb;
+    int m0_, n0_, kb_, nk_;
+    unit_geom(unit_at(i), m0_, n0_, kb_, nk_);
+    total += nk_;
   }
 
   // issue cursor: the round / K-step the next DMA stage loads
@@ -925,7 +1006,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
     slot = slot == NSTAGE - 1 ? 0 : slot + 1;
     hist <<= 1;
     if (++ck == cnk) {
-      if (!(p.dbg & 1)) epilogue<AMODE, EPI, T>(p, acc, cm0, cn0, cu / tiles, red, tid);
+      // a tail split ends its workgroup's stream: hand off, and only the tile's last runs on
+      bool epi = true;
+      if constexpr (kTail)
+        if (p.tail_r && cu >= p.tail_full) epi = tail_reduce<T>(p, acc, cu - p.tail_full, red, tid);
+      if (epi && !(p.dbg & 1)) epilogue<AMODE, EPI, T>(p, acc, cm0, cn0, cu / tiles, red, tid);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

@@ -109,15 +109,14 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
         d.conv_n, d.conv_h, d.conv_w, d.conv_c = conv.n, conv.h, conv.w, conv.c
         d.conv_k, d.conv_r, d.conv_s = conv.k, conv.r, conv.s
         d.conv_stride, d.conv_pad, d.conv_p, d.conv_q = conv.stride, conv.pad, conv.p, conv.q
-    if epilogue == L.EPI_F32_ACC:
-        need = lib().dfu_gemm_workspace_bytes(ctypes.byref(d))
-        if need > 0:
-            if workspace is None or workspace.numel() * workspace.element_size() < need:
-                workspace = torch.empty(need, dtype=torch.uint8, device=C.device)
-            d.workspace = workspace.data_ptr()
-            d.workspace_bytes = int(need)
-            cnt = tile_counters(C.device)
-            d.tile_counters, d.tile_counters_len = cnt.data_ptr(), cnt.numel()
+    need = lib().dfu_gemm_workspace_bytes(ctypes.byref(d))  # split-K or tail-split slabs
+    if need > 0:
+        if workspace is None or workspace.numel() * workspace.element_size() < need:
+            workspace = torch.empty(need, dtype=torch.uint8, device=C.device)
+        d.workspace = workspace.data_ptr()
+        d.workspace_bytes = int(need)
+        cnt = tile_counters(C.device)
+        d.tile_counters, d.tile_counters_len = cnt.data_ptr(), cnt.numel()
     check(lib().dfu_gemm(ctypes.byref(d), stream_ptr()), "dfu_gemm")
     if gemm_record is not None:
         flops = 2.0 * M * N * K
@@ -140,6 +139,11 @@ def tile_counters(device):
     if t is None:
         t = _COUNTERS[key] = torch.zeros(TILE_COUNTERS, dtype=torch.int32, device=device)
     return t
+
+
+def gemm_set_tail_split(enable):
+    """Tail split of the last partial round of tiles along K (dfu_gemm_set_tail_split)."""
+    return int(lib().dfu_gemm_set_tail_split(int(bool(enable))))
 
 
 def gemm_set_inkernel_reduce(enable):

@@ -102,7 +102,8 @@ typedef struct dfu_gemm_desc {
 int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
 /* 128-row blocks (rows of the stats slab) produced by DFU_EPI_BF16_STATS for M rows. */
 int dfu_gemm_stats_tiles(int32_t M);
-/* Workspace bytes for deterministic split-K slabs of this descriptor (0 if not split). */
+/* Workspace bytes for this descriptor: deterministic split-K slabs (F32_ACC) or tail-split
+ * slabs (other epilogues); 0 if the launch needs none. */
 int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* desc);
 /* The tile (1..5, as dfu_gemm_desc.tile) and split-K the cost model picks for this descriptor. */
 int dfu_gemm_plan(const dfu_gemm_desc* desc, int32_t* tile, int32_t* split_k);
@@ -114,6 +115,12 @@ int dfu_gemm_set_persistent(int32_t enable);
  * counters, 0 (default: measured faster) = the separate reduce kernel.  Bitwise-identical; returns the
  * previous setting. */
 int dfu_gemm_set_inkernel_reduce(int32_t enable);
+/* Tail-split switch: 1 (default) = when the tiles of an unsplit launch leave a last, partial
+ * round of workgroups, split each of those tiles along K over the idle workgroups (fp32 slabs
+ * in the descriptor's workspace, dfu_gemm_workspace_bytes; the tile's last split to finish sums
+ * them in split order and runs the epilogue; needs tile_counters).  0 = off.  Deterministic
+ * either way (not bitwise equal to each other).  Returns the previous setting. */
+int dfu_gemm_set_tail_split(int32_t enable);
 /* Exact fp32 GEMM for the tiny fusion head (train_multimodal_fusion.py:305-313):
  * C[m][n] = accumulate*C[m][n] + sum_k A[m*sam + k*sak] * B[n*sbn + k*sbk] (+bias[n]) (relu). */
 int dfu_gemm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t sam, int64_t sak,

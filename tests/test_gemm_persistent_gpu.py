@@ -198,3 +198,108 @@ def test_gemm_splitk_inkernel_bitwise(M, N, K, split, tile):
     assert int(ops.tile_counters(C0.device).abs().sum().item()) == 0
     ref = C0 + Akm.float()[:, :M].t() @ Bkn.float()[:, :N]
     assert (res[0][0] - ref).abs().max().item() < 3e-3 * math.sqrt(K)
+
+
+def both_tail(run):
+    """[outputs with the tail split, the same again, outputs without it]."""
+    res = []
+    for tail in (1, 1, 0):
+        old = ops.gemm_set_tail_split(tail)
+        try:
+            res.append([t.clone() for t in run()])
+        finally:
+            ops.gemm_set_tail_split(old)
+    torch.cuda.synchronize()
+    return res
+
+
+@pytest.mark.parametrize("tile", [0, 1, 5])
+@pytest.mark.parametrize("M,N,K,epi", [(12608, 768, 3072, "bf16"), (12608, 768, 2304, "resid"),
+                                       (3136, 512, 2048, "stats"), (1000, 300, 4096, "dgelu"),
+                                       (6001, 200, 2560, "gelu")])
+def test_gemm_tail_split(M, N, K, epi, tile):
+    """Tail split (the last partial round's tiles split along K, the last split to arrive sums
+    the fp32 slabs in split order and runs the epilogue): deterministic run to run, equal to the
+    unsplit launch up to fp32 summation order, the tile counters left zeroed."""
+    n8 = (N + 7) // 8 * 8
+    A = drnd(M, K, seed=31)
+    B = drnd(N, K, seed=32)
+    Bkn = drnd(K, n8, seed=33)
+    bias = drnd(N, dtype=torch.float32, seed=34)
+    h16 = drnd(M, N, seed=35)
+    r32 = drnd(M, N, dtype=torch.float32, seed=36)
+
+    def run():
+        if epi == "bf16":
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16, bias=bias, tile=tile)
+            return [C]
+        if epi == "resid":
+            C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_F32_RESID, bias=bias, aux=r32,
+                   ldaux=N, tile=tile)
+            return [C]
+        if epi == "stats":
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            st = torch.empty(ops.stats_tiles(M), 2, N, device=DEV)
+            gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_STATS, stats=st, tile=tile)
+            return [C, st]
+        if epi == "dgelu":
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            gemm_t(M, N, K, A, K, Bkn, n8, C, N, b_mode=L.OPND_MNMAJOR,
+                   epilogue=L.EPI_BF16_DGELU, aux=h16, ldaux=N, tile=tile)
+            return [C]
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        pre = torch.empty_like(C)
+        gemm_t(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_GELU, bias=bias, aux_out=pre,
+               ldaux_out=N, tile=tile)
+        return [C, pre]
+
+    e = {"bf16": L.EPI_BF16, "resid": L.EPI_F32_RESID, "stats": L.EPI_BF16_STATS,
+         "dgelu": L.EPI_BF16_DGELU, "gelu": L.EPI_BF16_GELU}[epi]
+    bm = L.OPND_MNMAJOR if epi == "dgelu" else L.OPND_KMAJOR
+    if tile:  # (the automatic plan may pick a tile without a tail round)
+        assert ops.gemm_workspace_bytes(M, N, K, L.OPND_KMAJOR, bm, e, tile=tile) > 0, "no tail"
+    on, again, off = both_tail(run)
+    for a, b in zip(on, again):
+        assert torch.equal(a, b), f"tail split not deterministic ({epi} {M}x{N}x{K} tile {tile})"
+    for a, b in zip(on, off):
+        a, b = a.float(), b.float()
+        tol = 2e-2 if a.dtype == torch.bfloat16 or epi in ("bf16", "dgelu", "gelu", "stats") else 1e-3
+        assert ((a - b).abs() <= tol * (1 + b.abs())).all(), (a - b).abs().max().item()
+    assert int(ops.tile_counters(A.device).abs().sum().item()) == 0
+    if epi == "bf16":
+        ref = A.float() @ B.float().t() + bias
+        err = (on[0].float() - ref).abs()
+        assert (err <= 3e-2 + 1e-2 * ref.abs()).all(), err.max().item()
+
+
+@pytest.mark.parametrize("case", [(64, 7, 7, 512, 512, 3, 3, 1, 1),
+                                  (64, 28, 28, 128, 128, 3, 3, 2, 1)])
+def test_conv_tail_split(case):
+    """Implicit-GEMM conv fwd (STATS) and strided dgrad (per-phase launches) with and without
+    the tail split."""
+    Nb, H, W, C, K, R, S, st, pad = case
+    g = ops.ConvGeom(Nb, H, W, C, K, R, S, st, pad)
+    x = drnd(Nb * H * W, C, seed=41)
+    w = drnd(K, R * S * C, seed=42, scale=0.05)
+    M = Nb * g.p * g.q
+    dy = drnd(M, K, seed=43)
+
+    def run():
+        y = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+        stt = torch.empty(ops.stats_tiles(M), 2, K, device=DEV)
+        ops.gemm(M, K, R * S * C, x, 0, w, R * S * C, y, K, a_mode=L.OPND_CONV_FWD,
+                 epilogue=L.EPI_BF16_STATS, stats=stt, conv=g)
+        dx = torch.empty(Nb * H * W, C, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(Nb * H * W, C, R * S * K, dy, 0, w, R * S * C, dx, C, a_mode=L.OPND_CONV_DGRAD,
+                 b_mode=L.OPND_CONV_DGRAD_W, epilogue=L.EPI_BF16, conv=g)
+        return [y, stt, dx]
+
+    on, again, off = both_tail(run)
+    for a, b in zip(on, again):
+        assert torch.equal(a, b)
+    for a, b in zip(on, off):
+        a, b = a.float(), b.float()
+        assert ((a - b).abs() <= 2e-2 * (1 + b.abs())).all(), (a - b).abs().max().item()
+    assert int(ops.tile_counters(x.device).abs().sum().item()) == 0

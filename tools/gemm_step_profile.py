@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--config", default="fusion")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--ab", action="store_true", help="also time the one-shot schedule")
+    ap.add_argument("--tail-ab", action="store_true",
+                    help="also time without the tail split (in the '1shot' column)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(42)
@@ -77,6 +79,12 @@ def main():
                 us1 = time_desc(d, a.iters)
             finally:
                 ops.gemm_set_persistent(old)
+        elif a.tail_ab:
+            old = ops.gemm_set_tail_split(0)
+            try:
+                us1 = time_desc(d, a.iters)
+            finally:
+                ops.gemm_set_tail_split(old)
         t, sk = ctypes.c_int32(), ctypes.c_int32()
         ops.check(ops.lib().dfu_gemm_plan(ctypes.byref(d), ctypes.byref(t), ctypes.byref(sk)), "plan")
         rows.append((n * us, n, us, us1, flops, nbytes, d, t.value, sk.value))
