@@ -47,8 +47,8 @@ DFU_DEV bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
 // Copy rows [0, NPAD) of one (b, h) slice of qkv (which = 0 q, 1 k, 2 v) or of a [B*N][H][64]
 // tensor into an r128 LDS image; rows >= N are zero.
 DFU_DEV void stage_rows(char* lds, const bf16_t* base, int64_t row_stride, int N, int NPAD,
-                        int tid) {
-  for (int idx = tid; idx < NPAD * 8; idx += 256) {
+                        int tid, int nthr = 256) {
+  for (int idx = tid; idx < NPAD * 8; idx += nthr) {
     const int row = idx >> 3, chunk = idx & 7;
     u32x4 v = {0u, 0u, 0u, 0u};
     if (row < N) v = *(const u32x4*)(base + (int64_t)row * row_stride + chunk * 8);
@@ -56,12 +56,46 @@ DFU_DEV void stage_rows(char* lds, const bf16_t* base, int64_t row_stride, int N
   }
 }
 
+// Two images at once (e.g. K and V), every load of the thread issued before any LDS write: one
+// memory round trip for the whole staging (a load-then-write loop pays one per iteration).
+template <int NPAD, int NTHR>
+DFU_DEV void stage_rows2(char* lds0, const bf16_t* base0, char* lds1, const bf16_t* base1,
+                         int64_t row_stride, int N, int tid) {
+  // branch-free: padding rows load row N-1 (in bounds) and are zeroed at the LDS write, so the
+  // loads are not split into exec-masked blocks that each wait for their own data
+  constexpr int IT = (NPAD * 8 + NTHR - 1) / NTHR;
+  u32x4 v0[IT], v1[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int idx = tid + i * NTHR, row = idx >> 3, chunk = idx & 7;
+    const int64_t o = (int64_t)(row < N ? row : N - 1) * row_stride + chunk * 8;
+    v0[i] = *(const u32x4*)(base0 + o);
+    v1[i] = *(const u32x4*)(base1 + o);
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int idx = tid + i * NTHR, row = idx >> 3, chunk = idx & 7;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    if (idx < NPAD * 8) {
+      *(u32x4*)(lds0 + r128_off(row, chunk)) = row < N ? v0[i] : z;
+      *(u32x4*)(lds1 + r128_off(row, chunk)) = row < N ? v1[i] : z;
+    }
+  }
+}
+
 constexpr float LOG2E = 1.4426950408889634f;
 
-template <int KT>
-__global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ qkv, int N, int H,
-                                                  float scale, bf16_t* __restrict__ o,
-                                                  float* __restrict__ lse) {
+// 2^x by the bare v_exp_f32 (softmax arguments are <= 0 and only need ~1 ulp; below 2^-126 the
+// hardware result flushes to 0, which a probability that small may).  exp2f would wrap it in
+// range-reduction code (cmp, cndmask, ldexp) that made the attention kernels VALU-bound.
+DFU_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// NW waves share the (b, h) slice: 13 query tiles of 16 at N = 197, at most 2 per wave with 8
+// (the LDS images allow 2 workgroups per CU, so waves, not workgroups, carry the parallelism).
+template <int KT, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__ qkv, int N, int H,
+                                                      float scale, bf16_t* __restrict__ o,
+                                                      float* __restrict__ lse) {
   constexpr int NPAD = KT * 16;
   __shared__ __attribute__((aligned(16))) char smem[2 * NPAD * 128];
   char* Ks = smem;
@@ -70,20 +104,28 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ qkv
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int64_t tok_stride = (int64_t)3 * H * 64;
   const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
-  stage_rows(Ks, qbase + H * 64, tok_stride, N, NPAD, tid);
-  stage_rows(Vs, qbase + 2 * H * 64, tok_stride, N, NPAD, tid);
+  const int QT = (N + 15) / 16;
+  // this wave's query fragments, one tile ahead: the first tile's load overlaps the K/V staging,
+  // each next tile's overlaps the current tile's math
+  auto load_q = [&](int qt, u32x4 (&v)[2]) {
+    const int q = qt * 16 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      v[ks] = (u32x4){0u, 0u, 0u, 0u};
+      if (qt < QT && q < N) v[ks] = *(const u32x4*)(qbase + (int64_t)q * tok_stride + 32 * ks + 8 * g);
+    }
+  };
+  u32x4 qnext[2];
+  load_q(wave, qnext);
+  stage_rows2<NPAD, 64 * NW>(Ks, qbase + H * 64, Vs, qbase + 2 * H * 64, tok_stride, N, tid);
   __syncthreads();
   const float c = scale * LOG2E;
-  const int QT = (N + 15) / 16;
-  for (int qt = wave; qt < QT; qt += 4) {
+  for (int qt = wave; qt < QT; qt += NW) {
     const int q = qt * 16 + (lane & 15);
     bf16x8 qf[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (q < N) v = *(const u32x4*)(qbase + (int64_t)q * tok_stride + 32 * ks + 8 * g);
-      qf[ks] = __builtin_bit_cast(bf16x8, v);
-    }
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, qnext[ks]);
+    load_q(qt + NW, qnext);
     f32x4 s[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
@@ -95,13 +137,15 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ qkv
     // lane holds S[q][key = 16t + 4g + r]
     float mx = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < KT; ++t)
+    for (int t = 0; t < KT; ++t) {
+      if (16 * t + 15 >= N) {  // (wave-uniform) only the last key tiles hold padding keys
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = 16 * t + 4 * g + r;
-        if (key >= N) s[t][r] = -INFINITY;
-        mx = fmaxf(mx, s[t][r]);
+        for (int r = 0; r < 4; ++r)
+          if (16 * t + 4 * g + r >= N) s[t][r] = -INFINITY;
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[t][r]);
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float l = 0.f;
@@ -109,7 +153,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const bf16_t* __restrict__ qkv
     for (int t = 0; t < KT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f((s[t][r] - mx) * c);
+        const float pv = fast_exp2(fmaf(s[t][r], c, -mx * c));
         s[t][r] = pv;
         l += pv;
       }
@@ -156,8 +200,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const bf16_t* __restrict__ 
   const int64_t o_stride = (int64_t)H * 64;
   const bf16_t* obase = o + (int64_t)b * N * o_stride + h * 64;
   const bf16_t* dobase = dout + (int64_t)b * N * o_stride + h * 64;
-  stage_rows(Ks, qbase + H * 64, tok_stride, N, NPAD, tid);
-  stage_rows(Vs, qbase + 2 * H * 64, tok_stride, N, NPAD, tid);
+  stage_rows2<NPAD, 256>(Ks, qbase + H * 64, Vs, qbase + 2 * H * 64, tok_stride, N, tid);
   __syncthreads();
   const float c = scale * LOG2E;
   const int QT = (N + 15) / 16;
@@ -198,7 +241,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const bf16_t* __restrict__ 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = 16 * t + 4 * g + r;
-        const float pv = (qv && key < N) ? exp2f(st[r] * c - lq) : 0.f;
+        const float pv = (qv && key < N) ? fast_exp2(fmaf(st[r], c, -lq)) : 0.f;
         st[r] = pv * (dp[r] - dsum);
       }
       s[t] = st;
@@ -287,7 +330,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(const bf16_t* __restrict__
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = 16 * qt + 4 * g + r;
-          const float pv = (kv && q < N) ? exp2f(st[r] * c - Ls[q]) : 0.f;
+          const float pv = (kv && q < N) ? fast_exp2(fmaf(st[r], c, -Ls[q])) : 0.f;
           ph[hh][r] = pv;
           dsh[hh][r] = pv * (dp[r] - Es[q]);
         }
@@ -339,17 +382,28 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
   const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
   const bf16_t* obase = o + (int64_t)b * N * o_stride + h * 64;
   const bf16_t* dobase = dout + (int64_t)b * N * o_stride + h * 64;
-  for (int idx = tid; idx < NPAD * 8; idx += NTH) {
-    const int row = idx >> 3, chunk = idx & 7;
-    u32x4 vq = {0u, 0u, 0u, 0u}, vk = vq, vv = vq, vd = vq, vo = vq;
-    if (row < N) {
-      const bf16_t* t = qbase + (int64_t)row * tok_stride + chunk * 8;
-      vq = *(const u32x4*)t;
-      vk = *(const u32x4*)(t + H * 64);
-      vv = *(const u32x4*)(t + 2 * H * 64);
-      vd = *(const u32x4*)(dobase + (int64_t)row * o_stride + chunk * 8);
-      vo = *(const u32x4*)(obase + (int64_t)row * o_stride + chunk * 8);
-    }
+  // all of a thread's staging loads (IT iterations x 5 tensors) issued before any is used
+  constexpr int IT = (NPAD * 8 + NTH - 1) / NTH;
+  u32x4 pq[IT], pk[IT], pv[IT], pd[IT], po[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {  // branch-free as stage_rows2: padding rows load row N-1
+    const int idx = tid + i * NTH, row = idx >> 3, chunk = idx & 7;
+    const int rr = row < N ? row : N - 1;
+    const bf16_t* t = qbase + (int64_t)rr * tok_stride + chunk * 8;
+    pq[i] = *(const u32x4*)t;
+    pk[i] = *(const u32x4*)(t + H * 64);
+    pv[i] = *(const u32x4*)(t + 2 * H * 64);
+    pd[i] = *(const u32x4*)(dobase + (int64_t)rr * o_stride + chunk * 8);
+    po[i] = *(const u32x4*)(obase + (int64_t)rr * o_stride + chunk * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int idx = tid + i * NTH, row = idx >> 3, chunk = idx & 7;
+    if (idx >= NPAD * 8) break;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    const bool in = row < N;
+    const u32x4 vq = in ? pq[i] : z, vk = in ? pk[i] : z, vv = in ? pv[i] : z,
+                vd = in ? pd[i] : z, vo = in ? po[i] : z;
     const int off = r128_off(row, chunk);
     *(u32x4*)(Qs + off) = vq;
     *(u32x4*)(Ks + off) = vk;
@@ -396,7 +450,7 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = 16 * t + 4 * g + r;
-          const float pv = (qv && key < N) ? exp2f(st[r] * c - lq) : 0.f;
+          const float pv = (qv && key < N) ? fast_exp2(fmaf(st[r], c, -lq)) : 0.f;
           st[r] = pv * (dp[r] - dsum);
         }
         s[t] = st;
@@ -449,7 +503,7 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int q = 16 * qt + 4 * g + r;
-            const float pv = (kv && q < N) ? exp2f(st[r] * c - Ls[q]) : 0.f;
+            const float pv = (kv && q < N) ? fast_exp2(fmaf(st[r], c, -Ls[q])) : 0.f;
             ph[hh][r] = pv;
             dsh[hh][r] = pv * (dp[r] - Es[q]);
           }
@@ -500,7 +554,7 @@ extern "C" int dfu_attention_fwd(const void* qkv, int32_t B, int32_t N, int32_t 
   DFU_CHECK_ARG(N > 0 && N <= 256, "dfu_attention_fwd: N=%d unsupported (<= 256)", N);
   const int KT = dfu_attention_npad(N) / 16;
   hipStream_t s = (hipStream_t)stream;
-#define CALL(K) hipLaunchKernelGGL(k_attn_fwd<K>, dim3(B * H), dim3(256), 0, s, (const bf16_t*)qkv, N, H, scale, (bf16_t*)o, lse)
+#define CALL(K) hipLaunchKernelGGL(k_attn_fwd<K>, dim3(B * H), dim3(512), 0, s, (const bf16_t*)qkv, N, H, scale, (bf16_t*)o, lse)
   DISPATCH_KT(KT, CALL)
 #undef CALL
   DFU_LAUNCH_CHECK();

@@ -8,7 +8,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdfu_hip.so")
+# DFU_HIP_LIB: another build of the library (A/B timing of two builds); default: in-tree
+LIB_PATH = os.environ.get("DFU_HIP_LIB") or os.path.join(_HERE, "libdfu_hip.so")
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "dfu_hip.h"))
 
 c_int32 = ctypes.c_int32
