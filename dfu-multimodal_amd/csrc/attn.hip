@@ -418,9 +418,12 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
     d += __shfl_xor(d, 1, 64);  // the 8 chunks of a row are 8 consecutive lanes
     d += __shfl_xor(d, 2, 64);
     d += __shfl_xor(d, 4, 64);
+    // padding queries get LSE = +inf: every probability of theirs is exp2(-inf) = 0, so no
+    // element needs a query mask below; padding keys need none either (their K, V rows are 0,
+    // so they add nothing to dQ, and their own dK / dV rows are never stored)
     if (chunk == 0) {
       Es[row] = row < N ? d : 0.f;
-      Ls[row] = row < N ? lse[(int64_t)bh * NPAD + row] * LOG2E : 0.f;
+      Ls[row] = row < N ? lse[(int64_t)bh * NPAD + row] * LOG2E : INFINITY;
     }
   }
   __syncthreads();
@@ -448,11 +451,7 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
           dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Vs, 16 * t, ks, lane), df[ks], dp, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = 16 * t + 4 * g + r;
-          const float pv = (qv && key < N) ? fast_exp2(fmaf(st[r], c, -lq)) : 0.f;
-          st[r] = pv * (dp[r] - dsum);
-        }
+        for (int r = 0; r < 4; ++r) st[r] = fast_exp2(fmaf(st[r], c, -lq)) * (dp[r] - dsum);
         s[t] = st;
       }
       f32x4 acc[4];
@@ -503,7 +502,7 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int q = 16 * qt + 4 * g + r;
-            const float pv = (kv && q < N) ? fast_exp2(fmaf(st[r], c, -Ls[q])) : 0.f;
+            const float pv = fast_exp2(fmaf(st[r], c, -Ls[q]));
             ph[hh][r] = pv;
             dsh[hh][r] = pv * (dp[r] - Es[q]);
           }
