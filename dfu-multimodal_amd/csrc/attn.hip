@@ -135,28 +135,36 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
         s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * t, ks, lane), qf[ks], s[t], 0, 0, 0);
     }
     // lane holds S[q][key = 16t + 4g + r]
+    // padding keys: NPAD rounds N up to a multiple of 32, so only the last two key tiles (a
+    // compile-time set) can hold them
     float mx = -INFINITY;
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      if (16 * t + 15 >= N) {  // (wave-uniform) only the last key tiles hold padding keys
+      if (t >= KT - 2) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (16 * t + 4 * g + r >= N) s[t][r] = -INFINITY;
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[t][r]);
+      mx = fmaxf(mx, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float l = 0.f;
+    // exponent arguments and the row sum on packed pairs (v_pk_fma_f32 / v_pk_add_f32)
+    const f32x2 c2 = {c, c}, b2 = {-mx * c, -mx * c};
+    f32x2 l2 = {0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < KT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = fast_exp2(fmaf(s[t][r], c, -mx * c));
-        s[t][r] = pv;
-        l += pv;
+      for (int r = 0; r < 4; r += 2) {
+        f32x2 a = {s[t][r], s[t][r + 1]};
+        a = a * c2 + b2;
+        a[0] = fast_exp2(a[0]);
+        a[1] = fast_exp2(a[1]);
+        s[t][r] = a[0];
+        s[t][r + 1] = a[1];
+        l2 += a;
       }
+    float l = l2[0] + l2[1];
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     f32x4 acc[4];

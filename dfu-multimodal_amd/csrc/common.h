@@ -13,6 +13,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 #define DFU_DEV __device__ __forceinline__
 
@@ -24,8 +25,11 @@ DFU_DEV bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// Two floats -> two bf16 (RNE) in one v_cvt_pk_bf16_f32 (the per-element casts cost a convert
+// per value plus a shift and an or).
 DFU_DEV uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2_t));
 }
 DFU_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 DFU_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
