@@ -48,6 +48,8 @@ def time_desc(d, iters, ws):
         ws = torch.empty(need, dtype=torch.uint8, device="cuda")
     d.workspace = ws.data_ptr() if need > 0 else None
     d.workspace_bytes = int(need)
+    cnt = ops.tile_counters(torch.device("cuda", 0))  # split-K / tail-split hand-off counters
+    d.tile_counters, d.tile_counters_len = cnt.data_ptr(), cnt.numel()
     s = ops.stream_ptr()
     for _ in range(2):
         ops.check(lib.dfu_gemm(ctypes.byref(d), s), "dfu_gemm")
@@ -68,6 +70,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "dfu-multimodal_amd", "csrc",
                                                   "gemm_tuned.inc"))
     ap.add_argument("--append", action="store_true", help="keep entries already in --out")
+    ap.add_argument("--dump", default=None,
+                    help="also write every timing (shape -> {tile/split: us}) to this JSON")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(42)
@@ -89,6 +93,7 @@ def main():
     print(f"{len(rec)} launches, {len(uniq)} distinct GEMMs", flush=True)
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
     lines, t_auto_sum, t_best_sum = [], 0.0, 0.0
+    dump = {}
     t0 = time.time()
     for k, (d0, flops, refs, cnt) in uniq.items():
         n = len(cnt)
@@ -106,6 +111,7 @@ def main():
                     t, ws = time_desc(d, a.iters, ws)
                 except L.DfuError:
                     break  # tile not instantiated for this combination
+                dump.setdefault(",".join(map(str, k)), {"n": n, "t": {}})["t"][f"{tile}/{sk}"] = t
                 if t < best[0]:
                     best = (t, tile, sk)
         t_auto_sum += n * t_auto
@@ -138,6 +144,10 @@ def main():
         for ln in keep + lines:
             f.write(ln + "\n")
     print(f"wrote {len(keep) + len(lines)} entries to {a.out}")
+    if a.dump:
+        import json
+        with open(a.dump, "w") as f:
+            json.dump(dump, f)
 
 
 if __name__ == "__main__":
