@@ -381,10 +381,12 @@ def test_pooling_and_layout():
     close(dx4, (g / 49)[:, None, :].expand(B, 49, 2048), atol=1e-3, rtol=1e-2, what="avgpool bwd")
     # stem im2col and patchify vs unfold
     xi = torch.randn(2, 3, 224, 224, device=DEV)
-    col, P, Q = ops.im2col_f32(xi, 7, 7, 2, 3, 160)
-    ref = F.unfold(xi, 7, padding=3, stride=2).transpose(1, 2).reshape(-1, 147)
-    close(col[:, :147], ref, atol=2e-2, rtol=1e-2, what="im2col")
-    assert col[:, 147:].abs().max().item() == 0
+    for xin in (xi, xi.contiguous(memory_format=torch.channels_last),
+                torch.randn(3, 3, 57, 61, device=DEV)):
+        col, P, Q = ops.im2col_f32(xin, 7, 7, 2, 3, 160)
+        ref = F.unfold(xin, 7, padding=3, stride=2).transpose(1, 2).reshape(-1, 147)
+        assert torch.equal(col[:, :147].float(), ref.to(torch.bfloat16).float()), "im2col"
+        assert col[:, 147:].abs().max().item() == 0
     pt = ops.patchify_f32(xi, 16)
     ref = F.unfold(xi, 16, stride=16).transpose(1, 2).reshape(-1, 768)
     close(pt, ref, atol=2e-2, rtol=1e-2, what="patchify")
