@@ -1,0 +1,228 @@
+// 256x256 phased GEMM for K-contiguous A and B (the ViT forward linears): the K-step is split
+// into four phases, each {one barrier; this phase's fragment reads; one half-tile of the NEXT
+// K-step's LDS-DMA; a 16-MFMA cluster}, so LDS reads, DMA issue and MFMAs interleave at a fine
+// grain instead of one burst each per K-step (cdna_hip_programming.md "The 256² 8-phase
+// template": the per-phase interleave is the lever).
+//
+// Geometry: 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns rows {h*128 + wr*64 + 0..63 : h = 0,1}
+// and columns {h*128 + wc*32 + 0..31 : h = 0,1}, i.e. one quarter of each operand HALF-tile
+// (A rows 0-127 / 128-255, B columns 0-127 / 128-255).  Phase q computes the quadrant
+// (A half, B half) = (top, left), (top, right), (bottom, right), (bottom, left): every wave reads
+// the same half-tiles in the same phase, so each phase waits only for the half-tile(s) it
+// reads.  The next K-step's half-tiles are issued in phases 1-4 in the order of first use (A-top,
+// B-left, B-right, A-bottom) into the other of two LDS buffers (2 x 64 KiB).
+//   RAW: phase 1 needs A-top + B-left (younger: 2 half-tiles = 4 DMA per thread -> vmcnt(4)),
+//        phase 2 B-right (younger: A-bottom + next A-top -> 4), phase 3 A-bottom (younger: next
+//        A-top + B-left -> 4), phase 4 reads B-left again (retired at phase 1).  Each wave waits
+//        for its own DMA, then the phase barrier publishes everyone's.
+//   WAR: a half-tile of the other buffer is re-filled at least one barrier after its last read
+//        (A-top: read phase 1, re-filled next phase 1; B-left 4 -> 2; B-right 2 -> 3;
+//        A-bottom 3 -> 4), and reads are retired (lgkmcnt(0)) before each MFMA cluster.
+// One workgroup per CU; workgroups walk tiles (grouped raster, XCD-aware) one at a time.
+// Epilogues: BF16 (+bias), BF16_GELU (pre-activation to aux_out), F32_RESID.
+#include "gemm_table.h"
+
+namespace dfu {
+namespace {
+
+constexpr int P8_IMG = 256 * 128;     // one operand image: 256 rows x 64 k x 2 B
+constexpr int P8_BUF = 2 * P8_IMG;    // A + B
+constexpr int P8_LDS = 2 * P8_BUF;    // two buffers: 128 KiB
+
+// One half-tile (128 rows x 64 k) of a K-contiguous operand into rows 128h.. of `img`: two
+// wave-instructions per thread; piece q = wave + 8i covers image rows 128h + 8q .. +7.
+DFU_DEV void p8_issue_half(const bf16_t* base, int64_t ld, int row0, int rows, int k0, int K,
+                           int h, char* img, int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+  const int c = kc_lane_chunk(lane);
+  const bool kin = k0 + c * 8 < K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave + 8 * i;
+    const int r = 128 * h + 8 * q + (lane >> 3);
+    const int g = row0 + r;
+    const bool ok = kin && g < rows;
+    glds16(ok ? (const void*)(base + (int64_t)g * ld + k0 + c * 8) : (const void*)g_zero16,
+           img + h * 16384 + q * 1024);
+  }
+}
+
+template <int EPI>
+DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc,
+                         int lane) {
+  const bool n4 = p.n4 != 0;
+  const int M = p.M, N = p.N;
+  const rsrc_t rc = make_rsrc(p.C);
+  const rsrc_t ra = make_rsrc(p.aux);
+  const rsrc_t ro = make_rsrc(p.aux_out);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + 4 * (lane >> 4);
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[r] = n + r < N ? p.bias[n + r] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + (i >> 2) * 128 + wr * 64 + (i & 3) * 16 + (lane & 15);
+      const bool okm = m < M;
+      const int64_t mc = okm ? m : 0;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha + bias[r];
+      if constexpr (EPI == DFU_EPI_BF16) {
+        st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
+      } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
+        float g[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g[r] = gelu_f(v[r]);
+        st4_bf16(ro, mc * p.ldaux_out + n, okm, n, N, n4, v);
+        st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, g);
+      } else {  // DFU_EPI_F32_RESID
+        float x[4];
+        ld4_f32(ra, mc * p.ldaux + n, okm, n, N, n4, x);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += x[r];
+        st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v);
+      }
+    }
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[P8_LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  int wg = bid;
+  if (nwg >= 16) {  // bijective XCD-aware remap: blocks b and b+8 share an XCD
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int nk = p.ktiles;
+  for (int t = wg; t < tiles; t += nwg) {
+    constexpr int GROUP_M = 4;
+    const int band = GROUP_M * p.tiles_n;
+    const int g0 = (t / band) * GROUP_M;
+    const int gm = min(GROUP_M, p.tiles_m - g0);
+    const int within = t - (t / band) * band;
+    const int m0 = (g0 + within % gm) * 256, n0 = (within / gm) * 256;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    // the previous tile's last reads of buffer 0 must be done before its prologue refills it
+    __builtin_amdgcn_s_barrier();
+    // prologue: K-step 0 into buffer 0, in first-use order (A-top, B-left, B-right, A-bottom)
+    p8_issue_half(p.A, p.lda, m0, p.M, 0, p.K, 0, smem, tid);
+    p8_issue_half(p.B, p.ldb, n0, p.N, 0, p.K, 0, smem + P8_IMG, tid);
+    p8_issue_half(p.B, p.ldb, n0, p.N, 0, p.K, 1, smem + P8_IMG, tid);
+    p8_issue_half(p.A, p.lda, m0, p.M, 0, p.K, 1, smem, tid);
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* la = smem + (kt & 1) * P8_BUF;
+      const char* lb = la + P8_IMG;
+      char* na = smem + ((kt & 1) ^ 1) * P8_BUF;
+      char* nb = na + P8_IMG;
+      const bool nxt = kt + 1 < nk;
+      const int k1 = (kt + 1) * BK;
+      bf16x8 fa[4][2], fb[2][2];
+      auto read_a = [&](int h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            fa[i][ks] = read_frag<true>(la, h * 128 + wr * 64 + i * 16, ks, lane);
+      };
+      auto read_b = [&](int h) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            fb[j][ks] = read_frag<true>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
+      };
+      auto mfma = [&](int ha, int hb) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  fb[j][ks], fa[i][ks], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+#if DFU_P8_FINE
+      // phase 1: A-top x B-left; next A-top
+      wait_vmcnt<4>();
+      __builtin_amdgcn_s_barrier();
+      read_a(0);
+      read_b(0);
+      if (nxt) p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 0, na, tid);
+      mfma(0, 0);
+      // phase 2: A-top x B-right; next B-left
+      if (nxt) wait_vmcnt<4>(); else wait_vmcnt<2>();
+      __builtin_amdgcn_s_barrier();
+      read_b(1);
+      if (nxt) p8_issue_half(p.B, p.ldb, n0, p.N, k1, p.K, 0, nb, tid);
+      mfma(0, 1);
+      // phase 3: A-bottom x B-right; next B-right
+      if (nxt) wait_vmcnt<4>(); else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      read_a(1);
+      if (nxt) p8_issue_half(p.B, p.ldb, n0, p.N, k1, p.K, 1, nb, tid);
+      mfma(1, 1);
+      // phase 4: A-bottom x B-left; next A-bottom
+      __builtin_amdgcn_s_barrier();
+      read_b(0);
+      if (nxt) p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 1, na, tid);
+      mfma(1, 0);
+#else
+      // one barrier per K-step (all of this K-step's half-tiles landed and published); the next
+      // K-step's DMA goes out in phases 1 and 2, leaving phases 3-4 of MFMAs to cover it; waves
+      // drift freely through phases 2-4 (no LDS hazard inside a K-step)
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      read_a(0);
+      read_b(0);
+      if (nxt) {
+        p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 0, na, tid);
+        p8_issue_half(p.B, p.ldb, n0, p.N, k1, p.K, 0, nb, tid);
+      }
+      mfma(0, 0);
+      read_b(1);
+      if (nxt) {
+        p8_issue_half(p.B, p.ldb, n0, p.N, k1, p.K, 1, nb, tid);
+        p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 1, na, tid);
+      }
+      mfma(0, 1);
+      read_a(1);
+      mfma(1, 1);
+      read_b(0);
+      mfma(1, 0);
+#endif
+    }
+    p8_epilogue<EPI>(p, acc, m0, n0, wr, wc, lane);
+  }
+}
+
+}  // namespace
+
+#define P8(E) {DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, E, T256x256p8, &gemm_p8<E>, P8_LDS, 512}
+const Entry kTable256x256p8[] = {
+    P8(DFU_EPI_BF16),
+    P8(DFU_EPI_BF16_GELU),
+    P8(DFU_EPI_F32_RESID),
+};
+#undef P8
+const int kTable256x256p8N = sizeof(kTable256x256p8) / sizeof(Entry);
+
+}  // namespace dfu

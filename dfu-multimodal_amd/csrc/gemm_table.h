@@ -12,7 +12,8 @@ struct Entry {
 };
 enum TileId {
   T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, T128x128o2 = 4, T128x128w4 = 5,
-  NTILES = 6
+  T256x256p8 = 6,  // phased 256x256 (gemm_p8.hip): K-contiguous A and B only
+  NTILES = 7
 };
 extern const Entry kTable128x128[];
 extern const int kTable128x128N;
@@ -26,6 +27,8 @@ extern const Entry kTable128x128o2[];
 extern const int kTable128x128o2N;
 extern const Entry kTable128x128w4[];
 extern const int kTable128x128w4N;
+extern const Entry kTable256x256p8[];
+extern const int kTable256x256p8N;
 }  // namespace dfu
 
 #define DFU_ENTRY(A, B, E, TMv, TNv, TID)                                             \

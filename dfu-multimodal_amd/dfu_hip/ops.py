@@ -47,7 +47,8 @@ class ConvGeom:
         self.q = (w + 2 * pad - s) // stride + 1
 
 
-TILES = {"auto": 0, "128x128": 1, "256x128": 2, "128x256": 3, "256x256": 4, "128x128o2": 5, "128x128w4": 6}
+TILES = {"auto": 0, "128x128": 1, "256x128": 2, "128x256": 3, "256x256": 4, "128x128o2": 5,
+         "128x128w4": 6, "256x256p8": 7}
 
 # Optional recording of GEMM launches (bench.py's roofline): when set to a list, every
 # dfu_gemm call appends (descriptor, algorithmic flops, tensors it touches) — the tensor

@@ -103,7 +103,7 @@ def main():
         best = (t_auto, 0, 0)
         ktiles = (d0.K + 63) // 64
         splits = [s for s in SPLITS if s <= ktiles] if d0.epilogue == L.EPI_F32_ACC else [1]
-        for tile in range(1, 7):
+        for tile in range(1, 8):
             for sk in splits:
                 d = copy_desc(d0)
                 d.tile, d.split_k = tile, sk
