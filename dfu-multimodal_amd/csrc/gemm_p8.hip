@@ -1,4 +1,4 @@
-// 256x256 phased GEMM for K-contiguous A and B (the ViT forward linears): the K-step is split
+// 256x256 phased GEMM for a K-contiguous A (the ViT linears, forward and dgrad): the K-step is split
 // into four phases, each {one barrier; this phase's fragment reads; one half-tile of the NEXT
 // K-step's LDS-DMA; a 16-MFMA cluster}, so LDS reads, DMA issue and MFMAs interleave at a fine
 // grain instead of one burst each per K-step (cdna_hip_programming.md "The 256² 8-phase
@@ -19,7 +19,9 @@
 //        (A-top: read phase 1, re-filled next phase 1; B-left 4 -> 2; B-right 2 -> 3;
 //        A-bottom 3 -> 4), and reads are retired (lgkmcnt(0)) before each MFMA cluster.
 // One workgroup per CU; workgroups walk tiles (grouped raster, XCD-aware) one at a time.
-// Epilogues: BF16 (+bias), BF16_GELU (pre-activation to aux_out), F32_RESID.
+// B K-contiguous (forward) or MN-major (dgrad: tr16 fragment reads of 128-column sub-images).
+// Epilogues: BF16 (+bias), BF16_GELU (pre-activation to aux_out), F32_RESID; dgrad: BF16,
+// BF16_DGELU, BF16_ADD.
 #include "gemm_table.h"
 
 namespace dfu {
@@ -44,6 +46,22 @@ DFU_DEV void p8_issue_half(const bf16_t* base, int64_t ld, int row0, int rows, i
     const bool ok = kin && g < rows;
     glds16(ok ? (const void*)(base + (int64_t)g * ld + k0 + c * 8) : (const void*)g_zero16,
            img + h * 16384 + q * 1024);
+  }
+}
+
+// One half-tile (64 k x 128 columns = one 16 KiB MN-contiguous sub-image) of an MN-major
+// operand X[k][mn] into sub-image h of `img`: the layout of gemm_kernel.h's MN images (piece q
+// = k-rows 4q .. 4q+3, lane chunk swizzled by the k-row), two wave-instructions per thread.
+DFU_DEV void p8_issue_half_mn(const bf16_t* base, int64_t ld, int col0, int col_bound, int k0,
+                              int K, int h, char* img, int tid) {
+  const int wave = tid >> 6;
+  const int col = col0 + 128 * h + 8 * mn_lane_chunk(tid);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int k = k0 + (tid >> 4) + 32 * i;
+    const bool ok = col < col_bound && k < K;
+    glds16(ok ? (const void*)(base + (int64_t)k * ld + col) : (const void*)g_zero16,
+           img + 16384 * h + 8192 * i + 1024 * wave);
   }
 }
 
@@ -78,6 +96,13 @@ DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
         for (int r = 0; r < 4; ++r) g[r] = gelu_f(v[r]);
         st4_bf16(ro, mc * p.ldaux_out + n, okm, n, N, n4, v);
         st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, g);
+      } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
+        float x[4];
+        ld4_bf16(ra, mc * p.ldaux + n, okm, n, N, n4, x);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[r] = EPI == DFU_EPI_BF16_DGELU ? v[r] * gelu_grad_f(x[r]) : v[r] + x[r];
+        st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
       } else {  // DFU_EPI_F32_RESID
         float x[4];
         ld4_f32(ra, mc * p.ldaux + n, okm, n, N, n4, x);
@@ -89,8 +114,15 @@ DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
   }
 }
 
-template <int EPI>
+template <int BMODE, int EPI>
 __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
+  constexpr bool BK_ = BMODE == DFU_OPND_KMAJOR;  // B K-contiguous (else MN-major: dgrad)
+  auto issue_b = [&](int n0_, int k0_, int h, char* img) {
+    if constexpr (BK_)
+      p8_issue_half(p.B, p.ldb, n0_, p.N, k0_, p.K, h, img, threadIdx.x);
+    else
+      p8_issue_half_mn(p.B, p.ldb, n0_, p.n_ld_bound, k0_, p.K, h, img, threadIdx.x);
+  };
   __shared__ __attribute__((aligned(16))) char smem[P8_LDS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
@@ -120,8 +152,8 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
     __builtin_amdgcn_s_barrier();
     // prologue: K-step 0 into buffer 0, in first-use order (A-top, B-left, B-right, A-bottom)
     p8_issue_half(p.A, p.lda, m0, p.M, 0, p.K, 0, smem, tid);
-    p8_issue_half(p.B, p.ldb, n0, p.N, 0, p.K, 0, smem + P8_IMG, tid);
-    p8_issue_half(p.B, p.ldb, n0, p.N, 0, p.K, 1, smem + P8_IMG, tid);
+    issue_b(n0, 0, 0, smem + P8_IMG);
+    issue_b(n0, 0, 1, smem + P8_IMG);
     p8_issue_half(p.A, p.lda, m0, p.M, 0, p.K, 1, smem, tid);
 
     for (int kt = 0; kt < nk; ++kt) {
@@ -144,7 +176,7 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
-            fb[j][ks] = read_frag<true>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
+            fb[j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
       };
       auto mfma = [&](int ha, int hb) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -172,13 +204,13 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
       if (nxt) wait_vmcnt<4>(); else wait_vmcnt<2>();
       __builtin_amdgcn_s_barrier();
       read_b(1);
-      if (nxt) p8_issue_half(p.B, p.ldb, n0, p.N, k1, p.K, 0, nb, tid);
+      if (nxt) issue_b(n0, k1, 0, nb);
       mfma(0, 1);
       // phase 3: A-bottom x B-right; next B-right
       if (nxt) wait_vmcnt<4>(); else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       read_a(1);
-      if (nxt) p8_issue_half(p.B, p.ldb, n0, p.N, k1, p.K, 1, nb, tid);
+      if (nxt) issue_b(n0, k1, 1, nb);
       mfma(1, 1);
       // phase 4: A-bottom x B-left; next A-bottom
       __builtin_amdgcn_s_barrier();
@@ -195,12 +227,12 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
       read_b(0);
       if (nxt) {
         p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 0, na, tid);
-        p8_issue_half(p.B, p.ldb, n0, p.N, k1, p.K, 0, nb, tid);
+        issue_b(n0, k1, 0, nb);
       }
       mfma(0, 0);
       read_b(1);
       if (nxt) {
-        p8_issue_half(p.B, p.ldb, n0, p.N, k1, p.K, 1, nb, tid);
+        issue_b(n0, k1, 1, nb);
         p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 1, na, tid);
       }
       mfma(0, 1);
@@ -216,11 +248,14 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
 
 }  // namespace
 
-#define P8(E) {DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, E, T256x256p8, &gemm_p8<E>, P8_LDS, 512}
+#define P8(B, E) {DFU_OPND_KMAJOR, B, E, T256x256p8, &gemm_p8<B, E>, P8_LDS, 512}
 const Entry kTable256x256p8[] = {
-    P8(DFU_EPI_BF16),
-    P8(DFU_EPI_BF16_GELU),
-    P8(DFU_EPI_F32_RESID),
+    P8(DFU_OPND_KMAJOR, DFU_EPI_BF16),
+    P8(DFU_OPND_KMAJOR, DFU_EPI_BF16_GELU),
+    P8(DFU_OPND_KMAJOR, DFU_EPI_F32_RESID),
+    P8(DFU_OPND_MNMAJOR, DFU_EPI_BF16),
+    P8(DFU_OPND_MNMAJOR, DFU_EPI_BF16_DGELU),
+    P8(DFU_OPND_MNMAJOR, DFU_EPI_BF16_ADD),
 };
 #undef P8
 const int kTable256x256p8N = sizeof(kTable256x256p8) / sizeof(Entry);

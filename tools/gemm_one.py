@@ -40,6 +40,11 @@ def build(case, tile):
         A, B, C, h = T(M, K), T(K, N), T(M, N), T(M, N)
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, N, C, N, b_mode=L.OPND_MNMAJOR,
                                                epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N, tile=tile)
+    if case in ("fc1_dgrad", "qkv_dgrad"):
+        M, N, K = {"fc1_dgrad": (12608, 768, 3072), "qkv_dgrad": (12608, 768, 2304)}[case]
+        A, B, C = T(M, K), T(K, N), T(M, N)
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, N, C, N, b_mode=L.OPND_MNMAJOR,
+                                               epilogue=L.EPI_BF16, tile=tile)
     if case == "fc1_wgrad":
         M, N, K = 3072, 768, 12608
         A, B = T(K, M), T(K, N)
