@@ -17,7 +17,7 @@ import json
 import re
 
 CATS = [
-    ("GEMM (MFMA template)", r"gemm_kernel<"),
+    ("GEMM (MFMA template)", r"gemm_kernel<|gemm_p8<"),
     ("GEMM split-K reduce", r"k_splitk_reduce"),
     ("fp32 head GEMM", r"k_gemm_f32"),
     ("BatchNorm", r"k_bn_"),
@@ -30,6 +30,11 @@ CATS = [
     ("elementwise / loss", r"k_relu|k_dropout|k_ce_|k_argmax|k_advance"),
     ("memset / copy (runtime)", r"__amd_rocclr|fillBuffer|copyBuffer"),
 ]
+
+
+def is_gemm(name):
+    """The MFMA GEMM template's kernels: gemm_kernel<...> and the phased gemm_p8<...>."""
+    return "gemm_kernel<" in name or "gemm_p8<" in name
 
 
 def short(name):
@@ -52,6 +57,9 @@ EPI = ["BF16", "BF16_RELU", "BF16_GELU", "F32", "F32_RESID", "BF16_DGELU", "BF16
 
 
 def gemm_label(name):
+    m8 = re.search(r"gemm_p8<(\d+), (\d+)>", name)
+    if m8:
+        return f"gemm KM x {OPND[int(m8.group(1))]} -> {EPI[int(m8.group(2))]} 256x256 phased"
     m = re.search(r"gemm_kernel<(\d+), (\d+), (\d+), (\d+), (\d+)(?:, (\d+))?(?:, \d+)?>", name)
     if not m:
         return short(name)
@@ -84,7 +92,7 @@ def main():
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.stats)))
     S = a.steps
-    gemm_calls = sum(int(r["Calls"]) for r in rows if "gemm_kernel<" in r["Name"])
+    gemm_calls = sum(int(r["Calls"]) for r in rows if is_gemm(r["Name"]))
     GS = S  # steps' worth of GEMM launches (the roofline replays add launches)
     if a.bench:
         b = json.loads(open(a.bench).read().strip().splitlines()[-1])
@@ -92,7 +100,7 @@ def main():
 
     def per_step(r):
         n = r["Name"]
-        return GS if ("gemm_kernel<" in n or "k_splitk_reduce" in n) else S
+        return GS if (is_gemm(n) or "k_splitk_reduce" in n) else S
     total = sum(float(r["TotalDurationNs"]) / 1e6 / per_step(r) for r in rows)
     print(f"# {a.title}\n")
     print("Kernel durations are summed per step; the encoders run on two streams, so the sum "
@@ -113,8 +121,8 @@ def main():
     print("## Per category (ms per step)\n\n| category | ms/step | share |\n|---|---:|---:|")
     for c, v in sorted(cats.items(), key=lambda kv: -kv[1]):
         print(f"| {c} | {v:.3f} | {100 * v / total:.1f}% |")
-    g = [r for r in rows if "gemm_kernel<" in r["Name"] or "k_splitk_reduce" in r["Name"]]
-    gl = [r for r in g if "gemm_kernel<" in r["Name"]]
+    g = [r for r in rows if is_gemm(r["Name"]) or "k_splitk_reduce" in r["Name"]]
+    gl = [r for r in g if is_gemm(r["Name"])]
     g_ns = sum(float(r["TotalDurationNs"]) for r in g)
     g_calls = sum(int(r["Calls"]) for r in gl)
     per_launch_us = g_ns / 1e3 / g_calls
@@ -124,8 +132,8 @@ def main():
     if a.fetch and a.write:
         fetch, fn = pmc_by_kernel(a.fetch, "FETCH_SIZE")
         write, wn = pmc_by_kernel(a.write, "WRITE_SIZE")
-        gk = [k for k in fetch if "gemm_kernel<" in k or "k_splitk_reduce" in k]
-        launches = sum(fn[k] for k in gk if "gemm_kernel<" in k)
+        gk = [k for k in fetch if is_gemm(k) or "k_splitk_reduce" in k]
+        launches = sum(fn[k] for k in gk if is_gemm(k))
         fb = sum(fetch[k] for k in gk) * 1024 * 2 / launches  # gfx950: FETCH_SIZE = 1/2 of 16-B streams
         wb = sum(write.get(k, 0.0) for k in gk) * 1024 / launches
         print(f"HBM traffic of the GEMM family (PMC, separate --pmc FETCH_SIZE and --pmc WRITE_SIZE "
