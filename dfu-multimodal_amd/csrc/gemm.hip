@@ -439,8 +439,12 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   // in-kernel split-K reduction: the last split of a tile to finish adds the slabs into C
   a.counters = nullptr;
   if (a.slab != nullptr && g_inkernel_reduce && splits <= 8 && d->tile_counters != nullptr &&
-      d->tile_counters_len >= a.tiles_m * a.tiles_n)
+      d->tile_counters_len >= a.tiles_m * a.tiles_n && pl.tile != T256x256p8)
     a.counters = d->tile_counters;
+  // the phased kernel has neither fp32 atomics nor the in-kernel reduction: split-K needs slabs
+  DFU_CHECK_ARG(!(pl.tile == T256x256p8 && acc_epi && splits > 1 && a.slab == nullptr),
+                "dfu_gemm: split-K on the phased 256x256 tile needs a workspace "
+                "(dfu_gemm_workspace_bytes)");
   a.ep_tokens = d->ep_tokens;
   a.cn = d->conv_n; a.ch = d->conv_h; a.cw = d->conv_w; a.cc = d->conv_c;
   a.ck = d->conv_k; a.cr = d->conv_r; a.cs = d->conv_s;

@@ -1,4 +1,4 @@
-// 256x256 phased GEMM for a K-contiguous A (the ViT linears, forward and dgrad): the K-step is split
+// 256x256 phased GEMM (the ViT linears: forward, dgrad and wgrad): the K-step is split
 // into four phases, each {one barrier; this phase's fragment reads; one half-tile of the NEXT
 // K-step's LDS-DMA; a 16-MFMA cluster}, so LDS reads, DMA issue and MFMAs interleave at a fine
 // grain instead of one burst each per K-step (cdna_hip_programming.md "The 256² 8-phase
@@ -19,7 +19,8 @@
 //        (A-top: read phase 1, re-filled next phase 1; B-left 4 -> 2; B-right 2 -> 3;
 //        A-bottom 3 -> 4), and reads are retired (lgkmcnt(0)) before each MFMA cluster.
 // One workgroup per CU; workgroups walk tiles (grouped raster, XCD-aware) one at a time.
-// B K-contiguous (forward) or MN-major (dgrad: tr16 fragment reads of 128-column sub-images).
+// A and B K-contiguous (forward), B MN-major (dgrad), or both MN-major (wgrad, split-K units
+// into fp32 slabs) -- MN-major halves are 128-column tr16 sub-images.
 // Epilogues: BF16 (+bias), BF16_GELU (pre-activation to aux_out), F32_RESID; dgrad: BF16,
 // BF16_DGELU, BF16_ADD.
 #include "gemm_table.h"
@@ -67,7 +68,7 @@ DFU_DEV void p8_issue_half_mn(const bf16_t* base, int64_t ld, int col0, int col_
 
 template <int EPI>
 DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc,
-                         int lane) {
+                         int lane, int sidx) {
   const bool n4 = p.n4 != 0;
   const int M = p.M, N = p.N;
   const rsrc_t rc = make_rsrc(p.C);
@@ -103,6 +104,16 @@ DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
         for (int r = 0; r < 4; ++r)
           v[r] = EPI == DFU_EPI_BF16_DGELU ? v[r] * gelu_grad_f(x[r]) : v[r] + x[r];
         st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
+      } else if constexpr (EPI == DFU_EPI_F32_ACC) {  // split-K slab, or C += acc unsplit
+        if (p.slab != nullptr) {
+          st4_f32(make_rsrc(p.slab), ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v);
+        } else {
+          float c[4];
+          ld4_f32(rc, mc * p.ldc + n, okm, n, N, n4, c);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += c[r];
+          st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v);
+        }
       } else {  // DFU_EPI_F32_RESID
         float x[4];
         ld4_f32(ra, mc * p.ldaux + n, okm, n, N, n4, x);
@@ -114,9 +125,16 @@ DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
   }
 }
 
-template <int BMODE, int EPI>
+template <int AMODE, int BMODE, int EPI>
 __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
-  constexpr bool BK_ = BMODE == DFU_OPND_KMAJOR;  // B K-contiguous (else MN-major: dgrad)
+  constexpr bool AK_ = AMODE == DFU_OPND_KMAJOR;  // A K-contiguous (else MN-major: wgrad)
+  constexpr bool BK_ = BMODE == DFU_OPND_KMAJOR;  // B K-contiguous (else MN-major: dgrad, wgrad)
+  auto issue_a = [&](int m0_, int k0_, int h, char* img) {
+    if constexpr (AK_)
+      p8_issue_half(p.A, p.lda, m0_, p.M, k0_, p.K, h, img, threadIdx.x);
+    else
+      p8_issue_half_mn(p.A, p.lda, m0_, p.m_ld_bound, k0_, p.K, h, img, threadIdx.x);
+  };
   auto issue_b = [&](int n0_, int k0_, int h, char* img) {
     if constexpr (BK_)
       p8_issue_half(p.B, p.ldb, n0_, p.N, k0_, p.K, h, img, threadIdx.x);
@@ -133,8 +151,13 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int nk = p.ktiles;
-  for (int t = wg; t < tiles; t += nwg) {
+  // work units: tile x K-split (split s covers K-steps [s*kps, (s+1)*kps) and stores an fp32
+  // slab for the reduce kernel; F32_ACC only)
+  const int units = tiles * p.split;
+  for (int u = wg; u < units; u += nwg) {
+    const int sidx = u / tiles, t = u - sidx * tiles;
+    const int kb = sidx * p.kt_per_split;
+    const int nk = min(p.ktiles, kb + p.kt_per_split) - kb;
     constexpr int GROUP_M = 4;
     const int band = GROUP_M * p.tiles_n;
     const int g0 = (t / band) * GROUP_M;
@@ -151,10 +174,10 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
     // the previous tile's last reads of buffer 0 must be done before its prologue refills it
     __builtin_amdgcn_s_barrier();
     // prologue: K-step 0 into buffer 0, in first-use order (A-top, B-left, B-right, A-bottom)
-    p8_issue_half(p.A, p.lda, m0, p.M, 0, p.K, 0, smem, tid);
-    issue_b(n0, 0, 0, smem + P8_IMG);
-    issue_b(n0, 0, 1, smem + P8_IMG);
-    p8_issue_half(p.A, p.lda, m0, p.M, 0, p.K, 1, smem, tid);
+    issue_a(m0, kb * BK, 0, smem);
+    issue_b(n0, kb * BK, 0, smem + P8_IMG);
+    issue_b(n0, kb * BK, 1, smem + P8_IMG);
+    issue_a(m0, kb * BK, 1, smem);
 
     for (int kt = 0; kt < nk; ++kt) {
       const char* la = smem + (kt & 1) * P8_BUF;
@@ -162,14 +185,14 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
       char* na = smem + ((kt & 1) ^ 1) * P8_BUF;
       char* nb = na + P8_IMG;
       const bool nxt = kt + 1 < nk;
-      const int k1 = (kt + 1) * BK;
+      const int k1 = (kb + kt + 1) * BK;
       bf16x8 fa[4][2], fb[2][2];
       auto read_a = [&](int h) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
-            fa[i][ks] = read_frag<true>(la, h * 128 + wr * 64 + i * 16, ks, lane);
+            fa[i][ks] = read_frag<AK_>(la, h * 128 + wr * 64 + i * 16, ks, lane);
       };
       auto read_b = [&](int h) {
 #pragma unroll
@@ -198,7 +221,7 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
       __builtin_amdgcn_s_barrier();
       read_a(0);
       read_b(0);
-      if (nxt) p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 0, na, tid);
+      if (nxt) issue_a(m0, k1, 0, na);
       mfma(0, 0);
       // phase 2: A-top x B-right; next B-left
       if (nxt) wait_vmcnt<4>(); else wait_vmcnt<2>();
@@ -215,7 +238,7 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
       // phase 4: A-bottom x B-left; next A-bottom
       __builtin_amdgcn_s_barrier();
       read_b(0);
-      if (nxt) p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 1, na, tid);
+      if (nxt) issue_a(m0, k1, 1, na);
       mfma(1, 0);
 #else
       // one barrier per K-step (all of this K-step's half-tiles landed and published); the next
@@ -226,14 +249,14 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
       read_a(0);
       read_b(0);
       if (nxt) {
-        p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 0, na, tid);
+        issue_a(m0, k1, 0, na);
         issue_b(n0, k1, 0, nb);
       }
       mfma(0, 0);
       read_b(1);
       if (nxt) {
         issue_b(n0, k1, 1, nb);
-        p8_issue_half(p.A, p.lda, m0, p.M, k1, p.K, 1, na, tid);
+        issue_a(m0, k1, 1, na);
       }
       mfma(0, 1);
       read_a(1);
@@ -242,20 +265,21 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
       mfma(1, 0);
 #endif
     }
-    p8_epilogue<EPI>(p, acc, m0, n0, wr, wc, lane);
+    p8_epilogue<EPI>(p, acc, m0, n0, wr, wc, lane, sidx);
   }
 }
 
 }  // namespace
 
-#define P8(B, E) {DFU_OPND_KMAJOR, B, E, T256x256p8, &gemm_p8<B, E>, P8_LDS, 512}
+#define P8(A, B, E) {A, B, E, T256x256p8, &gemm_p8<A, B, E>, P8_LDS, 512}
 const Entry kTable256x256p8[] = {
-    P8(DFU_OPND_KMAJOR, DFU_EPI_BF16),
-    P8(DFU_OPND_KMAJOR, DFU_EPI_BF16_GELU),
-    P8(DFU_OPND_KMAJOR, DFU_EPI_F32_RESID),
-    P8(DFU_OPND_MNMAJOR, DFU_EPI_BF16),
-    P8(DFU_OPND_MNMAJOR, DFU_EPI_BF16_DGELU),
-    P8(DFU_OPND_MNMAJOR, DFU_EPI_BF16_ADD),
+    P8(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
+    P8(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_GELU),
+    P8(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_RESID),
+    P8(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16),
+    P8(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_DGELU),
+    P8(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_ADD),
+    P8(DFU_OPND_MNMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_F32_ACC),  // weight gradients (split-K slabs)
 };
 #undef P8
 const int kTable256x256p8N = sizeof(kTable256x256p8) / sizeof(Entry);
