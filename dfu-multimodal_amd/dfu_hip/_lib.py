@@ -119,6 +119,10 @@ PROTOTYPES = {
     "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P],
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
+    "dfu_resize_ksize": [I32, I32],
+    "dfu_resize_coeffs": [I32, I32, P, P],
+    "dfu_resize_batch": [P, P, P, I32, I32, I32, P, P, P],
+    "dfu_augment_normalize": [P, P, I32, I32, I32, P, P, P, P, P],
 }
 _RESTYPE = {"dfu_last_error_string": c_char_p, "dfu_gemm_workspace_bytes": c_int64,
             "dfu_gemm_f32_workspace_bytes": c_int64}

@@ -319,6 +319,52 @@ int dfu_step_increment(int64_t* step_dev, void* stream);
 /* argmax over C for each row (torch.max(outputs, 1), :384) -> int64. */
 int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t* out, void* stream);
 
+/* ---------------------------------------------------------------- input pipeline ---- */
+/* The torchvision transforms of train_multimodal_fusion.py:172-205 on a decoded batch,
+ * bit-exact with torchvision's PIL backend (replaces the DataLoader workers' per-sample
+ * transform calls, :270-275 and MultimodalDataset.__getitem__ :151-165; decode stays PIL). */
+typedef struct dfu_resize_desc {
+  int64_t src_off;  /* byte offset of the image in the packed source (H x W x 3 u8) */
+  int64_t tmp_off;  /* byte offset of its horizontal-pass rows (h x out_w x 3) in the scratch */
+  int64_t coef_off; /* int32 offset of its taps: [out_w][2] bounds, [out_w][ksh] weights,
+                       [out_h][2] bounds, [out_h][ksv] weights (dfu_resize_coeffs) */
+  int32_t w, h;     /* source size */
+  int32_t ksh, ksv; /* tap counts of the two passes (dfu_resize_ksize) */
+} dfu_resize_desc;
+
+enum dfu_aug_op { DFU_AUG_BRIGHTNESS = 0, DFU_AUG_CONTRAST = 1, DFU_AUG_SATURATION = 2 };
+
+/* Per-image random parameters, drawn on the host in torchvision's order.  rot / aff are PIL's
+ * 16.16 fixed-point inverse maps (Geometry.c affine_fixed): a0 a1 a2' a3 a4 a5' with the
+ * half-pixel terms folded into a2' / a5'. */
+typedef struct dfu_aug_params {
+  int32_t hflip, vflip;
+  int32_t rotate;
+  int32_t rot[6];
+  int32_t affine;
+  int32_t aff[6];
+  int32_t n_ops;     /* ColorJitter ops applied, in order (RandomApply may give 0) */
+  int32_t op[3];     /* enum dfu_aug_op */
+  float factor[3];   /* ImageEnhance factors of op[k] */
+} dfu_aug_params;
+
+/* Host-only (no GPU): taps of one bilinear antialiased resize pass (PIL Resample.c
+ * precompute_coeffs + normalize_coeffs_8bpc).  ksize = dfu_resize_ksize(in, out);
+ * bounds [out][2] = (first source index, count), kk [out][ksize] 22-bit fixed point. */
+int dfu_resize_ksize(int32_t in_size, int32_t out_size);
+int dfu_resize_coeffs(int32_t in_size, int32_t out_size, int32_t* bounds, int32_t* kk);
+/* Resize n packed images to out_h x out_w (HWC u8): tmp holds sum_i h_i*out_w*3 bytes,
+ * dst n*out_h*out_w*3.  descs and coefs are device arrays. */
+int dfu_resize_batch(const uint8_t* src, const dfu_resize_desc* descs, const int32_t* coefs,
+                     int32_t n, int32_t out_w, int32_t out_h, uint8_t* tmp, uint8_t* dst,
+                     void* stream);
+/* Flips, rotation, colour jitter, affine, ToTensor and Normalize on n resized H x W x 3 u8
+ * images -> out fp32 [n][3][H][W].  params and contrast_means (n int32 scratch) are device
+ * arrays; mean3 / std3 are host arrays of 3 floats. */
+int dfu_augment_normalize(const uint8_t* img, const dfu_aug_params* params, int32_t n,
+                          int32_t H, int32_t W, const float* mean3, const float* std3,
+                          int32_t* contrast_means, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
