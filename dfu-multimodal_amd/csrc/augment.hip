@@ -33,7 +33,9 @@ DFU_DEV int clip8(int s) {
   return v < 0 ? 0 : (v > 255 ? 255 : v);
 }
 
-// Horizontal pass: tmp[img][y][x] for every source row y, out width OW.
+// Horizontal pass: tmp[img][y][x] for every source row y, out width OW; one thread per output
+// pixel, the source bytes through L1/L2 (a wave-per-row LDS-staged variant measured 1.6x
+// slower: its load and compute phases do not overlap at the occupancy its LDS allows).
 __global__ void k_resize_h(const uint8_t* __restrict__ src, const dfu_resize_desc* __restrict__ d,
                            const int32_t* __restrict__ coefs, int OW, uint8_t* __restrict__ tmp) {
   const dfu_resize_desc D = d[blockIdx.y];
@@ -150,30 +152,25 @@ DFU_DEV int contrast_slot(const dfu_aug_params& P) {
   return -1;
 }
 
-// ImageEnhance.Contrast: int(mean(L) + 0.5) of the image entering the contrast op; one block
-// per image.  sum <= 255 * H * W fits int32 for H * W < 8.4M.
-__global__ void __launch_bounds__(1024) k_augment_stats(const uint8_t* __restrict__ img,
-                                                        const dfu_aug_params* __restrict__ params,
-                                                        int H, int W, int32_t* __restrict__ means) {
-  const dfu_aug_params P = params[blockIdx.x];
+// ImageEnhance.Contrast needs int(mean(L) + 0.5) of the image entering the contrast op:
+// kStatBlocks blocks per image add their grey sums into sums[img] (integer atomics: the
+// order does not matter).  sum <= 255 * H * W fits int32 for H * W < 8.4M.
+constexpr int kStatBlocks = 8;
+
+__global__ void __launch_bounds__(256) k_augment_stats(const uint8_t* __restrict__ img,
+                                                       const dfu_aug_params* __restrict__ params,
+                                                       int H, int W, int32_t* __restrict__ sums) {
+  const dfu_aug_params P = params[blockIdx.y];
   const int slot = contrast_slot(P);
   if (slot < 0) return;
-  const uint8_t* im = img + (int64_t)blockIdx.x * H * W * 3;
+  const uint8_t* im = img + (int64_t)blockIdx.y * H * W * 3;
   int s = 0;
-  for (int i = threadIdx.x; i < H * W; i += blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < H * W; i += gridDim.x * blockDim.x) {
     const Px p = colour(rotated(im, P, W, H, i % W, i / W), P, slot, 0);
     s += grey(p);
   }
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  __shared__ int part[16];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t t = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
-    const int64_t n = (int64_t)H * W;
-    means[blockIdx.x] = (int32_t)((2 * t + n) / (2 * n));  // == int(t / n + 0.5)
-  }
+  if ((threadIdx.x & 63) == 0) atomicAdd(sums + blockIdx.y, s);
 }
 
 __global__ void k_augment_apply(const uint8_t* __restrict__ img,
@@ -182,8 +179,9 @@ __global__ void k_augment_apply(const uint8_t* __restrict__ img,
                                 float m2, float s0, float s1, float s2, float* __restrict__ out) {
   const dfu_aug_params P = params[blockIdx.y];
   const uint8_t* im = img + (int64_t)blockIdx.y * H * W * 3;
-  const int mean = contrast_slot(P) >= 0 ? means[blockIdx.y] : 0;
   const int n = H * W;
+  // == int(sum / n + 0.5), ImageStat's mean rounded as ImageEnhance.Contrast does
+  const int mean = contrast_slot(P) >= 0 ? (int)((2 * (int64_t)means[blockIdx.y] + n) / (2 * (int64_t)n)) : 0;
   float* o = out + (int64_t)blockIdx.y * 3 * n;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int x = i % W, y = i / W;
@@ -262,8 +260,10 @@ extern "C" int dfu_augment_normalize(const uint8_t* img, const dfu_aug_params* p
   DFU_CHECK_ARG(img && params && mean3 && std3 && contrast_means && out && n > 0 && H > 0 &&
                     W > 0 && (int64_t)H * W * 255 < (1ll << 31),
                 "dfu_augment_normalize: bad args");
-  hipLaunchKernelGGL(k_augment_stats, dim3(n), dim3(1024), 0, (hipStream_t)stream, img, params,
-                     H, W, contrast_means);
+  hipError_t e = hipMemsetAsync(contrast_means, 0, sizeof(int32_t) * n, (hipStream_t)stream);
+  DFU_CHECK_ARG(e == hipSuccess, "dfu_augment_normalize: memset: %s", hipGetErrorString(e));
+  hipLaunchKernelGGL(k_augment_stats, dim3(kStatBlocks, n), dim3(256), 0, (hipStream_t)stream,
+                     img, params, H, W, contrast_means);
   DFU_LAUNCH_CHECK();
   const int gx = (H * W + TPB - 1) / TPB;
   hipLaunchKernelGGL(k_augment_apply, dim3(gx < 64 ? gx : 64, n), dim3(TPB), 0,

@@ -220,12 +220,16 @@ class GpuPreprocessor:
         self._std = (ctypes.c_float * 3)(*spec.std)
 
     def __call__(self, images, params=None):
-        lib = L.load()
+        return self.run(self.stage(images, params))
+
+    def stage(self, images, params=None):
+        """Host side of one batch: pack descriptors, parameters, resize taps and pixels into one
+        pinned buffer and start its single H2D copy on the current stream."""
         spec = self.spec
         OH, OW = spec.size
         n = len(images)
         if n == 0:
-            return torch.empty((0, 3, OH, OW), dtype=torch.float32, device=self.device)
+            return _Staged(None, 0, 0, 0, 0, 0)
         if params is None:
             params = [AugParams() for _ in range(n)]
         if len(params) != n:
@@ -250,9 +254,8 @@ class GpuPreprocessor:
         o_par = _align(desc.nbytes)
         o_coef = o_par + _align(rec.nbytes)
         o_src = o_coef + _align(coef_len * 4)
-        total = o_src + src_len
-        pin = self.device.type == "cuda"
-        stage = torch.empty(total, dtype=torch.uint8, pin_memory=pin)
+        total = o_src + src_len + 4  # the resize reads whole dwords of the last row
+        stage = torch.empty(total, dtype=torch.uint8, pin_memory=self.device.type == "cuda")
         buf = stage.numpy()
         buf[:desc.nbytes] = desc.view(np.uint8)
         buf[o_par:o_par + rec.nbytes] = rec.view(np.uint8)
@@ -266,24 +269,42 @@ class GpuPreprocessor:
         for im in imgs:
             buf[at:at + im.size] = im.ravel()
             at += im.size
-        dev = stage.to(self.device, non_blocking=True)
-        base = dev.data_ptr()
-        tmp = torch.empty(tmp_len, dtype=torch.uint8, device=self.device)
-        resized = torch.empty(n * OH * OW * 3, dtype=torch.uint8, device=self.device)
+        return _Staged(stage.to(self.device, non_blocking=True), n, o_par, o_coef, o_src,
+                       tmp_len)
+
+    def run(self, st):
+        """Device side: resize + augment + normalise a staged batch (4 launches)."""
+        OH, OW = self.spec.size
+        if st.n == 0:
+            return torch.empty((0, 3, OH, OW), dtype=torch.float32, device=self.device)
+        lib = L.load()
+        base = st.dev.data_ptr()
+        tmp = torch.empty(st.tmp_len, dtype=torch.uint8, device=self.device)
+        resized = torch.empty(st.n * OH * OW * 3, dtype=torch.uint8, device=self.device)
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        check(lib.dfu_resize_batch(ctypes.c_void_p(base + o_src), ctypes.c_void_p(base),
-                                   ctypes.c_void_p(base + o_coef), n, OW, OH,
+        check(lib.dfu_resize_batch(ctypes.c_void_p(base + st.o_src), ctypes.c_void_p(base),
+                                   ctypes.c_void_p(base + st.o_coef), st.n, OW, OH,
                                    ctypes.c_void_p(tmp.data_ptr()),
                                    ctypes.c_void_p(resized.data_ptr()), stream),
               "dfu_resize_batch")
-        out = torch.empty((n, 3, OH, OW), dtype=torch.float32, device=self.device)
-        means = torch.empty(n, dtype=torch.int32, device=self.device)
+        out = torch.empty((st.n, 3, OH, OW), dtype=torch.float32, device=self.device)
+        means = torch.empty(st.n, dtype=torch.int32, device=self.device)
         check(lib.dfu_augment_normalize(ctypes.c_void_p(resized.data_ptr()),
-                                        ctypes.c_void_p(base + o_par), n, OH, OW, self._mean,
-                                        self._std, ctypes.c_void_p(means.data_ptr()),
+                                        ctypes.c_void_p(base + st.o_par), st.n, OH, OW,
+                                        self._mean, self._std, ctypes.c_void_p(means.data_ptr()),
                                         ctypes.c_void_p(out.data_ptr()), stream),
               "dfu_augment_normalize")
         return out
+
+
+@dataclass
+class _Staged:
+    dev: torch.Tensor      # the batch's staging buffer in HBM
+    n: int
+    o_par: int
+    o_coef: int
+    o_src: int
+    tmp_len: int
 
 
 def decode_rgb(path):

@@ -354,13 +354,15 @@ typedef struct dfu_aug_params {
 int dfu_resize_ksize(int32_t in_size, int32_t out_size);
 int dfu_resize_coeffs(int32_t in_size, int32_t out_size, int32_t* bounds, int32_t* kk);
 /* Resize n packed images to out_h x out_w (HWC u8): tmp holds sum_i h_i*out_w*3 bytes,
- * dst n*out_h*out_w*3.  descs and coefs are device arrays. */
+ * dst n*out_h*out_w*3.  descs and coefs are device arrays; src is read in whole aligned
+ * dwords, so it must stay readable up to 3 bytes past the last image. */
 int dfu_resize_batch(const uint8_t* src, const dfu_resize_desc* descs, const int32_t* coefs,
                      int32_t n, int32_t out_w, int32_t out_h, uint8_t* tmp, uint8_t* dst,
                      void* stream);
 /* Flips, rotation, colour jitter, affine, ToTensor and Normalize on n resized H x W x 3 u8
  * images -> out fp32 [n][3][H][W].  params and contrast_means (n int32 scratch) are device
- * arrays; mean3 / std3 are host arrays of 3 floats. */
+ * arrays (contrast_means receives the per-image grey sums); mean3 / std3 are host
+ * arrays of 3 floats. */
 int dfu_augment_normalize(const uint8_t* img, const dfu_aug_params* params, int32_t n,
                           int32_t H, int32_t W, const float* mean3, const float* std3,
                           int32_t* contrast_means, float* out, void* stream);
