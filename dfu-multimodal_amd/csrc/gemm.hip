@@ -4,6 +4,8 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "gemm_table.h"
 
 using namespace dfu;
@@ -32,6 +34,8 @@ constexpr double kReduceLaunchUs = 2.0;
 constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0};
 int g_persistent = 1;       // dfu_gemm_set_persistent
 int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
+// the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
+const int g_wide_reduce = getenv("DFU_GEMM_WIDE_REDUCE") ? atoi(getenv("DFU_GEMM_WIDE_REDUCE")) : 1;
 int g_tail_split = 1;       // dfu_gemm_set_tail_split
 
 const Entry* find_entry(int a, int b, int e, int tile) {
@@ -158,6 +162,42 @@ __global__ void k_splitk_reduce_scalar(const float* __restrict__ slab, int split
       for (int k = 0; k < splits; ++k) s += slab[k * plane + i];
       C[(int64_t)m * ldc + n] += s;
     }
+}
+
+// Small planes with many splits (the ResNet weight gradients: 64x64 .. 512x512 tiles of
+// K = 12544 .. 802816 split 16-256 ways): one lane per element (f32x4 when VEC), the waves of a
+// block split the slabs between them (wave w sums slabs w, w + nw, ...) and combine in wave
+// order through LDS — a fixed summation order, so still bitwise reproducible.
+template <bool VEC>
+__global__ void __launch_bounds__(1024) k_splitk_reduce_wide(const float* __restrict__ slab,
+                                                             int splits, int M, int N,
+                                                             float* __restrict__ C, int64_t ldc) {
+  using V = typename std::conditional<VEC, f32x4, float>::type;
+  __shared__ V red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int64_t plane = (int64_t)M * N;
+  const int64_t units = VEC ? plane / 4 : plane;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  V s = {};
+  if (e < units) {
+    const V* p = (const V*)slab + e;
+    const int64_t step = VEC ? plane / 4 : plane;
+#pragma unroll 4
+    for (int k = w; k < splits; k += nw) s += p[k * step];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0 || e >= units) return;
+  for (int j = 1; j < nw; ++j) s += red[j][lane];
+  if (VEC) {
+    const int64_t m = 4 * e / N;
+    const int n = (int)(4 * e - m * N);
+    V* c = (V*)(C + m * ldc + n);  // N % 4 == 0, ldc % 4 == 0, C 16-B aligned (host-checked)
+    *c += s;
+  } else {
+    const int64_t m = e / N;
+    C[m * ldc + (e - m * N)] += *(const float*)&s;
+  }
 }
 
 // Tail split (GemmArgs::tail_*) for an unsplit launch of `tiles` tiles over `slots`
@@ -507,7 +547,18 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
     const bool vec = d->N % 4 == 0 && d->ldc % 4 == 0 && ((uintptr_t)d->C & 15) == 0;
     int64_t blocks = (vec ? n / 4 : n) / 256 + 1;
     if (blocks > 8192) blocks = 8192;
-    if (vec)
+    if (blocks < kCUs && splits >= 8 && g_wide_reduce) {
+      // too few elements to fill the chip one lane each: split the slabs over waves too
+      const int nw = splits < 16 ? splits : 16;
+      const int64_t units = vec ? n / 4 : n;
+      const unsigned wb = (unsigned)((units + 63) / 64);
+      if (vec)
+        hipLaunchKernelGGL(k_splitk_reduce_wide<true>, dim3(wb), dim3(64 * nw), 0, s, a.slab,
+                           splits, d->M, d->N, (float*)d->C, d->ldc);
+      else
+        hipLaunchKernelGGL(k_splitk_reduce_wide<false>, dim3(wb), dim3(64 * nw), 0, s, a.slab,
+                           splits, d->M, d->N, (float*)d->C, d->ldc);
+    } else if (vec)
       hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, a.slab, splits,
                          d->M, d->N, (float*)d->C, d->ldc);
     else

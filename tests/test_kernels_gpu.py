@@ -90,6 +90,25 @@ def test_gemm_split_slab_deterministic():
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("M,N,K,split", [(64, 64, 200704, 96), (64, 147, 65536, 64),
+                                         (256, 128, 50176, 48), (64, 64, 4096, 8)])
+def test_gemm_split_wide_reduce(M, N, K, split):
+    """Small planes with many splits take the wave-split reduce (k_splitk_reduce_wide):
+    vector and scalar (N = 147, the stem) forms against fp32, bitwise reproducible."""
+    ldb = (N + 7) // 8 * 8  # MN-major operands need ld % 8 == 0 (the stem pads 147 -> 152)
+    Akm = rnd(K, M, seed=42)
+    Bkn = rnd(K, ldb, seed=43)
+    ref = Akm.float().t() @ Bkn[:, :N].float()
+    outs = []
+    for _ in range(2):
+        C = torch.full((M, N), 0.25, dtype=torch.float32, device=DEV)
+        ops.gemm(M, N, K, Akm, M, Bkn, ldb, C, N, a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR,
+                 epilogue=L.EPI_F32_ACC, split_k=split)
+        outs.append(C)
+    assert torch.equal(outs[0], outs[1])
+    close(outs[0], ref + 0.25, atol=2e-3 * (K ** 0.5), rtol=1e-3, what="wide reduce")
+
+
 def gemm_or_auto(*args, tile=0, **kw):
     """ops.gemm with a tile preference; falls back to auto where that tile is not built."""
     try:
