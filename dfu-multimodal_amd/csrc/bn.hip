@@ -15,20 +15,25 @@ namespace {
 // var = E[x^2] - mean^2 exact to ~1e-12 relative, and the tile loop is independent adds.
 constexpr int FIN_WAVES = 16;
 
+// CPW channels per block: a wave's 64 lanes cover CPW channels x (64 / CPW) tile slots, so
+// narrow layers (C = 64 over up to 6272 stem tiles) spread their tile loop over more lanes.
+template <int CPW>
 __global__ __launch_bounds__(1024) void k_bn_finalize(
     const float* __restrict__ stats, int tiles, int M, int C, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ rmean,
     float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ mean_out,
     float* __restrict__ invstd_out, float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  constexpr int TS = 64 / CPW;  // tile slots per wave
   __shared__ double sh_s[FIN_WAVES][64], sh_q[FIN_WAVES][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int cl = lane % CPW, slot = lane / CPW;
+  const int c = blockIdx.x * CPW + cl;
   double sx = 0.0, sxx = 0.0;
   if (c < C) {
     const int last = tiles - 1;
     const double inv_last = 1.0 / (double)(M - last * 128);
 #pragma unroll 4
-    for (int t = w; t < tiles; t += FIN_WAVES) {
+    for (int t = w * TS + slot; t < tiles; t += FIN_WAVES * TS) {
       const double sb = stats[((int64_t)t * 2 + 0) * C + c];
       const double qb = stats[((int64_t)t * 2 + 1) * C + c];
       sx += sb;
@@ -38,8 +43,13 @@ __global__ __launch_bounds__(1024) void k_bn_finalize(
   sh_s[w][lane] = sx;
   sh_q[w][lane] = sxx;
   __syncthreads();
-  if (w == 0 && c < C) {
-    for (int k = 1; k < FIN_WAVES; ++k) { sx += sh_s[k][lane]; sxx += sh_q[k][lane]; }
+  if (w == 0 && slot == 0 && c < C) {
+    sx = sxx = 0.0;
+    for (int k = 0; k < FIN_WAVES; ++k)
+      for (int j = 0; j < TS; ++j) {
+        sx += sh_s[k][j * CPW + cl];
+        sxx += sh_q[k][j * CPW + cl];
+      }
     const double nn = (double)M;
     const double mu = sx / nn;
     const double var = fmax(sxx / nn - mu * mu, 0.0);  // biased, used to normalise
@@ -287,7 +297,10 @@ extern "C" int dfu_bn_finalize(const float* stats, int32_t tiles, int32_t M, int
   DFU_CHECK_ARG(stats && tiles == (M + 127) / 128 && C > 0 && mean_out && invstd_out &&
                     scale_out && shift_out,
                 "dfu_bn_finalize: bad args (tiles=%d M=%d)", tiles, M);
-  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0,
+  // aim for >= 4 blocks: 16 channels per block up to C = 64, 32 up to 128, else 64
+  auto kern = C <= 64 ? k_bn_finalize<16> : (C <= 128 ? k_bn_finalize<32> : k_bn_finalize<64>);
+  const int cpw = C <= 64 ? 16 : (C <= 128 ? 32 : 64);
+  hipLaunchKernelGGL(kern, dim3((C + cpw - 1) / cpw), dim3(64 * FIN_WAVES), 0,
                      (hipStream_t)stream, stats,
                      tiles, M, C, gamma, beta, eps, momentum, running_mean, running_var,
                      num_batches, mean_out, invstd_out, scale_out, shift_out);

@@ -306,8 +306,12 @@ __global__ void k_reduce_partials(const float* __restrict__ partial, int blocks,
   const int64_t i = (int64_t)blockIdx.x * 8 + cl;  // flattened (v, d)
   const bool ok = i < (int64_t)nvec * D;
   float s = 0.f;
-  if (ok)
-    for (int b = bl; b < blocks; b += 32) s += partial[(int64_t)b * nvec * D + i];
+  if (ok) {
+    // loads issued 8 ahead, added in the same order (bitwise the same sum)
+    const int64_t st = (int64_t)nvec * D;
+#pragma unroll 8
+    for (int b = bl; b < blocks; b += 32) s += partial[(int64_t)b * st + i];
+  }
   red[bl][cl] = s;
   __syncthreads();
   if (bl == 0 && ok) {
