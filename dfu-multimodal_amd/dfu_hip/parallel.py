@@ -42,6 +42,28 @@ def broadcast_parameters(module, src=0):
             dist.broadcast(t.data, src)
 
 
+_AVG_OK = {}
+
+
+def _supports_avg(group=None):
+    """Whether all_reduce(op=AVG) works on this process group (NCCL/RCCL >= 2.10 backends do;
+    gloo does not).  Probed once per group with a 1-element collective on every rank — ranks
+    reach the same answer, so the collectives stay paired."""
+    key = id(group)
+    if key not in _AVG_OK:
+        ok = False
+        if dist.get_backend(group) == "nccl" and hasattr(dist.ReduceOp, "AVG"):
+            t = torch.ones(1, device="cuda")
+            try:
+                dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group)
+                torch.cuda.synchronize()
+                ok = bool(abs(t.item() - 1.0) < 1e-6)
+            except (RuntimeError, ValueError):
+                ok = False
+        _AVG_OK[key] = ok
+    return _AVG_OK[key]
+
+
 class GradAllReducer:
     """Bucketed all-reduce (sum, then /world) over the FusedAdamW flat gradient buffer.
 
@@ -49,12 +71,20 @@ class GradAllReducer:
     backward; call ``finish()`` before the optimizer step.  overlap=False: ``finish()`` issues
     every bucket after backward (graph-capture friendly)."""
 
-    def __init__(self, flat, bucket_mb=32.0, overlap=True, group=None):
+    def __init__(self, flat, bucket_mb=None, overlap=True, group=None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.overlap = overlap and self.world > 1
         self.stream = torch.cuda.Stream() if flat.grad.is_cuda else None
+        # Buckets exist to start reducing while backward still runs.  Without overlap every
+        # bucket is issued back to back after backward, so one large bucket (fewer collective
+        # launches, full-size ring transfers over xGMI) is strictly better.
+        if bucket_mb is None:
+            bucket_mb = 32.0 if self.overlap else 1024.0
+        # the mean as one collective (RCCL/NCCL ReduceOp.AVG: the 1/world scaling rides in the
+        # reduction) where the backend has it; otherwise SUM then one scaling pass per bucket
+        self.avg = self.world > 1 and flat.grad.is_cuda and _supports_avg(group)
         cap = int(bucket_mb * (1 << 20) / 4)
         # reverse parameter order: the last parameters' gradients are produced first
         order = list(range(len(flat.params)))[::-1]
@@ -90,12 +120,17 @@ class GradAllReducer:
             self.stream.wait_stream(torch.cuda.current_stream())
             Fn.join_grad_streams(self.stream, clear=False)
             with torch.cuda.stream(self.stream):
-                dist.all_reduce(view, group=self.group)
-                view.mul_(1.0 / self.world)
+                self._reduce(view)
+        else:
+            self._reduce(view)
+        self._issued[k] = True
+
+    def _reduce(self, view):
+        if self.avg:
+            dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group)
         else:
             dist.all_reduce(view, group=self.group)
             view.mul_(1.0 / self.world)
-        self._issued[k] = True
 
     def _on_ready(self, p):
         if self._pending is None:
