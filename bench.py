@@ -40,7 +40,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="per GPU (default 64; gradcam 32)")
     ap.add_argument("--config", default="fusion", choices=["fusion", "thermal", "rgb", "gradcam",
                                                                "pipeline"])
-    ap.add_argument("--no-graph", action="store_true", help="eager step instead of a HIP graph")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the train step as one HIP graph (default: eager, measured faster: "
+                         "the two encoder streams overlap better than the graph's branches)")
+    ap.add_argument("--no-graph", action="store_true", help="eager (the default; kept for scripts)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -443,13 +446,18 @@ def main():
     parallel.broadcast_parameters(model)
     opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
     crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
-    reducer = parallel.GradAllReducer(opt.flat, overlap=False) if world > 1 else None
+    use_graph = args.graph and not args.no_graph
+    # eager: bucketed all-reduce on a side stream, launched from the gradient-ready hooks while
+    # backward runs; a captured graph issues every bucket after backward instead
+    reducer = parallel.GradAllReducer(opt.flat, overlap=not use_graph) if world > 1 else None
     rgb, th, y = synthetic(args.batch, dev, seed=42 + rank)
 
     from dfu_hip import functional as Fn
 
     def fwd_bwd():
         opt.zero_grad()
+        if reducer is not None and reducer.overlap:
+            reducer.start()
         out = fwd(model, rgb, th)
         loss = crit(out, y)
         loss.backward()
@@ -461,7 +469,6 @@ def main():
             reducer.finish()
         opt.step()
 
-    use_graph = not args.no_graph
     graph = None
     # warm-up (also builds every persistent buffer) on a side stream, as graph capture needs
     s = torch.cuda.Stream()
