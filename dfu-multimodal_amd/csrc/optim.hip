@@ -84,33 +84,64 @@ DFU_DEV void adam_update(float& p, float g, float& m, float& v, const AdamCoef& 
 
 // Optionally also writes the bf16 shadow of the updated parameters (the GEMM operand copy),
 // so no per-step cast kernels are needed.
-__global__ void k_adamw_flat(float* __restrict__ p, const float* __restrict__ g,
-                             float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
-                             float b1, float b2, float eps, float wd,
-                             const int64_t* __restrict__ step_dev, bf16_t* __restrict__ shadow) {
+__device__ __forceinline__ void adamw_vec4(float* __restrict__ p, const float* __restrict__ g,
+                                           float* __restrict__ m, float* __restrict__ v,
+                                           bf16_t* __restrict__ shadow, int64_t i, f32x4 pp,
+                                           f32x4 gg, f32x4 mm, f32x4 vv, const AdamCoef& a,
+                                           float b1, float b2, float eps) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float pe = pp[e], me = mm[e], ve = vv[e];
+    adam_update(pe, gg[e], me, ve, a, b1, b2, eps);
+    pp[e] = pe; mm[e] = me; vv[e] = ve;
+  }
+  ((f32x4*)p)[i] = pp;
+  ((f32x4*)m)[i] = mm;
+  ((f32x4*)v)[i] = vv;
+  if (shadow) ((u32x2*)shadow)[i] = (u32x2){pack2(pp[0], pp[1]), pack2(pp[2], pp[3])};
+}
+
+// Each thread handles ADAM_UNROLL float4 groups per grid-stride pass, spaced one grid apart so
+// every wave's accesses stay contiguous; all 4 x ADAM_UNROLL loads issue before the first
+// update.  The optimizer is a pure streaming pass (4 reads + 3 writes of fp32 and one bf16
+// write per parameter, 30 B).  Measured on MI355X at 110.75M parameters (same box): one block
+// per CU beats a wide grid by ~20% (601 vs 767 us; 4096 blocks keep 7 streams x 16 waves per
+// CU fighting over HBM pages), and unrolling does not help at that grid (unroll 2/4: 656/625 us).
+template <int ADAM_UNROLL>
+__global__ void __launch_bounds__(256) k_adamw_flat(float* __restrict__ p,
+                                                    const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    int64_t n, float lr, float b1, float b2,
+                                                    float eps, float wd,
+                                                    const int64_t* __restrict__ step_dev,
+                                                    bf16_t* __restrict__ shadow) {
   const AdamCoef a = adam_coef(*step_dev, lr, b1, b2, wd);
   const int64_t n4 = n / 4;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    f32x4 pp = ((f32x4*)p)[i], mm = ((f32x4*)m)[i], vv = ((f32x4*)v)[i];
-    const f32x4 gg = ((const f32x4*)g)[i];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + (ADAM_UNROLL - 1) * stride < n4; i += ADAM_UNROLL * stride) {
+    f32x4 pp[ADAM_UNROLL], gg[ADAM_UNROLL], mm[ADAM_UNROLL], vv[ADAM_UNROLL];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pp[e], me = mm[e], ve = vv[e];
-      adam_update(pe, gg[e], me, ve, a, b1, b2, eps);
-      pp[e] = pe; mm[e] = me; vv[e] = ve;
+    for (int u = 0; u < ADAM_UNROLL; ++u) {
+      const int64_t j = i + u * stride;
+      gg[u] = ((const f32x4*)g)[j];
+      pp[u] = ((f32x4*)p)[j];
+      mm[u] = ((f32x4*)m)[j];
+      vv[u] = ((f32x4*)v)[j];
     }
-    ((f32x4*)p)[i] = pp;
-    ((f32x4*)m)[i] = mm;
-    ((f32x4*)v)[i] = vv;
-    if (shadow) ((u32x2*)shadow)[i] = (u32x2){pack2(pp[0], pp[1]), pack2(pp[2], pp[3])};
+#pragma unroll
+    for (int u = 0; u < ADAM_UNROLL; ++u)
+      adamw_vec4(p, g, m, v, shadow, i + u * stride, pp[u], gg[u], mm[u], vv[u], a, b1, b2, eps);
   }
-  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float pe = p[i], me = m[i], ve = v[i];
-    adam_update(pe, g[i], me, ve, a, b1, b2, eps);
-    p[i] = pe; m[i] = me; v[i] = ve;
-    if (shadow) shadow[i] = f2bf(pe);
+  for (; i < n4; i += stride)
+    adamw_vec4(p, g, m, v, shadow, i, ((f32x4*)p)[i], ((const f32x4*)g)[i], ((f32x4*)m)[i],
+               ((f32x4*)v)[i], a, b1, b2, eps);
+  for (int64_t k = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
+       k += stride) {
+    float pe = p[k], me = m[k], ve = v[k];
+    adam_update(pe, g[k], me, ve, a, b1, b2, eps);
+    p[k] = pe; m[k] = me; v[k] = ve;
+    if (shadow) shadow[k] = f2bf(pe);
   }
 }
 
@@ -179,9 +210,16 @@ extern "C" int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, f
                     ((uintptr_t)shadow_bf16 & 7) == 0,
                 "dfu_adamw_flat: buffers must be 16-byte aligned (shadow 8-byte)");
   int64_t blocks = (n / 4 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
+  static const int64_t cap = [] {  // one block per CU (see k_adamw_flat)
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return (int64_t)cus;
+  }();
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_adamw_flat, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param,
+  hipLaunchKernelGGL(k_adamw_flat<1>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param,
                      grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step_dev,
                      (bf16_t*)shadow_bf16);
   DFU_LAUNCH_CHECK();
