@@ -57,7 +57,8 @@ __global__ void k_ln_fwd(const float* __restrict__ x, int64_t ldx, int rows, int
   }
 }
 
-constexpr int LNB_ROWS = 16;  // rows per block in the backward (4 per wave): 788 blocks at B=64
+constexpr int LNB_ROWS = 32;  // rows per block in the backward (8 per wave): 394 blocks at B=64
+constexpr int LNB_ILP = 2;    // rows per wave whose loads issue together (same box: 16/2 34.4 us, 32/2 31.7, 64/2 36.8, 32/4 41.5)
 
 // Backward, one wave per row, 4 rows per wave processed two at a time: all loads of a row pair
 // (x, dy, and the residual gradient gx it adds into) are issued before either row's
@@ -84,12 +85,12 @@ __global__ __launch_bounds__(256) void k_ln_bwd(
   }
   const int row0 = blockIdx.x * LNB_ROWS + wave * (LNB_ROWS / 4);
 #pragma unroll 1
-  for (int rp = 0; rp < LNB_ROWS / 4; rp += 2) {
-    f32x4 xv[2][NV], gv[2][NV];
-    float dy[2][NV][4], mu[2], rs[2];
-    bool ok[2];
+  for (int rp = 0; rp < LNB_ROWS / 4; rp += LNB_ILP) {
+    f32x4 xv[LNB_ILP][NV], gv[LNB_ILP][NV];
+    float dy[LNB_ILP][NV][4], mu[LNB_ILP], rs[LNB_ILP];
+    bool ok[LNB_ILP];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // load phase: both rows
+    for (int h = 0; h < LNB_ILP; ++h) {  // load phase: LNB_ILP rows
       const int row = row0 + rp + h;
       ok[h] = row < rows;
       mu[h] = ok[h] ? mean_in[row] : 0.f;
@@ -117,9 +118,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd(
         }
       }
     }
-    float s1[2], s2[2];
+    float s1[LNB_ILP], s2[LNB_ILP];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < LNB_ILP; ++h) {
       s1[h] = 0.f;
       s2[h] = 0.f;
 #pragma unroll
@@ -135,12 +136,12 @@ __global__ __launch_bounds__(256) void k_ln_bwd(
         }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < LNB_ILP; ++h) {
       s1[h] = wave_sum(s1[h]) / (float)D;
       s2[h] = wave_sum(s2[h]) / (float)D;
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < LNB_ILP; ++h) {
       if (!ok[h]) continue;
       const int row = row0 + rp + h;
 #pragma unroll
