@@ -46,6 +46,11 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager (the default; kept for scripts)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16x3"],
+                    help="forward precision of the timed step (value); the other mode is timed "
+                         "beside it and reported under precision_modes")
+    ap.add_argument("--no-alt-precision", action="store_true",
+                    help="skip timing the other precision mode")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = 32 if args.config == "gradcam" else 64
@@ -85,13 +90,34 @@ def build(config, device):
     return model.to(device).train(), fwd
 
 
-def cpu_baseline(config, threads, budget_s=10.0):
+def host_cores():
+    """Host CPU description for cpu_baseline: os.cpu_count() and lscpu's sockets x cores per
+    socket x threads per core (the core count is stated)."""
+    import subprocess
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        keys = {"Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                "Thread(s) per core": "threads_per_core", "Model name": "model"}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in keys:
+                v = v.strip()
+                info[keys[k.strip()]] = int(v) if v.isdigit() else v
+        if "sockets" in info and "cores_per_socket" in info:
+            info["physical_cores"] = info["sockets"] * info["cores_per_socket"]
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
+
+
+def cpu_baseline(config, threads, warmup=3, timed=10, B=8):
     """The oracle (plain PyTorch fp32, oracle/torch_ref.py) timed on the host cores on a bounded
-    sample of the same workload: full train step (fwd+bwd+AdamW) at B=8, 1 warm-up, then timed
-    steps until ~budget_s of CPU work (at most 6)."""
+    sample of the same workload, as BASELINE.md prescribes: the full train step (fwd + bwd +
+    AdamW) at batch B, `warmup` untimed steps, then the median of `timed` steps."""
+    import statistics
     from oracle import torch_ref as R
     torch.set_num_threads(threads)
-    B = 8
     torch.manual_seed(0)
     if config == "fusion":
         model = R.MultimodalFusionModel(num_classes=2, dropout=0.7)
@@ -113,18 +139,23 @@ def cpu_baseline(config, threads, budget_s=10.0):
         loss.backward()
         opt.step()
 
-    step()
-    t0 = time.perf_counter()
-    n = 0
-    while n < 6 and (n == 0 or time.perf_counter() - t0 < budget_s):
+    for _ in range(warmup):
         step()
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(B * n / dt, 3), "unit": "images/sec", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle fp32 eager {config} train step (fwd+bwd+AdamW), batch {B}, "
-                      f"{n} timed steps ({dt:.1f} s) after 1 warm-up, "
-                      f"torch.set_num_threads({threads})"}
+    times = []
+    for _ in range(timed):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    cores = host_cores()
+    return {"value": round(B / med, 3), "unit": "images/sec", "cores": threads,
+            "kind": "port", "host": cores,
+            "sample": f"oracle fp32 eager {config} train step (fwd+bwd+AdamW), batch {B}: "
+                      f"median of {timed} timed steps ({med * 1e3:.0f} ms/step, "
+                      f"{sum(times):.1f} s) after {warmup} warm-up, "
+                      f"torch.set_num_threads({threads}) on a host with "
+                      f"{cores.get('physical_cores', '?')} physical cores "
+                      f"(os.cpu_count() {cores['os_cpu_count']})"}
 
 
 def cpu_baseline_gradcam(threads, budget_s=10.0):
@@ -158,17 +189,19 @@ def cpu_baseline_gradcam(threads, budget_s=10.0):
                       f"warm-up, torch.set_num_threads({threads})"}
 
 
+# The PMC traffic measurement this tree's bench line cites (tools/prof_summary.py output of the
+# separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; bench.py cannot read counters itself).
+TRAFFIC_FILE = os.path.join("profiles", "r03_gemm_traffic.json")
+
+
 def gemm_traffic():
-    """HBM bytes per GEMM launch from the latest committed PMC measurement
-    (profiles/r*_gemm_traffic.json, written by tools/prof_summary.py from separate rocprofv3
-    --pmc FETCH_SIZE / WRITE_SIZE passes of this bench; bench.py cannot read counters itself)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_gemm_traffic.json")), key=os.path.getmtime)
-    if not files:
+    """HBM bytes per GEMM launch from TRAFFIC_FILE (chosen by name, never by file time)."""
+    path = os.path.join(ROOT, TRAFFIC_FILE)
+    if not os.path.exists(path):
         return None, None
-    with open(files[-1]) as f:
+    with open(path) as f:
         t = json.load(f)
-    return t["bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return t["bytes_per_launch"], TRAFFIC_FILE
 
 
 def gemm_roofline(fwd_bwd, tail, replays=3):
@@ -426,6 +459,64 @@ def main_pipeline(args, rank, world, dev):
         dist.destroy_process_group()
 
 
+def timed_steps(step, steps, world, dev, per_step=True):
+    """Run `steps` steps between barrier + synchronize brackets; returns the wall-clock seconds
+    (max over ranks), the HIP-event window in ms (max over ranks) and the per-step HIP-event
+    durations (ms, this rank) from an event recorded after every step."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record()
+    for k in range(steps):
+        step()
+        if per_step or k == steps - 1:
+            evs[k + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = evs[0].elapsed_time(evs[-1])
+    durs = [evs[k].elapsed_time(evs[k + 1]) for k in range(steps)] if per_step else []
+    if world > 1:
+        t = torch.tensor([elapsed, gpu_ms / 1000.0], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gpu_s = t.tolist()
+        gpu_ms = gpu_s * 1000.0
+    return elapsed, gpu_ms, durs
+
+
+def pct(xs, q):
+    """q-th percentile (linear interpolation) of a non-empty list."""
+    xs = sorted(xs)
+    k = (len(xs) - 1) * q
+    lo = int(k)
+    hi = min(lo + 1, len(xs) - 1)
+    return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+
+def parity_record():
+    """The committed whole-model parity measurement (tests/test_model_parity_gpu.py output,
+    copied to profiles/r03_parity.json): the bf16x3 / bf16 logits deltas at B=64."""
+    path = os.path.join(ROOT, "profiles", "r03_parity.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    out = {"source": "profiles/r03_parity.json (tests/test_model_parity_gpu.py, C3 B=64)"}
+    if "c3_b64_bf16x3" in d:
+        out["bf16x3_max_abs_logits_vs_fp32_oracle"] = d["c3_b64_bf16x3"][
+            "max_abs_logits_vs_fp32_oracle"]
+    if "c3_b64_bf16" in d:
+        out["bf16_max_abs_logits_vs_fp32_oracle"] = d["c3_b64_bf16"][
+            "max_abs_logits_vs_fp32_oracle"]
+        out["bf16_max_abs_logits_vs_bf16_oracle"] = d["c3_b64_bf16"][
+            "max_abs_logits_vs_bf16_oracle"]
+    out["bar"] = 1e-3
+    return out
+
+
 def main():
     args = parse()
     from dfu_hip import parallel
@@ -434,14 +525,18 @@ def main():
         args.gpus = world
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    torch.manual_seed(42)
+    # per-rank torch seed (the dropout RNG is seeded per rank; dfu_hip.nn.Dropout
+    # also mixes the rank into its key); the weights are broadcast from rank 0 below
+    torch.manual_seed(42 + rank)
     if args.config == "gradcam":
         return main_gradcam(args, rank, world, dev)
     if args.config == "pipeline":
         return main_pipeline(args, rank, world, dev)
 
+    from dfu_hip import functional as Fn
     from dfu_hip import nn as hnn
     from dfu_hip.optim import FusedAdamW
+    Fn.set_precision(args.precision)
     model, fwd = build(args.config, dev)
     parallel.broadcast_parameters(model)
     opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
@@ -451,8 +546,6 @@ def main():
     # backward runs; a captured graph issues every bucket after backward instead
     reducer = parallel.GradAllReducer(opt.flat, overlap=not use_graph) if world > 1 else None
     rgb, th, y = synthetic(args.batch, dev, seed=42 + rank)
-
-    from dfu_hip import functional as Fn
 
     def fwd_bwd():
         opt.zero_grad()
@@ -508,27 +601,22 @@ def main():
             fwd_bwd()
             tail()
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
-        step()
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    gpu_ms = ev0.elapsed_time(ev1)
-    if world > 1:
-        t = torch.tensor([elapsed, gpu_ms / 1000.0], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gpu_s = t.tolist()
-        gpu_ms = gpu_s * 1000.0
+    elapsed, gpu_ms, durs = timed_steps(step, args.steps, world, dev)
+    # the other precision mode, same model and batch, eager (reported beside `value`)
+    alt = None
+    if not args.no_alt_precision and graph is None:
+        other = "bf16x3" if args.precision == "bf16" else "bf16"
+        old = Fn.set_precision(other)
+        try:
+            for _ in range(2):
+                step()
+            a_el, a_ms, a_durs = timed_steps(step, args.steps, world, dev)
+        finally:
+            Fn.set_precision(old)
+        alt = {"precision": other,
+               "value": round(args.batch * args.gpus * args.steps / a_el, 2),
+               "ms_per_step": round(a_el * 1000.0 / args.steps, 3),
+               "gpu_ms_per_step_median": round(pct(a_durs, 0.5), 3)}
     # every rank runs the instrumented steps (their all-reduces must pair up); rank 0 reports
     opt.check_grads = True
     gr = gemm_roofline(fwd_bwd, tail)
@@ -547,6 +635,10 @@ def main():
                   "thermal": "images/sec (thermal ViT-B/16 fwd+bwd, bs=64/GPU)",
                   "rgb": "images/sec (RGB ResNet50 fwd+bwd, bs=64/GPU)"}[args.config]
         traffic, traffic_src = gemm_traffic()
+        modes = {args.precision: {"value": round(value, 2),
+                                  "ms_per_step": round(elapsed * 1000.0 / args.steps, 3)}}
+        if alt is not None:
+            modes[alt["precision"]] = {k: v for k, v in alt.items() if k != "precision"}
         line = {
             "metric": metric,
             "value": round(value, 2),
@@ -559,6 +651,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
+            "precision": args.precision,
             "data": "synthetic 224x224 RGB+thermal pairs (uint8 U{0..255}, reference "
                     "normalisation), random-init weights (seed 42), resident in HBM",
             "config": {"workload": f"C3 {args.config} train step (fwd+bwd+AdamW) "
@@ -567,6 +660,11 @@ def main():
                        "global_batch": args.batch * args.gpus, "per_gpu_batch": args.batch,
                        "image": 224, "parallelism": f"dp{args.gpus}",
                        "hip_graph": graph is not None},
+            "gpu_step_ms": {"median": round(pct(durs, 0.5), 3), "p10": round(pct(durs, 0.1), 3),
+                            "p90": round(pct(durs, 0.9), 3), "basis": "HIP events after every "
+                            "step of the timed window (rank 0)"},
+            "precision_modes": modes,
+            "parity": parity_record(),
             "roofline": {"bound": "mfma", "achieved": round(gr["achieved"], 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(gr["achieved"] / PEAK_BF16_TFLOPS, 4),

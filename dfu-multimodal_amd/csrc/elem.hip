@@ -68,12 +68,27 @@ __global__ void k_cast_rows_f32(const bf16_t* __restrict__ in, int64_t ld_in,
 }
 
 // ---------------------------------------------------------------- stem im2col / patchify
+// 8 values as the split-bf16 triple of csrc/precise.hip: hi | lo | hi, segments C apart.
+DFU_DEV void store_triple8(bf16_t* row, int C, int c, const float* f) {
+  float hi[8], lo[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    hi[e] = bf2f(f2bf(f[e]));
+    lo[e] = f[e] - hi[e];
+  }
+  const u32x4 h = pack8(hi);
+  *(u32x4*)(row + c) = h;
+  *(u32x4*)(row + C + c) = pack8(lo);
+  *(u32x4*)(row + 2 * C + c) = h;
+}
+
 // out[m][k], m = (b, oh, ow), k = c*R*S + r*S + s; each thread writes one 16-B vector (8 k).
 // Stem im2col: fp32 NCHW input -> bf16 [B*P*Q][Kp] rows, k = (c, r, s) (OIHW weight order),
 // zero-padded to Kp.  Each thread owns one 16-byte chunk kv of the row (its 8 taps decoded
 // once); a block of VPR*RPB threads covers RPB consecutive rows per iteration, so a wave's
 // stores are contiguous row bytes.  One division per row decodes (b, oh, ow).
-template <int VPR>
+// X3: the split-bf16 triple [hi | lo | hi] (row stride 3 Kp; csrc/precise.hip) instead.
+template <int VPR, bool X3 = false>
 __global__ __launch_bounds__(VPR * 16) void k_im2col_f32(
     const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int B, int C,
     int H, int W, int R, int S, int stride, int pad, int P, int Q, bf16_t* __restrict__ out) {
@@ -104,10 +119,15 @@ __global__ __launch_bounds__(VPR * 16) void k_im2col_f32(
       const bool ok = tc[e] >= 0 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
       f[e] = ok ? xb[tc[e] * sc + ih * sh + iw * sw] : 0.f;
     }
-    *(u32x4*)(out + (int64_t)m * Kp + kv * 8) = pack8(f);
+    if constexpr (X3) {
+      store_triple8(out + (int64_t)m * 3 * Kp, Kp, kv * 8, f);
+    } else {
+      *(u32x4*)(out + (int64_t)m * Kp + kv * 8) = pack8(f);
+    }
   }
 }
 
+template <bool X3 = false>
 __global__ void k_patchify_f32(const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh,
                                int64_t sw, int B, int C, int H, int W, int ps,
                                bf16_t* __restrict__ out) {
@@ -130,7 +150,11 @@ __global__ void k_patchify_f32(const float* __restrict__ x, int64_t sn, int64_t 
     float f[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = src[e * sw];
-    *(u32x4*)(out + m * K + k0) = pack8(f);
+    if constexpr (X3) {
+      store_triple8(out + m * 3 * K, K, k0, f);
+    } else {
+      *(u32x4*)(out + m * K + k0) = pack8(f);
+    }
   }
 }
 
@@ -580,7 +604,32 @@ extern "C" int dfu_patchify_f32(const float* x, int64_t sn, int64_t sc, int64_t 
   DFU_CHECK_ARG(x && out && ps % 8 == 0 && H % ps == 0 && W % ps == 0,
                 "dfu_patchify_f32: bad patch size %d for %dx%d", ps, H, W);
   const int64_t n = (int64_t)B * (H / ps) * (W / ps) * (C * ps * ps / 8);
-  LAUNCH(k_patchify_f32, n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
+  LAUNCH(k_patchify_f32<false>, n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
+  return DFU_OK;
+}
+
+extern "C" int dfu_im2col_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
+                                 int32_t B, int32_t C, int32_t H, int32_t W, int32_t R, int32_t S,
+                                 int32_t stride, int32_t pad, int32_t P, int32_t Q, void* out,
+                                 int32_t Kp, void* stream) {
+  DFU_CHECK_ARG(x && out && Kp == 160 && Kp >= C * R * S, "dfu_im2col_f32_x3: bad Kp=%d", Kp);
+  DFU_CHECK_ARG(((uintptr_t)out & 15) == 0, "dfu_im2col_f32_x3: out must be 16-B aligned");
+  const int64_t rows = (int64_t)B * P * Q;
+  DFU_CHECK_ARG(rows < (1ll << 31), "dfu_im2col_f32_x3: too many rows");
+  const int blocks = (int)((rows + 15) / 16 < 8192 ? (rows + 15) / 16 : 8192);
+  hipLaunchKernelGGL((k_im2col_f32<20, true>), dim3(blocks), dim3(320), 0, (hipStream_t)stream,
+                     x, sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q, (bf16_t*)out);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_patchify_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
+                                   int32_t B, int32_t C, int32_t H, int32_t W, int32_t ps,
+                                   void* out, void* stream) {
+  DFU_CHECK_ARG(x && out && ps % 8 == 0 && H % ps == 0 && W % ps == 0,
+                "dfu_patchify_f32_x3: bad patch size %d for %dx%d", ps, H, W);
+  const int64_t n = (int64_t)B * (H / ps) * (W / ps) * (C * ps * ps / 8);
+  LAUNCH(k_patchify_f32<true>, n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
   return DFU_OK;
 }
 

@@ -379,7 +379,7 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
     DFU_CHECK_ARG(d->lda >= round8(d->M), "dfu_gemm: MN-major A needs lda >= round8(M)");
   if (d->b_mode == DFU_OPND_MNMAJOR)
     DFU_CHECK_ARG(d->ldb >= round8(d->N), "dfu_gemm: MN-major B needs ldb >= round8(N)");
-  if (d->epilogue == DFU_EPI_BF16_STATS)
+  if (d->epilogue == DFU_EPI_BF16_STATS || d->epilogue == DFU_EPI_F32_STATS)
     DFU_CHECK_ARG(d->stats != nullptr, "dfu_gemm: STATS epilogue needs a stats slab");
 
   const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
@@ -514,7 +514,8 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   }
   // the epilogue addresses its outputs by 32-bit offsets within a 2 GiB buffer range
   const bool c32 = d->epilogue == DFU_EPI_F32 || d->epilogue == DFU_EPI_F32_RESID ||
-                   d->epilogue == DFU_EPI_F32_ACC || d->epilogue == DFU_EPI_PATCH;
+                   d->epilogue == DFU_EPI_F32_ACC || d->epilogue == DFU_EPI_PATCH ||
+                   d->epilogue == DFU_EPI_F32_STATS;
   int64_t c_rows = d->M;
   if (ph) c_rows = (int64_t)d->conv_n * d->conv_h * d->conv_w;
   if (d->epilogue == DFU_EPI_PATCH && d->ep_tokens > 0)

@@ -657,9 +657,9 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
   const int M = p.M, N = p.N;
   const rsrc_t rc = make_rsrc(p.C);
 
-  if constexpr (EPI == DFU_EPI_BF16_STATS) {
-    // bf16 store + per-column (sum, M2) of this TM-row tile over the rounded values: per wave
-    // two-pass in registers, then Chan's merge across the WGM row-waves in LDS.  The stats
+  if constexpr (EPI == DFU_EPI_BF16_STATS || EPI == DFU_EPI_F32_STATS) {
+    // bf16 (fp32) store + per-column (sum, M2) of this TM-row tile over the stored values: per
+    // wave two-pass in registers, then Chan's merge across the WGM row-waves in LDS.  The stats
     // records are stored before the tile (the K-loop's waits count only the tile stores).
     float cnt = 0.f;
 #pragma unroll
@@ -673,7 +673,8 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const int m = m0 + wr * WTM + 16 * i + lrow;
-          const float v = bf2f(f2bf(acc[i][j][r] * p.alpha));
+          const float v = EPI == DFU_EPI_BF16_STATS ? bf2f(f2bf(acc[i][j][r] * p.alpha))
+                                                    : acc[i][j][r] * p.alpha;
           acc[i][j][r] = v;
           s += (m < M) ? v : 0.f;
         }
@@ -734,7 +735,15 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[j][r] = acc[i][j][r];
-      st_row_bf16<FN>(rc, (int64_t)m * p.ldc, m < M, n0 + wc * WTN, N, p.n8, n4, lane, v);
+      if constexpr (EPI == DFU_EPI_BF16_STATS) {
+        st_row_bf16<FN>(rc, (int64_t)m * p.ldc, m < M, n0 + wc * WTN, N, p.n8, n4, lane, v);
+      } else {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = n0 + wc * WTN + 16 * j + lcol;
+          st4_f32(rc, (int64_t)(m < M ? m : 0) * p.ldc + n, m < M, n, N, n4, v[j]);
+        }
+      }
     }
   } else {
     constexpr bool kBias = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU || EPI == DFU_EPI_F32 ||
@@ -842,7 +851,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   using T = Tile<TM, TN, OCC, NST, NW>;
   constexpr int WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
   constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
-  constexpr int SCRATCH = EPI == DFU_EPI_BF16_STATS ? T::STATS_BYTES : 16;  // stats / flag
+  constexpr int SCRATCH =
+      (EPI == DFU_EPI_BF16_STATS || EPI == DFU_EPI_F32_STATS) ? T::STATS_BYTES : 16;  // stats / flag
   // ALL LDS in one array: a second __shared__ object can make hipcc drain the DMA per K-step
   __shared__ __attribute__((aligned(16))) char smem[T::LDS_BYTES + SCRATCH];
   const int tid = threadIdx.x;

@@ -23,7 +23,7 @@ c_char_p = ctypes.c_char_p
 OPND_KMAJOR, OPND_MNMAJOR, OPND_CONV_FWD, OPND_CONV_DGRAD, OPND_CONV_DGRAD_W, OPND_CONV_WGRAD_X = range(6)
 # enum dfu_epilogue
 (EPI_BF16, EPI_BF16_RELU, EPI_BF16_GELU, EPI_F32, EPI_F32_RESID, EPI_BF16_DGELU, EPI_BF16_ADD,
- EPI_F32_ACC, EPI_F32_ACC_CONVW, EPI_BF16_STATS, EPI_PATCH) = range(11)
+ EPI_F32_ACC, EPI_F32_ACC_CONVW, EPI_BF16_STATS, EPI_PATCH, EPI_F32_STATS) = range(12)
 
 DFU_E_INVALID = 1001
 DFU_E_UNSUPPORTED = 1002
@@ -119,6 +119,16 @@ PROTOTYPES = {
     "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P],
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
+    "dfu_split_x3": [P, I64, I32, I32, I32, P, I32, P, I64, P],
+    "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, P],
+    "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],
+    "dfu_patchify_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
+    "dfu_bn_apply_x3": [P, P, P, P, I32, I32, P, P, P, P, I64, I32, P],
+    "dfu_maxpool_fwd_x3": [P, I32, I32, I32, I32, P, P, P, I32, I32, P],
+    "dfu_avgpool_fwd_x3": [P, I32, I32, I32, P, P],
+    "dfu_layernorm_fwd_x3": [P, I64, I32, I32, P, P, F, P, P, P, P, P],
+    "dfu_gelu_x3": [P, I64, I32, P, P, P, P],
+    "dfu_attention_fwd_f32": [P, I32, I32, I32, I32, F, I32, P, P, P, P],
     "dfu_resize_ksize": [I32, I32],
     "dfu_resize_coeffs": [I32, I32, P, P],
     "dfu_resize_batch": [P, P, P, I32, I32, I32, P, P, P],

@@ -30,6 +30,49 @@ from . import ops
 BF16 = torch.bfloat16
 F32 = torch.float32
 
+# ------------------------------------------------------------------------ precision mode
+# "bf16" (default): bf16 GEMM operands and activations, fp32 accumulation and statistics.
+# "bf16x3": the FORWARD pass at fp32 accuracy (csrc/precise.hip): every forward contraction
+#   runs on the same MFMA GEMM over split-bf16 triples (hi/lo operands, K tripled), activations
+#   stay fp32 between kernels and attention runs in fp32, so the fusion logits meet north_star's
+#   "within 1e-3 abs of the reference CPU path" against the fp32 oracle.  The backward pass is
+#   the bf16 one (it reads the plain bf16 tensors the split kernels also write).
+PRECISIONS = ("bf16", "bf16x3")
+_precision = ["bf16"]
+
+
+def set_precision(mode):
+    """Select the forward precision ("bf16" or "bf16x3"); returns the previous mode."""
+    if mode not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {mode!r}")
+    old = _precision[0]
+    _precision[0] = mode
+    return old
+
+
+def get_precision():
+    return _precision[0]
+
+
+class precision:
+    """Context manager: ``with functional.precision("bf16x3"): logits = model(rgb, th)``."""
+
+    def __init__(self, mode):
+        self.mode = mode
+        self.old = None
+
+    def __enter__(self):
+        self.old = set_precision(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_precision(self.old)
+        return False
+
+
+def _x3():
+    return _precision[0] == "bf16x3"
+
 # ------------------------------------------------------------------------- grad plumbing
 _grad_ready_hooks = []
 
@@ -147,6 +190,33 @@ def conv_weight_bf16(w):
     return ops.pack_conv_weight(w.detach())
 
 
+def weight_x3_rows(w, seg=None):
+    """fp32 [N, K...] parameter -> bf16x3 GEMM B operand [N, 3 seg] = [hi | hi | lo]."""
+    return ops.split_x3(w.detach().reshape(w.shape[0], -1), ops.X3_B, seg=seg)
+
+
+def conv_weight_x3(w):
+    """fp32 OIHW conv weight -> bf16x3 KRSC' operand (C' = 3C; 1x1: the row split)."""
+    if w.shape[2] == 1 and w.shape[3] == 1:
+        return weight_x3_rows(w)
+    return ops.pack_conv_weight_x3(w.detach())
+
+
+def _take_x3(x):
+    """The fp32-accurate triple [rows][3C] a bf16x3 producer attached to activation x (and
+    detach it from x: each one has a single consumer); built from x itself (lo = 0) when x came
+    from elsewhere."""
+    t = getattr(x, "_dfu_x3", None)
+    if t is not None:
+        try:
+            del x._dfu_x3
+        except AttributeError:
+            pass
+        return t
+    xb = nhwc_bf16(x.detach())
+    return ops.split_x3(ops.cast_rows_f32(rows_view(xb).contiguous()), ops.X3_A)
+
+
 # ---------------------------------------------------------------------- BatchNorm helper
 class _BN:
     """Forward/backward state of one BatchNorm2d applied to a GEMM output with stats."""
@@ -204,6 +274,21 @@ def conv_fwd(x_rows, geom, w_krsc, y, stats):
                  epilogue=L.EPI_BF16_STATS, stats=stats, conv=g)
 
 
+def conv_fwd_x3(x3_rows, geom, w3, y, stats):
+    """bf16x3: fp32 y[M, K] = conv(x) over the channel-tripled triple x3 [N*H*W, 3C] and KRSC'
+    weights; BN tile statistics of the unrounded outputs into stats."""
+    g = geom
+    M = g.n * g.p * g.q
+    C3 = 3 * g.c
+    if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
+        ops.gemm(M, g.k, C3, x3_rows, C3, w3, C3, y, g.k, epilogue=L.EPI_F32_STATS, stats=stats)
+    else:
+        g3 = ops.ConvGeom(g.n, g.h, g.w, C3, g.k, g.r, g.s, g.stride, g.pad)
+        K = g.r * g.s * C3
+        ops.gemm(M, g.k, K, x3_rows, 0, w3, K, y, g.k, a_mode=L.OPND_CONV_FWD,
+                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3)
+
+
 def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None):
     """dx[N*H*W, C] = dgrad(dy) (+ add, bf16)."""
     g = geom
@@ -257,24 +342,43 @@ class StemFn(torch.autograd.Function):
         st, pad = conv.stride[0], conv.padding[0]
         Kp = ((C * R * S + 15) // 16) * 16
         xf = x.detach().float() if x.dtype != F32 else x.detach()
-        col, P, Q = ops.im2col_f32(xf, R, S, st, pad, Kp)
         wb = weight_bf16_rows(w, ld=Kp)
         Cout = w.shape[0]
+        x3 = _x3()
+        if x3:
+            col, P, Q = ops.im2col_f32_x3(xf, R, S, st, pad, Kp)  # [M][3 Kp] triple
+        else:
+            col, P, Q = ops.im2col_f32(xf, R, S, st, pad, Kp)
         M = B * P * Q
         y = _empty((M, Cout), BF16, x.device)
         stats = _empty((ops.stats_tiles(M), 2, Cout), F32, x.device)
-        ops.gemm(M, Cout, Kp, col, Kp, wb, Kp, y, Cout, epilogue=L.EPI_BF16_STATS, stats=stats)
-        bns = _BN(bn, M, Cout, x.device)
-        bns.forward_coeffs(stats)
         a = _empty((M, Cout), BF16, x.device)
-        ops.bn_apply(y, bns.scale, bns.shift, None, True, a, M, Cout)
-        out, am, P2, Q2 = ops.maxpool_fwd(a, B, P, Q, Cout)
+        bns = _BN(bn, M, Cout, x.device)
+        if x3:
+            yf = _empty((M, Cout), F32, x.device)
+            ops.gemm(M, Cout, 3 * Kp, col, 3 * Kp, weight_x3_rows(w, seg=Kp), 3 * Kp, yf, Cout,
+                     epilogue=L.EPI_F32_STATS, stats=stats)
+            bns.forward_coeffs(stats)
+            af = _empty((M, Cout), F32, x.device)
+            ops.bn_apply_x3(yf, bns.scale, bns.shift, None, 0, True, M, Cout, out_bf16=a,
+                            out_f32=af, y_bf16=y)
+            out3, out, am, P2, Q2 = ops.maxpool_fwd_x3(af, B, P, Q, Cout)
+        else:
+            ops.gemm(M, Cout, Kp, col, Kp, wb, Kp, y, Cout, epilogue=L.EPI_BF16_STATS,
+                     stats=stats)
+            bns.forward_coeffs(stats)
+            ops.bn_apply(y, bns.scale, bns.shift, None, True, a, M, Cout)
+            out, am, P2, Q2 = ops.maxpool_fwd(a, B, P, Q, Cout)
         ctx.mod = mod
         ctx.bns = bns
+        ctx.x3 = x3
         ctx.dims = (B, C, H, W, P, Q, P2, Q2, Cout, Kp, R, S, st, pad)
         ctx.x_requires_grad = x.requires_grad
         ctx.save_for_backward(col, y, a, am, wb)
-        return out.permute(0, 3, 1, 2)
+        res = out.permute(0, 3, 1, 2)
+        if x3:
+            res._dfu_x3 = out3
+        return res
 
     @staticmethod
     def backward(ctx, gout):
@@ -285,12 +389,16 @@ class StemFn(torch.autograd.Function):
         da = ops.maxpool_bwd(g, am, B, P, Q, Cout, P2, Q2).view(B * P * Q, Cout)
         M = B * P * Q
         dy = torch.empty_like(y)
-        ctx.bns.backward(da, y, None, 2, dy, None)
+        if ctx.x3:  # the forward's own ReLU mask (its pre-activation was fp32)
+            ctx.bns.backward(da, y, a, 1, dy, None)
+        else:
+            ctx.bns.backward(da, y, None, 2, dy, None)
         w = mod.conv1.weight
         if _wants(w):
             dw = grad_buffer(w).view(Cout, -1)
             K = C * R * S
-            ops.gemm(Cout, K, M, dy, Cout, col, Kp, dw, K, a_mode=L.OPND_MNMAJOR,
+            # bf16 im2col rows: the col itself, or the hi segment of the bf16x3 triple
+            ops.gemm(Cout, K, M, dy, Cout, col, col.stride(0), dw, K, a_mode=L.OPND_MNMAJOR,
                      b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
             grads_done(w)
         dx = None
@@ -319,6 +427,8 @@ class BottleneckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, *params_and_mod):
         mod = params_and_mod[-1]
+        x3mode = _x3()
+        xin3 = _take_x3(x) if x3mode else None
         x = nhwc_bf16(x.detach())
         B, Cin, H, W = x.shape
         dev = x.device
@@ -344,17 +454,55 @@ class BottleneckFn(torch.autograd.Function):
             ops.bn_apply(y, st.scale, st.shift, residual, relu, out, M, geom.k)
             return y, out, st
 
-        y1, a1, s1 = conv_bn(xr, g1, w1, mod.bn1, True)
-        y2, a2, s2 = conv_bn(a1, g2, w2, mod.bn2, True)
+        def conv_bn_x3(x3rows, geom, w3x, bnmod, relu, res=None, res_mode=0, want3=True,
+                       want_bf=True, want_f32=False):
+            """bf16x3: fp32 conv + BN (+res) (+ReLU) -> (y bf16, out bf16, out triple, out
+            fp32, BN state)."""
+            M = geom.n * geom.p * geom.q
+            yf = _empty((M, geom.k), F32, dev)
+            stats = _empty((ops.stats_tiles(M), 2, geom.k), F32, dev)
+            conv_fwd_x3(x3rows, geom, w3x, yf, stats)
+            st = _BN(bnmod, M, geom.k, dev)
+            st.forward_coeffs(stats)
+            y = _empty((M, geom.k), BF16, dev)
+            out = _empty((M, geom.k), BF16, dev) if want_bf else None
+            out3 = _empty((M, 3 * geom.k), BF16, dev) if want3 else None
+            of = _empty((M, geom.k), F32, dev) if want_f32 else None
+            ops.bn_apply_x3(yf, st.scale, st.shift, res, res_mode, relu, M, geom.k, out3=out3,
+                            out_bf16=out, out_f32=of, y_bf16=y)
+            return y, out, out3, of, st
+
+        out3 = None
+        if x3mode:
+            y1, a1, a1_3, _, s1 = conv_bn_x3(xin3, g1, conv_weight_x3(mod.conv1.weight),
+                                              mod.bn1, True)
+            y2, a2, a2_3, _, s2 = conv_bn_x3(a1_3, g2, conv_weight_x3(mod.conv2.weight),
+                                              mod.bn2, True)
+            del a1_3
+        else:
+            y1, a1, s1 = conv_bn(xr, g1, w1, mod.bn1, True)
+            y2, a2, s2 = conv_bn(a1, g2, w2, mod.bn2, True)
         if mod.downsample is not None:
             dconv, dbn = mod.downsample[0], mod.downsample[1]
             gd = _geom(dconv, B, H, W)
             wd = conv_weight_bf16(dconv.weight)
-            yd, idn, sd = conv_bn(xr, gd, wd, dbn, False)
+            if x3mode:
+                yd, _, _, idn, sd = conv_bn_x3(xin3, gd, conv_weight_x3(dconv.weight), dbn, False,
+                                               want3=False, want_bf=False, want_f32=True)
+                res, res_mode = idn, 1
+            else:
+                yd, idn, sd = conv_bn(xr, gd, wd, dbn, False)
         else:
             gd = wd = yd = sd = None
             idn = xr
-        y3, out, s3 = conv_bn(a2, g3, w3, mod.bn3, True, residual=idn)
+            res, res_mode = xin3, 2
+        if x3mode:
+            y3, out, out3, _, s3 = conv_bn_x3(a2_3, g3, conv_weight_x3(mod.conv3.weight),
+                                              mod.bn3, True, res=res, res_mode=res_mode)
+            del a2_3, res, xin3
+        else:
+            y3, out, s3 = conv_bn(a2, g3, w3, mod.bn3, True, residual=idn)
+        ctx.x3 = x3mode
         ctx.mod = mod
         ctx.geo = (g1, g2, g3, gd)
         ctx.bns = (s1, s2, s3, sd)
@@ -370,7 +518,10 @@ class BottleneckFn(torch.autograd.Function):
             mod._probes = ctx.probes
         ctx.save_for_backward(xr, y1, a1, y2, a2, y3, out, w1, w2, w3,
                               *( (yd, wd) if yd is not None else ()))
-        return from_rows(out, B, g3.p, g3.q, outc)
+        res = from_rows(out, B, g3.p, g3.q, outc)
+        if out3 is not None:
+            res._dfu_x3 = out3
+        return res
 
     @staticmethod
     def backward(ctx, gout):
@@ -406,8 +557,10 @@ class BottleneckFn(torch.autograd.Function):
             conv_wgrad(dy3, a2, g3, grad_buffer(mod.conv3.weight))
             grads_done(mod.conv3.weight)
         # bn2 + relu, conv2
+        # BN + ReLU masks: recomputed from y (bf16), or in bf16x3 mode (fp32 pre-activations)
+        # read from the forward's outputs
         dy2 = torch.empty_like(y2)
-        s2.backward(da2, y2, None, 2, dy2, None)
+        s2.backward(da2, y2, a2 if ctx.x3 else None, 1 if ctx.x3 else 2, dy2, None)
         da1 = torch.empty_like(a1)
         conv_dgrad(dy2, g2, w2, da1)
         if ctx.probes is not None:
@@ -417,7 +570,7 @@ class BottleneckFn(torch.autograd.Function):
             grads_done(mod.conv2.weight)
         # bn1 + relu, conv1 (+ identity gradient fused in the dgrad epilogue)
         dy1 = torch.empty_like(y1)
-        s1.backward(da1, y1, None, 2, dy1, None)
+        s1.backward(da1, y1, a1 if ctx.x3 else None, 1 if ctx.x3 else 2, dy1, None)
         dx = None
         if ctx.x_requires_grad:
             dxr = _empty((M1, Cin), BF16, dev)
@@ -438,10 +591,14 @@ class BottleneckFn(torch.autograd.Function):
 class AvgPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
+        x3 = _take_x3(x) if _x3() else None
         x = nhwc_bf16(x.detach())
         B, C, H, W = x.shape
         ctx.shape = (B, C, H, W)
-        y = ops.avgpool_fwd(rows_view(x), B, H * W, C)
+        if x3 is not None:
+            y = ops.avgpool_fwd_x3(x3, B, H * W, C)
+        else:
+            y = ops.avgpool_fwd(rows_view(x), B, H * W, C)
         return y.view(B, C, 1, 1)
 
     @staticmethod
@@ -463,12 +620,17 @@ class PatchEmbedFn(torch.autograd.Function):
         B, C, H, W = x.shape
         D = w.shape[0]
         xf = x.detach().float() if x.dtype != F32 else x.detach()
-        patches = ops.patchify_f32(xf, ps)
         T = (H // ps) * (W // ps)
         wb = weight_bf16_rows(w)
         K = wb.shape[1]
         X = _empty((B, T + 1, D), F32, x.device)
-        ops.gemm(B * T, D, K, patches, K, wb, K, X, D, epilogue=L.EPI_PATCH,
+        if _x3():  # [B*T][3K] triple; the backward reads its hi segment (row stride 3K)
+            patches = ops.patchify_f32_x3(xf, ps)
+            A, Bop, Kg = patches, weight_x3_rows(w), 3 * K
+        else:
+            patches = ops.patchify_f32(xf, ps)
+            A, Bop, Kg = patches, wb, K
+        ops.gemm(B * T, D, Kg, A, Kg, Bop, Kg, X, D, epilogue=L.EPI_PATCH,
                  bias=b.detach() if b is not None else None, aux=pos.detach().reshape(T + 1, D),
                  ldaux=D, ep_tokens=T)
         ops.vit_cls_rows(cls.detach().reshape(D), pos.detach().reshape(T + 1, D), X, B, T + 1, D)
@@ -490,8 +652,8 @@ class PatchEmbedFn(torch.autograd.Function):
                                    grad_buffer(b) if _wants(b) else None)
         if _wants(w):
             dw = grad_buffer(w).view(D, K)
-            ops.gemm(D, K, B * T, gpatch, D, patches, K, dw, K, a_mode=L.OPND_MNMAJOR,
-                     b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+            ops.gemm(D, K, B * T, gpatch, D, patches, patches.stride(0), dw, K,
+                     a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
         grads_done(w, b, cls, pos)
         dx = None
         if ctx.x_requires_grad:
@@ -567,6 +729,9 @@ class ViTBlockFn(torch.autograd.Function):
         wfc2 = weight_bf16_rows(mlp.fc2.weight)
         Dh = wfc1.shape[0]
         bias = lambda lin: lin.bias.detach() if lin.bias is not None else None  # noqa: E731
+        if _x3():
+            return ViTBlockFn._forward_x3(ctx, blk, x2, B, T, D, H, dh, rows, wqkv, wproj, wfc1,
+                                          wfc2, bias)
         # attention branch
         xn1 = _empty((rows, D), BF16, dev)
         m1, r1 = _ln_fwd(x2, blk.norm1, rows, D, xn1)
@@ -587,6 +752,52 @@ class ViTBlockFn(torch.autograd.Function):
         xo = _empty((B, T, D), F32, dev)
         ops.gemm(rows, D, Dh, h, Dh, wfc2, Dh, xo.view(rows, D), D, epilogue=L.EPI_F32_RESID,
                  bias=bias(mlp.fc2), aux=xm, ldaux=D)
+        ctx.blk = blk
+        ctx.dims = (B, T, D, H, dh, Dh)
+        ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv,
+                              wproj, wfc1, wfc2)
+        return xo
+
+    @staticmethod
+    def _forward_x3(ctx, blk, x2, B, T, D, H, dh, rows, wqkv, wproj, wfc1, wfc2, bias):
+        """bf16x3 forward: the four Linears on split-bf16 triples (K tripled), fp32 GEMM
+        outputs, fp32 attention; saves the same bf16 tensors as the bf16 forward."""
+        attn, mlp = blk.attn, blk.mlp
+        dev = x2.device
+        Dh = wfc1.shape[0]
+
+        def ln_x3(xsrc, norm):
+            t3 = _empty((rows, 3 * D), BF16, dev)
+            tb = _empty((rows, D), BF16, dev)
+            mean = _empty((rows,), F32, dev)
+            rstd = _empty((rows,), F32, dev)
+            ops.layernorm_fwd_x3(xsrc, D, rows, D, norm.weight, norm.bias, norm.eps, t3, tb, mean,
+                                 rstd)
+            return t3, tb, mean, rstd
+
+        xn1_3, xn1, m1, r1 = ln_x3(x2, blk.norm1)
+        qkvf = _empty((rows, 3 * D), F32, dev)
+        ops.gemm(rows, 3 * D, 3 * D, xn1_3, 3 * D, weight_x3_rows(attn.qkv.weight), 3 * D, qkvf,
+                 3 * D, epilogue=L.EPI_F32, bias=bias(attn.qkv))
+        del xn1_3
+        qkv = ops.cast_rows_bf16(qkvf)
+        o3, o, lse = ops.attention_fwd_f32(qkvf, B, T, H, dh, attn.scale)
+        del qkvf
+        xm = _empty((rows, D), F32, dev)
+        ops.gemm(rows, D, 3 * D, o3, 3 * D, weight_x3_rows(attn.proj.weight), 3 * D, xm, D,
+                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D)
+        del o3
+        xn2_3, xn2, m2, r2 = ln_x3(xm, blk.norm2)
+        hf = _empty((rows, Dh), F32, dev)
+        ops.gemm(rows, Dh, 3 * D, xn2_3, 3 * D, weight_x3_rows(mlp.fc1.weight), 3 * D, hf, Dh,
+                 epilogue=L.EPI_F32, bias=bias(mlp.fc1))
+        del xn2_3
+        h3, h, hpre = ops.gelu_x3(hf)
+        del hf
+        xo = _empty((B, T, D), F32, dev)
+        ops.gemm(rows, D, 3 * Dh, h3, 3 * Dh, weight_x3_rows(mlp.fc2.weight), 3 * Dh,
+                 xo.view(rows, D), D, epilogue=L.EPI_F32_RESID, bias=bias(mlp.fc2), aux=xm,
+                 ldaux=D)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv,

@@ -5,7 +5,11 @@ Each class subclasses its torch.nn counterpart so that parameters, buffers, init
 reference's loaders remap prefixes and call load_state_dict(strict=False),
 extended_metrics.py:40-92).  Only ``forward`` differs: it runs libdfu_hip kernels.
 """
+import itertools
+import os
+
 import torch
+import torch.distributed as dist
 import torch.nn as tnn
 
 from . import functional as Fn
@@ -145,12 +149,40 @@ class LayerNormFn(torch.autograd.Function):
         return gx.view(ctx.shape), None, None, None
 
 
+_M64 = (1 << 64) - 1
+_dropout_instances = itertools.count()
+
+
+def _splitmix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def _rank():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank()
+    return int(os.environ.get("RANK", "0"))
+
+
+def dropout_seed(instance, rank=None, base=None):
+    """64-bit key of one Dropout instance's mask stream: torch.initial_seed(), the instance's
+    creation index and the data-parallel rank, mixed by splitmix64.  The kernel's counter is
+    z = seed + golden * (offset + i), so distinct well-mixed keys give unrelated streams (two
+    layers of one head, or two ranks, never replay each other's masks)."""
+    base = int(torch.initial_seed()) if base is None else int(base)
+    rank = _rank() if rank is None else int(rank)
+    return _splitmix64(_splitmix64(_splitmix64(base & _M64) ^ instance) ^ rank)
+
+
 class Dropout(tnn.Dropout):
-    """Inverted dropout with a counter-based device RNG (graph-replay safe)."""
+    """Inverted dropout with a counter-based device RNG (graph-replay safe).  Each instance
+    draws its own stream (dropout_seed: torch seed x instance index x DP rank)."""
 
     def __init__(self, p=0.5, inplace=False):
         super().__init__(p, inplace)
-        self.seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFF
+        self.seed = dropout_seed(next(_dropout_instances))
         self.register_buffer("rng_offset", torch.zeros((), dtype=torch.int64), persistent=False)
 
     def forward(self, x):

@@ -67,7 +67,7 @@ def _algorithmic_bytes(d, conv):
          }.get(d.a_mode, 2 * M * K)
     b = act_in if d.b_mode == L.OPND_CONV_WGRAD_X else 2 * N * K
     e = d.epilogue
-    c = {L.EPI_F32: 4, L.EPI_F32_RESID: 8, L.EPI_F32_ACC: 8, L.EPI_PATCH: 4,
+    c = {L.EPI_F32: 4, L.EPI_F32_RESID: 8, L.EPI_F32_ACC: 8, L.EPI_PATCH: 4, L.EPI_F32_STATS: 4,
          L.EPI_BF16_GELU: 4, L.EPI_BF16_DGELU: 4, L.EPI_BF16_ADD: 4}.get(e, 2) * M * N
     return a + b + c
 
@@ -555,3 +555,112 @@ def argmax_rows(x):
     check(lib().dfu_argmax_rows(ptr(x), x.shape[0], x.shape[1], ptr(out), stream_ptr()),
           "dfu_argmax_rows")
     return out
+
+
+# --------------------------------------------------------------- bf16x3 (split) forward
+# csrc/precise.hip: a triple is bf16 [rows][3C] = [hi | lo | hi] (pattern 0, GEMM A operand)
+# or [hi | hi | lo] (pattern 1, GEMM B operand / weights), hi = bf16(x), lo = bf16(x - hi).
+X3_A, X3_B = 0, 1
+
+
+def split_x3(x, pattern, seg=None, hi_out=None):
+    """fp32 [rows, cols] (any row stride) -> triple [rows, 3*seg] (seg >= cols, zero-padded;
+    default cols rounded up to 8), optionally also the plain bf16 hi [rows, seg]."""
+    _req(x, F32, "split_x3")
+    x2 = x.reshape(x.shape[0], -1) if x.dim() != 2 else x
+    if x2.stride(1) != 1:
+        x2 = x2.contiguous()
+    rows, cols = x2.shape
+    seg = (cols + 7) // 8 * 8 if seg is None else int(seg)
+    out = torch.empty((rows, 3 * seg), dtype=BF16, device=x.device)
+    check(lib().dfu_split_x3(ptr(x2), x2.stride(0), rows, cols, seg, ptr(out), int(pattern),
+                             ptr(hi_out), seg if hi_out is None else hi_out.stride(0),
+                             stream_ptr()), "dfu_split_x3")
+    return out
+
+
+def pack_conv_weight_x3(w):
+    """fp32 OIHW -> bf16 KRSC' (C' = 3C, pattern 1)."""
+    _req(w, F32, "pack_conv_weight_x3")
+    K, C, R, S = w.shape
+    out = torch.empty((K, R, S, 3 * C), dtype=BF16, device=w.device)
+    check(lib().dfu_pack_conv_weight_x3(ptr(w.contiguous()), ptr(out), K, C, R, S, stream_ptr()),
+          "dfu_pack_conv_weight_x3")
+    return out
+
+
+def im2col_f32_x3(x, R, S, stride, pad, Kp):
+    _req(x, F32, "im2col_f32_x3")
+    B, C, H, W = x.shape
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - S) // stride + 1
+    out = torch.empty((B * P * Q, 3 * Kp), dtype=BF16, device=x.device)
+    sn, sc, sh, sw = x.stride()
+    check(lib().dfu_im2col_f32_x3(ptr(x), sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q,
+                                  ptr(out), Kp, stream_ptr()), "dfu_im2col_f32_x3")
+    return out, P, Q
+
+
+def patchify_f32_x3(x, ps):
+    _req(x, F32, "patchify_f32_x3")
+    B, C, H, W = x.shape
+    out = torch.empty((B * (H // ps) * (W // ps), 3 * C * ps * ps), dtype=BF16, device=x.device)
+    sn, sc, sh, sw = x.stride()
+    check(lib().dfu_patchify_f32_x3(ptr(x), sn, sc, sh, sw, B, C, H, W, ps, ptr(out),
+                                    stream_ptr()), "dfu_patchify_f32_x3")
+    return out
+
+
+def bn_apply_x3(y, scale, shift, residual, res_mode, relu, M, C, out3=None, out_bf16=None,
+                out_f32=None, y_bf16=None):
+    _req(y, F32, "bn_apply_x3")
+    check(lib().dfu_bn_apply_x3(ptr(y), ptr(scale), ptr(shift), ptr(residual), int(res_mode),
+                                int(relu), ptr(out3), ptr(out_bf16), ptr(out_f32), ptr(y_bf16),
+                                int(M), int(C), stream_ptr()), "dfu_bn_apply_x3")
+
+
+def maxpool_fwd_x3(x, B, H, W, C):
+    _req(x, F32, "maxpool_fwd_x3")
+    P = (H - 1) // 2 + 1
+    Q = (W - 1) // 2 + 1
+    y3 = torch.empty((B * P * Q, 3 * C), dtype=BF16, device=x.device)
+    y = torch.empty((B, P, Q, C), dtype=BF16, device=x.device)
+    am = torch.empty((B, P, Q, C), dtype=torch.uint8, device=x.device)
+    check(lib().dfu_maxpool_fwd_x3(ptr(x), B, H, W, C, ptr(y3), ptr(y), ptr(am), P, Q,
+                                   stream_ptr()), "dfu_maxpool_fwd_x3")
+    return y3, y, am, P, Q
+
+
+def avgpool_fwd_x3(x3, B, HW, C):
+    y = torch.empty((B, C), dtype=F32, device=x3.device)
+    check(lib().dfu_avgpool_fwd_x3(ptr(x3), B, HW, C, ptr(y), stream_ptr()), "dfu_avgpool_fwd_x3")
+    return y
+
+
+def layernorm_fwd_x3(x, ldx, rows, D, gamma, beta, eps, out3, out_bf16, mean, rstd):
+    check(lib().dfu_layernorm_fwd_x3(ptr(x), ldx, rows, D, ptr(gamma), ptr(beta), eps, ptr(out3),
+                                     ptr(out_bf16), ptr(mean), ptr(rstd), stream_ptr()),
+          "dfu_layernorm_fwd_x3")
+
+
+def gelu_x3(hpre):
+    rows, N = hpre.shape
+    h3 = torch.empty((rows, 3 * N), dtype=BF16, device=hpre.device)
+    h = torch.empty((rows, N), dtype=BF16, device=hpre.device)
+    hp = torch.empty((rows, N), dtype=BF16, device=hpre.device)
+    check(lib().dfu_gelu_x3(ptr(hpre), rows, N, ptr(h3), ptr(h), ptr(hp), stream_ptr()),
+          "dfu_gelu_x3")
+    return h3, h, hp
+
+
+def attention_fwd_f32(qkv, B, N, H, dh, scale):
+    """fp32 attention on fp32 qkv -> (o triple, o bf16, lse)."""
+    _req(qkv, F32, "attention_fwd_f32")
+    D = H * dh
+    o3 = torch.empty((B * N, 3 * D), dtype=BF16, device=qkv.device)
+    o = torch.empty((B * N, D), dtype=BF16, device=qkv.device)
+    npad = attention_npad(N)
+    lse = torch.empty((B * H, npad), dtype=F32, device=qkv.device)
+    check(lib().dfu_attention_fwd_f32(ptr(qkv), B, N, H, dh, scale, npad, ptr(o3), ptr(o),
+                                      ptr(lse), stream_ptr()), "dfu_attention_fwd_f32")
+    return o3, o, lse

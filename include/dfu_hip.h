@@ -60,7 +60,9 @@ enum dfu_epilogue {
   DFU_EPI_F32_ACC = 7,       /* C f32 += acc   (split-K: fp32 slabs + reduce, or atomics)   */
   DFU_EPI_F32_ACC_CONVW = 8, /* retired: conv wgrad accumulates KRSC + dfu_conv_grad_krsc... */
   DFU_EPI_BF16_STATS = 9,    /* C bf16 = acc; per-column (sum, M2) of each 128-row tile     */
-  DFU_EPI_PATCH = 10         /* ViT patch-embed: C f32 [B][T+1][N] row 1+p = acc+bias+pos   */
+  DFU_EPI_PATCH = 10,        /* ViT patch-embed: C f32 [B][T+1][N] row 1+p = acc+bias+pos   */
+  DFU_EPI_F32_STATS = 11     /* C f32 = acc; per-column (sum, M2) of each 128-row tile (the
+                                split-bf16 "bf16x3" forward: BN statistics of unrounded y)  */
 };
 
 typedef struct dfu_gemm_desc {
@@ -79,7 +81,7 @@ typedef struct dfu_gemm_desc {
   int64_t ldaux;
   void* aux_out;       /* GELU pre-activation output                            */
   int64_t ldaux_out;
-  float* stats;        /* DFU_EPI_BF16_STATS: [ceil(M/128)][2][N] fp32 (sum, M2)  */
+  float* stats;        /* DFU_EPI_{BF16,F32}_STATS: [ceil(M/128)][2][N] fp32 (sum, M2) */
   int32_t split_k;     /* F32_ACC only: 0 = auto (cost model), 1 = none, >1 fixed */
   int32_t ep_tokens;   /* DFU_EPI_PATCH: patches per image                      */
   /* implicit-GEMM convolution geometry (modes 2-5 and the CONVW epilogue)       */
@@ -318,6 +320,52 @@ int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_a
 int dfu_step_increment(int64_t* step_dev, void* stream);
 /* argmax over C for each row (torch.max(outputs, 1), :384) -> int64. */
 int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t* out, void* stream);
+
+/* ---------------------------------------------------------------- bf16x3 forward ---- */
+/* The "bf16x3" precision mode (csrc/precise.hip): the forward pass of the training step at
+ * fp32 accuracy on the bf16 MFMA GEMM, so the fusion logits meet north_star's 1e-3 bar against
+ * the reference's fp32 CPU path.  A contraction A.B^T runs as one GEMM over a tripled K with
+ * A3 = [hi(A) | lo(A) | hi(A)] ("pattern 0"), B3 = [hi(B) | hi(B) | lo(B)] ("pattern 1"),
+ * hi = bf16(x), lo = bf16(x - hi); a triple is bf16 [rows][3C].  GEMM outputs stay fp32
+ * (DFU_EPI_F32 / F32_RESID / F32_STATS / PATCH); the kernels below also write the plain bf16
+ * tensors the (bf16) backward pass saves.  Reference ops: the same as their bf16 twins above. */
+/* fp32 [rows][cols] (ld_in) -> triple [rows][3 seg] of `pattern`, seg >= cols (seg % 8 == 0,
+ * columns past cols zero); optional plain bf16 copy hi_out [rows][ld_hi >= seg]. */
+int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_t cols, int32_t seg,
+                 void* out, int32_t pattern, void* hi_out, int64_t ld_hi, void* stream);
+/* fp32 OIHW conv weight -> bf16 KRSC' with C' = 3C, pattern 1 along the channels. */
+int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int32_t C, int32_t R, int32_t S,
+                            void* stream);
+/* dfu_im2col_f32 / dfu_patchify_f32 writing the pattern-0 triple (row stride 3 Kp / 3 K). */
+int dfu_im2col_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
+                      int32_t C, int32_t H, int32_t W, int32_t R, int32_t S, int32_t stride,
+                      int32_t pad, int32_t P, int32_t Q, void* out, int32_t Kp, void* stream);
+int dfu_patchify_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
+                        int32_t C, int32_t H, int32_t W, int32_t ps, void* out, void* stream);
+/* BN apply on the fp32 conv output y: v = act(y*scale + shift (+ residual)); residual mode 0
+ * none, 1 fp32 [M][C], 2 triple [M][3C].  Optional outputs: out3 (triple), out_bf16, out_f32,
+ * y_bf16 (= bf16(y), the BN backward's input). */
+int dfu_bn_apply_x3(const float* y, const float* scale, const float* shift, const void* residual,
+                    int32_t res_mode, int32_t relu, void* out3, void* out_bf16, float* out_f32,
+                    void* y_bf16, int64_t M, int32_t C, void* stream);
+/* resnet maxpool 3x3/s2/p1 on fp32 NHWC -> triple, plain bf16 and uint8 argmax. */
+int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y3,
+                       void* y_bf16, uint8_t* argmax, int32_t P, int32_t Q, void* stream);
+/* AdaptiveAvgPool2d(1) on a triple [B*HW][3C] -> fp32 [B][C]. */
+int dfu_avgpool_fwd_x3(const void* x3, int32_t B, int32_t HW, int32_t C, float* y, void* stream);
+/* timm LayerNorm -> triple [rows][3D] + plain bf16 [rows][D]; mean / rstd per row. */
+int dfu_layernorm_fwd_x3(const float* x, int64_t ldx, int32_t rows, int32_t D,
+                         const float* gamma, const float* beta, float eps, void* out3,
+                         void* out_bf16, float* mean, float* rstd, void* stream);
+/* exact GELU of the fp32 fc1 output -> triple [rows][3N], bf16 h and bf16 pre-activation. */
+int dfu_gelu_x3(const float* hpre, int64_t rows, int32_t N, void* h3, void* h_bf16,
+                void* hpre_bf16, void* stream);
+/* fp32 softmax attention (SDPA) on fp32 qkv [B*N][3][H][dh] -> o triple [B*N][3*H*dh], o bf16,
+ * lse fp32 [B*H][npad] (as dfu_attention_fwd's: the bf16 backward's inputs).  dh == 64,
+ * N <= 208. */
+int dfu_attention_fwd_f32(const float* qkv, int32_t B, int32_t N, int32_t H, int32_t dh,
+                          float scale, int32_t npad, void* o3, void* o_bf16, float* lse,
+                          void* stream);
 
 /* ---------------------------------------------------------------- input pipeline ---- */
 /* The torchvision transforms of train_multimodal_fusion.py:172-205 on a decoded batch,

@@ -1,28 +1,25 @@
-"""Whole-model parity on the GPU: HIP fusion model vs the CPU oracle (oracle/torch_ref.py) on
-the identical synthetic batch and weights (train-mode BN, dropout identity).
+"""Whole-model parity on the GPU: the HIP fusion model vs the CPU oracle (oracle/torch_ref.py)
+on the identical synthetic batch and weights (train-mode BN, dropout identity).
 
-Oracle modes (SURVEY.md §7 "report both fp32-oracle and bf16-rounded-oracle deltas"):
-  * bf16-rounded oracle: fp32 arithmetic, bf16 rounding exactly where the HIP path stores bf16;
-  * fp32 oracle: the reference's own precision.
+north_star: "logits match the reference CPU path within 1e-3 abs bf16 on identical synthetic
+224x224 batches".  Measured at BASELINE config C3's size (B = 64), torchvision's default
+ResNet initialisation, train-mode BatchNorm:
 
-Tolerances.  north_star: "logits match the reference CPU path within 1e-3
-abs bf16".  Applied as written where bf16 storage allows it:
-  * the fusion head runs in exact fp32: tests/test_golden_gpu.py, rtol 1e-5 against the
-    reference's own head code;
-  * the RGB (ResNet-50) branch: swapping the HIP rgb features into the fp32 head moves the
-    logits by < 1e-3 (LOGIT_ATOL) from the fp32 oracle.
-For the whole model, bf16 storage of ViT weights and activations alone moves the fp32 oracle's
-logits by ~1.5-2.3e-3 (tools/precision_study.py: the error is spread over every rounding site,
-weights about half).  So the bar is the oracle's own bf16 band:
-  * HIP vs bf16-rounded oracle <= max(1e-3, 1.5 x |oracle(bf16, GPU) - oracle(bf16, CPU)|),
-    i.e. no worse than two realisations of the same bf16 algorithm;
-  * HIP vs fp32 oracle <= max(1e-3, 1.5 x max |oracle(bf16) - oracle(fp32)|).
-Conditioning: a randomly initialised ResNet-50 in train-mode BN amplifies perturbations ~35x,
-so test_logits_well_conditioned uses torchvision's ``zero_init_residual=True`` init (every
-block starts as the identity); test_default_init_noise_band checks the default init against
-the same oracle-vs-oracle band.
+  * precision "bf16x3" (dfu_hip.functional.precision; csrc/precise.hip): the forward pass at
+    fp32 accuracy on the same MFMA GEMMs (split-bf16 operands).  Asserted with the FIXED bar:
+    max |logits(HIP) - logits(fp32 oracle)| <= 1e-3 (LOGIT_ATOL, train_multimodal_fusion.py:
+    374-376), and the same for the loss.
+  * precision "bf16" (the default, benchmarked mode): bf16 storage alone moves the logits of the
+    fp32 oracle itself by more than 1e-3, so it is held to the oracle's own bf16
+    band: no further from the bf16-rounded oracle than two realisations of that oracle (CPU,
+    GPU) are from each other.  Its fp32-oracle delta is reported.
+
+Every measured delta is written to gpurun_out/parity_r03.json (DFU_PARITY_JSON overrides) and
+committed as profiles/r03_parity.json.
 """
 import copy
+import json
+import os
 
 import pytest
 import torch
@@ -32,6 +29,22 @@ from oracle import torch_ref as R
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 LOGIT_ATOL = 1e-3  # north_star: "logits match the reference CPU path within 1e-3 abs bf16"
+B_C3 = 64          # BASELINE.json C3: fusion bs=64
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PARITY_JSON = os.environ.get("DFU_PARITY_JSON",
+                             os.path.join(REPO, "gpurun_out", "parity_r03.json"))
+
+
+def _record(key, value):
+    """Merge one measurement into the parity JSON (created on first use)."""
+    os.makedirs(os.path.dirname(PARITY_JSON), exist_ok=True)
+    data = {}
+    if os.path.exists(PARITY_JSON):
+        with open(PARITY_JSON) as f:
+            data = json.load(f)
+    data[key] = value
+    with open(PARITY_JSON, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
 
 
 def _models(zero_init_residual=False, seed=0):
@@ -51,36 +64,59 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp(min=1e-12)).item()
 
 
-def _oracle(ref, rgb, th, y, w, emu, dev="cpu"):
+def _oracle(ref, rgb, th, y, w, emu, dev="cpu", backward=True):
     m = copy.deepcopy(ref).to(dev).train()
     R.set_bf16_emulation(emu)
     try:
-        fr = m.resnet(rgb.to(dev))
-        ft = m.vit(th.to(dev))
-        out = m.fusion(fr, ft)
-        loss = torch.nn.functional.cross_entropy(out, y.to(dev), weight=w.to(dev))
-        loss.backward()
+        with torch.set_grad_enabled(backward):
+            fr = m.resnet(rgb.to(dev))
+            ft = m.vit(th.to(dev))
+            out = m.fusion(fr, ft)
+            loss = torch.nn.functional.cross_entropy(out, y.to(dev), weight=w.to(dev))
+        if backward:
+            loss.backward()
     finally:
         R.set_bf16_emulation(False)
     return dict(m=m, fr=fr.detach().cpu(), ft=ft.detach().cpu(), out=out.detach().cpu(),
                 loss=loss.item())
 
 
-def _hip(hip, rgb, th, y, w):
+def _hip(hip, rgb, th, y, w, precision="bf16"):
+    from dfu_hip import functional as Fn
     from dfu_hip import nn as hnn
     hip.train()
-    fr = hip.resnet(rgb.to(DEV))
-    ft = hip.vit(th.to(DEV))
-    out = hip.fusion(fr, ft)
-    loss = hnn.CrossEntropyLoss(weight=w.to(DEV))(out, y.to(DEV))
-    loss.backward()
+    for p in hip.parameters():
+        p.grad = None
+    with Fn.precision(precision):
+        fr = hip.resnet(rgb.to(DEV))
+        ft = hip.vit(th.to(DEV))
+        out = hip.fusion(fr, ft)
+        loss = hnn.CrossEntropyLoss(weight=w.to(DEV))(out, y.to(DEV))
+        loss.backward()
     torch.cuda.synchronize()
-    return dict(m=hip, fr=fr.detach().cpu(), ft=ft.detach().cpu(), out=out.detach().float().cpu(),
-                loss=loss.item())
+    grads = {n: p.grad.detach().cpu().clone() for n, p in hip.named_parameters()}
+    return dict(fr=fr.detach().cpu(), ft=ft.detach().cpu(), out=out.detach().float().cpu(),
+                loss=loss.item(), grads=grads)
 
 
 def _maxd(a, b):
     return (a["out"] - b["out"]).abs().max().item()
+
+
+@pytest.fixture(scope="module")
+def c3():
+    """C3 at B=64, default (torchvision) init: fp32 oracle (fwd+bwd), bf16-rounded oracle
+    (fwd), HIP bf16x3 and HIP bf16 train steps on the identical batch and weights."""
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref, hip = _models()
+    rgb, th, y = R.synthetic_batch(B_C3, seed=42)
+    w = R.class_weights(y)
+    res = dict(f32=_oracle(ref, rgb, th, y, w, False),
+               emu=_oracle(ref, rgb, th, y, w, True),
+               emu_gpu=_oracle(ref, rgb, th, y, w, True, dev=DEV, backward=False),
+               x3=_hip(hip, rgb, th, y, w, "bf16x3"),
+               bf16=_hip(hip, rgb, th, y, w, "bf16"))
+    return res
 
 
 def test_state_dict_keys_match_reference_surface():
@@ -89,67 +125,95 @@ def test_state_dict_keys_match_reference_surface():
     assert sum(p.numel() for p in hip.parameters()) == 110_750_018
 
 
-def test_logits_well_conditioned():
+def test_c3_logits_bf16x3_within_1e3_of_fp32_oracle(c3):
+    """The north-star bar as written, at C3's batch: |logits - fp32 oracle| <= 1e-3 abs."""
+    f32, h = c3["f32"], c3["x3"]
+    d = _maxd(h, f32)
+    dl = abs(h["loss"] - f32["loss"])
+    print(f"\n[C3 B={B_C3} bf16x3] |logits|max={f32['out'].abs().max().item():.3e}  "
+          f"max|d logits| vs fp32 oracle = {d:.3e} (bar {LOGIT_ATOL}); loss {h['loss']:.6f} vs "
+          f"{f32['loss']:.6f}; rgb feat rel {rel(h['fr'], f32['fr']):.2e}, thermal feat rel "
+          f"{rel(h['ft'], f32['ft']):.2e}")
+    _record("c3_b64_bf16x3", {"max_abs_logits_vs_fp32_oracle": d, "abs_loss_vs_fp32_oracle": dl,
+                              "rgb_feat_rel": rel(h["fr"], f32["fr"]),
+                              "thermal_feat_rel": rel(h["ft"], f32["ft"]),
+                              "max_abs_logit": f32["out"].abs().max().item(),
+                              "bar": LOGIT_ATOL, "batch": B_C3, "init": "torchvision default"})
+    assert d <= LOGIT_ATOL
+    assert dl <= LOGIT_ATOL
+
+
+def test_c3_grads_bf16x3_vs_fp32_oracle(c3):
+    """Parameter gradients of the bf16x3 step against the fp32 oracle.  Its backward is the
+    bf16 one, so every parameter is held to the bf16-rounded oracle's own distance from the
+    fp32 oracle (relative L2, x1.5 + 1e-2).  (The head's gradients are not held tighter: the
+    few-1e-4 feature differences of the chaotic default-init ResNet flip a handful of the
+    64 x 512 head ReLU masks; the head's own arithmetic is pinned to the reference's code at
+    rtol 1e-5 by tests/test_golden_gpu.py.)"""
+    f32, emu, h = c3["f32"], c3["emu"], c3["x3"]
+    rp = dict(f32["m"].named_parameters())
+    re = dict(emu["m"].named_parameters())
+    errs = sorted(((rel(g, rp[n].grad), rel(re[n].grad, rp[n].grad), n)
+                   for n, g in h["grads"].items()), reverse=True)
+    for e, b, n in errs[:6]:
+        print(f"  grad rel err vs fp32 oracle {n}: {e:.3e} (bf16 oracle: {b:.3e})")
+    _record("c3_b64_bf16x3_grads", {"worst": [[n, e, b] for e, b, n in errs[:10]],
+                                    "median": errs[len(errs) // 2][0],
+                                    "columns": "param, HIP bf16x3 rel err, bf16 oracle rel err"})
+    for e, b, n in errs:
+        assert e <= 1.5 * b + 1e-2, (n, e, b)
+
+
+def test_c3_logits_bf16_within_oracle_band(c3):
+    """Default bf16 precision: within the oracle's own bf16 band (see module docstring)."""
+    f32, emu, emu_gpu, h = c3["f32"], c3["emu"], c3["emu_gpu"], c3["bf16"]
+    band = _maxd(emu_gpu, emu)
+    d_emu, d_f32 = _maxd(h, emu), _maxd(h, f32)
+    q_gap = max(_maxd(emu, f32), _maxd(emu_gpu, f32))
+    print(f"\n[C3 B={B_C3} bf16] max|d logits| HIP vs bf16-rounded oracle {d_emu:.3e} (oracle "
+          f"CPU-vs-GPU band {band:.3e}); HIP vs fp32 oracle {d_f32:.3e} (bf16 oracle vs fp32 "
+          f"oracle {q_gap:.3e})")
+    _record("c3_b64_bf16", {"max_abs_logits_vs_bf16_oracle": d_emu,
+                            "max_abs_logits_vs_fp32_oracle": d_f32,
+                            "oracle_bf16_cpu_vs_gpu_band": band,
+                            "oracle_bf16_vs_fp32_gap": q_gap})
+    assert d_emu <= 2 * band + LOGIT_ATOL
+    assert d_f32 <= 2 * q_gap + LOGIT_ATOL
+
+
+def test_well_conditioned_b8_grads_within_oracle_band():
+    """torchvision zero_init_residual=True (every block starts as the identity), B=8, bf16:
+    per-parameter gradients within the bf16 oracle's own band, BN running stats as torch."""
     B = 8
     ref, hip = _models(zero_init_residual=True)
     rgb, th, y = R.synthetic_batch(B, seed=42)
     w = R.class_weights(y)
     emu = _oracle(ref, rgb, th, y, w, True)
-    emu_gpu = _oracle(ref, rgb, th, y, w, True, dev=DEV)  # second bf16 realisation
+    emu_gpu = _oracle(ref, rgb, th, y, w, True, dev=DEV)
     f32 = _oracle(ref, rgb, th, y, w, False)
     h = _hip(hip, rgb, th, y, w)
-    band = _maxd(emu_gpu, emu)
-    q_gap = max(_maxd(emu, f32), _maxd(emu_gpu, f32))
-    head = copy.deepcopy(f32["m"].fusion).eval()
-    with torch.no_grad():
-        rgb_only = (head(h["fr"], f32["ft"]) - head(f32["fr"], f32["ft"])).abs().max().item()
-    print(f"\n[well-conditioned B={B}] |logits|max={f32['out'].abs().max().item():.3e}")
-    print(f"  logits max|d| HIP vs bf16-rounded oracle = {_maxd(h, emu):.3e} "
-          f"(oracle GPU-vs-CPU bf16 band {band:.3e})")
-    print(f"  logits max|d| HIP vs fp32 oracle         = {_maxd(h, f32):.3e} "
-          f"(bf16 oracle vs fp32 oracle up to {q_gap:.3e})")
-    print(f"  logits max|d| RGB branch only vs fp32    = {rgb_only:.3e} (bar {LOGIT_ATOL})")
-    print(f"  loss HIP {h['loss']:.6f} bf16-oracle {emu['loss']:.6f} fp32-oracle {f32['loss']:.6f}")
-    assert rgb_only < LOGIT_ATOL
-    assert _maxd(h, emu) <= max(LOGIT_ATOL, 1.5 * band)
-    assert _maxd(h, f32) <= max(LOGIT_ATOL, 1.5 * q_gap)
-    assert abs(h["loss"] - f32["loss"]) <= max(LOGIT_ATOL, 1.5 * abs(emu["loss"] - f32["loss"]))
-    # parameter gradients: within the oracle's own bf16 band, parameter by parameter
+    x3 = _hip(_models(zero_init_residual=True)[1], rgb, th, y, w, "bf16x3")
+    print(f"\n[well-conditioned B={B}] bf16: vs bf16 oracle {_maxd(h, emu):.3e} (band "
+          f"{_maxd(emu_gpu, emu):.3e}), vs fp32 oracle {_maxd(h, f32):.3e}; bf16x3 vs fp32 "
+          f"oracle {_maxd(x3, f32):.3e}")
+    _record("b8_zero_init", {"bf16_vs_bf16_oracle": _maxd(h, emu),
+                             "bf16_vs_fp32_oracle": _maxd(h, f32),
+                             "bf16x3_vs_fp32_oracle": _maxd(x3, f32),
+                             "oracle_band": _maxd(emu_gpu, emu)})
+    assert _maxd(x3, f32) <= LOGIT_ATOL
     rp = dict(emu["m"].named_parameters())
     rg = dict(emu_gpu["m"].named_parameters())
     worst = []
-    for n, p in hip.named_parameters():
-        e, b = rel(p.grad, rp[n].grad), rel(rg[n].grad, rp[n].grad)
+    for n, g in h["grads"].items():
+        e, b = rel(g, rp[n].grad), rel(rg[n].grad, rp[n].grad)
         worst.append((e - 2 * b, e, b, n))
     worst.sort(reverse=True)
     for _, e, b, n in worst[:6]:
         print(f"  grad rel err vs bf16 oracle {n}: {e:.3e} (oracle band {b:.3e})")
     assert worst[0][0] <= 1e-2, worst[0]
-    # running statistics updated like torch's BatchNorm2d in train mode
     rb = dict(emu["m"].named_buffers())
     for n, b in hip.named_buffers():
         if n.endswith("num_batches_tracked"):
             assert b.item() == rb[n].item() == 1
         elif "running" in n:
             assert rel(b, rb[n]) < 2e-2, n
-
-
-def test_default_init_noise_band():
-    B = 4
-    ref, hip = _models()
-    rgb, th, y = R.synthetic_batch(B, seed=42)
-    w = R.class_weights(y)
-    cpu = _oracle(ref, rgb, th, y, w, True)
-    gpu = _oracle(ref, rgb, th, y, w, True, dev=DEV)  # a second bf16 realisation of the oracle
-    f32 = _oracle(ref, rgb, th, y, w, False)
-    h = _hip(hip, rgb, th, y, w)
-    band = _maxd(gpu, cpu)
-    print(f"\n[default init B={B}] oracle-vs-oracle bf16 band: logits {band:.3e}, "
-          f"rgb feat {rel(gpu['fr'], cpu['fr']):.3e}, thermal feat {rel(gpu['ft'], cpu['ft']):.3e}")
-    print(f"  HIP vs bf16 oracle: logits {_maxd(h, cpu):.3e}, rgb feat {rel(h['fr'], cpu['fr']):.3e},"
-          f" thermal feat {rel(h['ft'], cpu['ft']):.3e}")
-    print(f"  HIP vs fp32 oracle: logits {_maxd(h, f32):.3e}; bf16 oracle vs fp32 oracle: "
-          f"{_maxd(cpu, f32):.3e}")
-    assert _maxd(h, cpu) <= 2 * band + LOGIT_ATOL
-    assert rel(h["fr"], cpu["fr"]) <= 2 * rel(gpu["fr"], cpu["fr"]) + 1e-3
-    assert rel(h["ft"], cpu["ft"]) <= 2 * rel(gpu["ft"], cpu["ft"]) + 1e-3

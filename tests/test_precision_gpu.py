@@ -1,0 +1,199 @@
+"""bf16x3 ("split-bf16") forward kernels (csrc/precise.hip) against plain PyTorch fp32.
+
+Each kernel of the fp32-accurate forward mode is checked against the fp32 op it replaces: the
+split itself (hi + lo reconstructs x to 2^-17), GEMMs over triples (fp32-grade products), the
+F32_STATS epilogue (fp32 output + the BN tile statistics), BN apply with both residual forms,
+maxpool / avgpool, LayerNorm, exact GELU and fp32 softmax attention.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ops():
+    from dfu_hip import _lib as L
+    from dfu_hip import ops
+    return L, ops
+
+
+def _trip(t3, C):
+    """hi + lo of a pattern-0 triple [rows][3C] and its two hi copies."""
+    t = t3.float()
+    return t[:, :C] + t[:, C:2 * C], t[:, :C], t[:, 2 * C:]
+
+
+def test_split_x3_patterns_and_padding():
+    L, ops = _ops()
+    torch.manual_seed(0)
+    x = torch.randn(37, 147, device=DEV) * 3.0
+    a = ops.split_x3(x, ops.X3_A, seg=160)
+    b = ops.split_x3(x, ops.X3_B, seg=160)
+    assert a.shape == (37, 480) and b.shape == (37, 480)
+    af, bf = a.float(), b.float()
+    hi = x.to(torch.bfloat16).float()
+    # pattern A: hi | lo | hi ; pattern B: hi | hi | lo ; columns 147..159 of each segment zero
+    for seg in (af[:, 0:160], af[:, 320:480], bf[:, 0:160], bf[:, 160:320]):
+        assert torch.equal(seg[:, :147], hi) and torch.all(seg[:, 147:] == 0)
+    recon = af[:, :147] + af[:, 160:307]
+    assert torch.equal(bf[:, 320:467], af[:, 160:307])
+    assert ((recon - x).abs() <= x.abs() * 2.0 ** -16).all()
+
+
+def test_pack_conv_weight_x3():
+    L, ops = _ops()
+    w = torch.randn(64, 32, 3, 3, device=DEV)
+    p = ops.pack_conv_weight_x3(w).float()  # [K][R][S][3C]
+    krsc = w.permute(0, 2, 3, 1)
+    hi = krsc.to(torch.bfloat16).float()
+    assert torch.equal(p[..., :32], hi) and torch.equal(p[..., 32:64], hi)
+    assert ((p[..., :32] + p[..., 64:] - krsc).abs() <= krsc.abs() * 2.0 ** -16).all()
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 768, 768), (1000, 384, 3072), (333, 200, 160)])
+def test_gemm_over_triples_is_fp32_accurate(M, N, K):
+    """A3 . B3^T on the bf16 MFMA GEMM equals fp32 A . B^T to ~1e-5 relative (bf16: ~4e-3)."""
+    L, ops = _ops()
+    torch.manual_seed(1)
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(N, K, device=DEV)
+    ref = (A.double() @ B.double().T)
+    A3, B3 = ops.split_x3(A, ops.X3_A), ops.split_x3(B, ops.X3_B)
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(M, N, 3 * K, A3, 3 * K, B3, 3 * K, C, N, epilogue=L.EPI_F32)
+    err = ((C.double() - ref).norm() / ref.norm()).item()
+    Cb = torch.empty(M, N, device=DEV)
+    ops.gemm(M, N, K, A.to(torch.bfloat16), K, B.to(torch.bfloat16), K, Cb, N, epilogue=L.EPI_F32)
+    errb = ((Cb.double() - ref).norm() / ref.norm()).item()
+    print(f"\n[x3 gemm {M}x{N}x{K}] rel err {err:.2e} (plain bf16 {errb:.2e})")
+    assert err < 2e-5 and errb > 20 * err
+
+
+@pytest.mark.parametrize("tile", [1, 2])
+def test_f32_stats_epilogue(tile):
+    """fp32 output + per-128-row (sum, M2) of the unrounded accumulators, both tiles that
+    instantiate it; an implicit-GEMM conv forward over a channel-tripled input too."""
+    L, ops = _ops()
+    torch.manual_seed(2)
+    M, N, K = 1000, 256, 192
+    A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    B = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    C = torch.empty(M, N, device=DEV)
+    st = torch.empty(ops.stats_tiles(M), 2, N, device=DEV)
+    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_F32_STATS, stats=st, tile=tile)
+    ref = A.float() @ B.float().T
+    assert torch.allclose(C, ref, rtol=1e-5, atol=1e-4)
+    for t in range(ops.stats_tiles(M)):
+        blk = C[t * 128:(t + 1) * 128].double()
+        s = blk.sum(0)
+        q = ((blk - blk.mean(0)) ** 2).sum(0)
+        assert torch.allclose(st[t, 0].double(), s, rtol=1e-5, atol=1e-3)
+        assert torch.allclose(st[t, 1].double(), q, rtol=1e-4, atol=1e-2)
+
+
+def test_conv_fwd_x3_matches_fp32_conv():
+    from dfu_hip import functional as Fn
+    L, ops = _ops()
+    torch.manual_seed(3)
+    Bn, C, H, W, Kout = 4, 64, 14, 14, 128
+    x = torch.randn(Bn, C, H, W, device=DEV)
+    w = torch.randn(Kout, C, 3, 3, device=DEV) * 0.05
+    for stride in (1, 2):
+        g = ops.ConvGeom(Bn, H, W, C, Kout, 3, 3, stride, 1)
+        x3 = ops.split_x3(x.permute(0, 2, 3, 1).reshape(-1, C), ops.X3_A)
+        y = torch.empty(Bn * g.p * g.q, Kout, device=DEV)
+        st = torch.empty(ops.stats_tiles(y.shape[0]), 2, Kout, device=DEV)
+        Fn.conv_fwd_x3(x3, g, Fn.conv_weight_x3(w), y, st)
+        ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=stride, padding=1)
+        ref = ref.permute(0, 2, 3, 1).reshape(-1, Kout)
+        err = ((y.double() - ref).norm() / ref.norm()).item()
+        assert err < 2e-5, (stride, err)
+
+
+def test_bn_apply_x3_residual_modes():
+    L, ops = _ops()
+    torch.manual_seed(4)
+    M, C = 3000, 256
+    y = torch.randn(M, C, device=DEV)
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV)
+    res = torch.randn(M, C, device=DEV)
+    res3 = ops.split_x3(res, ops.X3_A)
+    for mode, r in ((0, None), (1, res), (2, res3)):
+        out3 = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=DEV)
+        ob = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+        of = torch.empty(M, C, device=DEV)
+        yb = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+        ops.bn_apply_x3(y, sc, sh, r, mode, True, M, C, out3=out3, out_bf16=ob, out_f32=of,
+                        y_bf16=yb)
+        ref = y * sc + sh + (res if mode else 0)
+        ref = ref.clamp_min(0)
+        tol = 2e-6 if mode != 2 else 2e-5  # the triple residual carries 16 mantissa bits
+        assert torch.allclose(of, ref, rtol=tol, atol=tol), mode
+        v, h0, h2 = _trip(out3, C)
+        assert ((v - of).abs() <= of.abs() * 2.0 ** -16).all() and torch.equal(h0, h2)
+        assert torch.equal(ob.float(), of.to(torch.bfloat16).float())
+        assert torch.equal(yb, y.to(torch.bfloat16))
+
+
+def test_maxpool_and_avgpool_x3():
+    L, ops = _ops()
+    torch.manual_seed(5)
+    B, H, W, C = 2, 112, 112, 64
+    x = torch.randn(B, H, W, C, device=DEV)
+    y3, yb, am, P, Q = ops.maxpool_fwd_x3(x.reshape(-1, C), B, H, W, C)
+    ref = torch.nn.functional.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    v, _, _ = _trip(y3, C)
+    assert torch.allclose(v.view(B, P, Q, C), ref, rtol=2e-5, atol=0)
+    assert torch.equal(yb.float(), ref.to(torch.bfloat16).float())
+    # avgpool over a triple
+    t = torch.randn(B * 49, 2048, device=DEV)
+    t3 = ops.split_x3(t, ops.X3_A)
+    a = ops.avgpool_fwd_x3(t3, B, 49, 2048)
+    assert torch.allclose(a, t.view(B, 49, 2048).mean(1), rtol=1e-5, atol=1e-6)
+
+
+def test_layernorm_and_gelu_x3():
+    L, ops = _ops()
+    torch.manual_seed(6)
+    rows, D = 1000, 768
+    x = torch.randn(rows, D, device=DEV) * 2 + 0.5
+    g = torch.randn(D, device=DEV)
+    b = torch.randn(D, device=DEV)
+    o3 = torch.empty(rows, 3 * D, dtype=torch.bfloat16, device=DEV)
+    ob = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    ops.layernorm_fwd_x3(x, D, rows, D, g, b, 1e-6, o3, ob, mean, rstd)
+    ref = torch.nn.functional.layer_norm(x.double(), (D,), g.double(), b.double(), 1e-6)
+    v, _, _ = _trip(o3, D)
+    assert ((v.double() - ref).abs().max() / ref.abs().max()).item() < 2e-5
+    h = torch.randn(rows, 3072, device=DEV) * 3
+    h3, hb, hp = ops.gelu_x3(h)
+    refg = torch.nn.functional.gelu(h.double())
+    v, _, _ = _trip(h3, 3072)
+    assert (v.double() - refg).abs().max().item() < 1e-5 * 9
+    assert torch.equal(hp, h.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("N", [197, 50])
+def test_attention_fwd_f32_matches_sdpa(N):
+    L, ops = _ops()
+    torch.manual_seed(7)
+    B, H, dh = 3, 12, 64
+    D = H * dh
+    qkv = torch.randn(B * N, 3 * D, device=DEV) * 2
+    o3, ob, lse = ops.attention_fwd_f32(qkv, B, N, H, dh, dh ** -0.5)
+    q, k, v = qkv.double().view(B, N, 3, H, dh).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * dh ** -0.5
+    ref = (s.softmax(-1) @ v).permute(0, 2, 1, 3).reshape(B * N, D)
+    o, _, _ = _trip(o3, D)
+    err = (o.double() - ref).abs().max().item()
+    print(f"\n[attn f32 N={N}] max abs err {err:.2e} (max |o| {ref.abs().max().item():.2f})")
+    assert err < 2.0 ** -16 * ref.abs().max().item()  # the triple's 16 mantissa bits
+    assert torch.equal(ob, o3[:, :D])  # the plain bf16 o is the triple's hi segment
+    lref = torch.logsumexp(s, -1).reshape(B * H, N)
+    assert torch.allclose(lse[:, :N].double(), lref, atol=1e-5)
