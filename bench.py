@@ -72,20 +72,16 @@ def synthetic(B, device, seed):
 
 
 def build(config, device):
-    import torch.nn as tnn
-    from models import encoders
     from models.fusion import MultimodalFusionModel
-    from dfu_hip import nn as hnn
+    from models.single import RGBOnlyModel, ThermalOnlyModel
     if config == "fusion":
         model = MultimodalFusionModel(num_classes=2, dropout=0.7)
         fwd = lambda m, r, t: m(r, t)  # noqa: E731
     elif config == "thermal":  # train_thermal_only.py:188-205
-        model = encoders.vit_base_patch16_224(num_classes=2)
-        model.head = tnn.Sequential(hnn.Dropout(0.5), hnn.Linear(768, 2))
+        model = ThermalOnlyModel(num_classes=2)
         fwd = lambda m, r, t: m(t)  # noqa: E731
     else:  # train_rgb_only.py:200-217
-        model = encoders.resnet50()
-        model.fc = tnn.Sequential(hnn.Dropout(0.5), hnn.Linear(2048, 2))
+        model = RGBOnlyModel(num_classes=2)
         fwd = lambda m, r, t: m(r)  # noqa: E731
     return model.to(device).train(), fwd
 

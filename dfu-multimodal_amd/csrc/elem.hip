@@ -535,6 +535,32 @@ inline unsigned grid_for(int64_t n) {
   return (unsigned)(b < 1 ? 1 : b);
 }
 
+// Per-step training metrics kept on the device (train_multimodal_fusion.py:383-388 does
+// loss.item(), torch.max(outputs, 1) and .cpu() every step): confusion[label][argmax] += 1 per
+// row (first maximum wins, as torch.max) and, from one lane, loss_sum += loss, batches += 1.
+// Integer atomics and a single-lane fp64 add: the totals are exact and order-independent.
+__global__ void k_metrics_accumulate(const float* __restrict__ logits,
+                                     const int64_t* __restrict__ labels, int rows, int C,
+                                     const float* __restrict__ loss,
+                                     unsigned long long* __restrict__ confusion,
+                                     double* __restrict__ loss_sum,
+                                     unsigned long long* __restrict__ batches) {
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += gridDim.x * blockDim.x) {
+    int best = 0;
+    float bv = logits[(int64_t)r * C];
+    for (int c = 1; c < C; ++c) {
+      const float v = logits[(int64_t)r * C + c];
+      if (v > bv) { bv = v; best = c; }
+    }
+    const int64_t y = labels[r];
+    if (y >= 0 && y < C) atomicAdd(confusion + y * C + best, 1ull);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (loss) *loss_sum += (double)*loss;
+    *batches += 1ull;
+  }
+}
+
 }  // namespace
 
 #define LAUNCH(kern, n, stream, ...)                                                     \
@@ -781,5 +807,17 @@ extern "C" int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t*
                                void* stream) {
   DFU_CHECK_ARG(x && out && rows > 0 && C > 0, "dfu_argmax_rows: bad args");
   LAUNCH(k_argmax_rows, (int64_t)rows, stream, x, rows, C, out);
+  return DFU_OK;
+}
+
+extern "C" int dfu_metrics_accumulate(const float* logits, const int64_t* labels, int32_t rows,
+                                      int32_t C, const float* loss, int64_t* confusion,
+                                      double* loss_sum, int64_t* batches, void* stream) {
+  DFU_CHECK_ARG(logits && labels && confusion && loss_sum && batches && rows > 0 && C > 0,
+                "dfu_metrics_accumulate: bad args");
+  hipLaunchKernelGGL(k_metrics_accumulate, dim3(1), dim3(256), 0, (hipStream_t)stream, logits,
+                     labels, rows, C, loss, (unsigned long long*)confusion, loss_sum,
+                     (unsigned long long*)batches);
+  DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -384,3 +384,50 @@ class GpuPairLoader:
                       else AugParams())
         y = torch.tensor(labels, dtype=torch.long).to(self.device, non_blocking=True)
         return self.rgb(rgb, rp), self.thermal(th, tp), y
+
+
+class GpuImageLoader:
+    """DataLoader replacement for the single-modality datasets (data.single_modality:
+    RGBDataset, train_rgb_only.py:181-197; ThermalDataset): yields (images, labels) already on
+    the GPU, fp32 NCHW, through the same decode-ahead threads and HIP transform kernels as
+    GpuPairLoader.  `spec` defaults to the RGB train / val-test transform of
+    train_rgb_only.py:102-118 (the fusion script's RGB transforms, identical); the thermal-only
+    script's train transform adds a GaussianBlur this pipeline does not implement, so a thermal
+    loader takes `thermal_val_test_transform` (or a spec without blur)."""
+
+    def __init__(self, dataset, batch_size, sampler=None, shuffle=False, train=False,
+                 spec=None, device="cuda", num_threads=4, generator=None, drop_last=False):
+        self.dataset = dataset
+        self.batch_size = batch_size
+        self.sampler = sampler
+        self.shuffle = shuffle
+        self.generator = generator
+        self.drop_last = drop_last
+        spec = spec or (rgb_train_transform if train else rgb_val_test_transform)
+        self.pre = GpuPreprocessor(spec, device)
+        self.device = torch.device(device)
+        self.num_threads = num_threads
+
+    _batches = GpuPairLoader._batches
+    __len__ = GpuPairLoader.__len__
+
+    def _decode(self, pool, idx):
+        imgs = pool.map(decode_rgb, [self.dataset.image_paths[i] for i in idx])
+        return list(imgs), [self.dataset.labels[i] for i in idx]
+
+    def __iter__(self):
+        with ThreadPoolExecutor(self.num_threads) as pool, ThreadPoolExecutor(1) as ahead:
+            pending = None
+            for idx in self._batches():
+                nxt = ahead.submit(self._decode, pool, idx)
+                if pending is not None:
+                    yield self._finish(*pending.result())
+                pending = nxt
+            if pending is not None:
+                yield self._finish(*pending.result())
+
+    def _finish(self, imgs, labels):
+        params = [sample_params(self.pre.spec, self.generator) if self.pre.spec.random
+                  else AugParams() for _ in labels]
+        y = torch.tensor(labels, dtype=torch.long).to(self.device, non_blocking=True)
+        return self.pre(imgs, params), y

@@ -119,6 +119,7 @@ PROTOTYPES = {
     "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P],
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
+    "dfu_metrics_accumulate": [P, P, I32, I32, P, P, P, P, P],
     "dfu_split_x3": [P, I64, I32, I32, I32, P, I32, P, I64, P],
     "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, P],
     "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],

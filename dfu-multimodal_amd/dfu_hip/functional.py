@@ -21,6 +21,7 @@ Conventions:
     (the producer of every such tensor is a Function in this file).
 """
 import math
+import weakref
 
 import torch
 
@@ -754,6 +755,7 @@ class ViTBlockFn(torch.autograd.Function):
                  bias=bias(mlp.fc2), aux=xm, ldaux=D)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
+        ctx.out_ref = weakref.ref(xo)
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
@@ -800,6 +802,7 @@ class ViTBlockFn(torch.autograd.Function):
                  ldaux=D)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
+        ctx.out_ref = weakref.ref(xo)
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
@@ -816,8 +819,16 @@ class ViTBlockFn(torch.autograd.Function):
         g = gout.contiguous()
         if g.dtype != F32:
             g = g.float()
+        # The LayerNorm backwards below update the residual-stream gradient IN PLACE.  That is
+        # safe for a gradient only this Function sees (another block's or TokenNormFn's
+        # output); when the block output carries a tensor hook or retain_grad (Grad-CAM's
+        # 'blocks.*' hooks, user code), the hook may hold that very tensor: work on a copy.
+        out = ctx.out_ref()
+        if g is gout and out is not None and (out.retains_grad or getattr(out, "_backward_hooks",
+                                                                           None)):
+            g = g.clone()
         g2 = g.view(rows, D)
-        gb = _bf16_of_grad(g).view(rows, D)
+        gb = _bf16_of_grad(gout if gout.dtype == F32 else g).view(rows, D)
         # ---- MLP branch: x_out = x_mid + fc2(gelu(fc1(norm2(x_mid))))
         dh_pre = _empty((rows, Dh), BF16, dev)
         ops.gemm(rows, Dh, D, gb, D, wfc2, Dh, dh_pre, Dh, b_mode=L.OPND_MNMAJOR,
@@ -825,7 +836,7 @@ class ViTBlockFn(torch.autograd.Function):
         if _wants(mlp.fc2.weight):
             _linear_wgrad(gb, h, mlp.fc2.weight, rows)
         if _wants(mlp.fc2.bias):
-            _colsum_of_grad(g, grad_buffer(mlp.fc2.bias))
+            _colsum_of_grad(gout if gout.dtype == F32 else g, grad_buffer(mlp.fc2.bias))
         grads_done(mlp.fc2.weight, mlp.fc2.bias)
         dxn2 = _empty((rows, D), BF16, dev)
         ops.gemm(rows, D, Dh, dh_pre, Dh, wfc1, D, dxn2, D, b_mode=L.OPND_MNMAJOR,

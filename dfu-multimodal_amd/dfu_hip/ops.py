@@ -664,3 +664,20 @@ def attention_fwd_f32(qkv, B, N, H, dh, scale):
     check(lib().dfu_attention_fwd_f32(ptr(qkv), B, N, H, dh, scale, npad, ptr(o3), ptr(o),
                                       ptr(lse), stream_ptr()), "dfu_attention_fwd_f32")
     return o3, o, lse
+
+
+def metrics_accumulate(logits, labels, loss, confusion, loss_sum, batches):
+    """Device-side per-step metrics (dfu_metrics_accumulate): confusion int64 [C, C] (label,
+    argmax) counts, fp64 loss sum, int64 batch count; no host synchronisation."""
+    lg = logits.detach()
+    if lg.dtype != F32 or not lg.is_contiguous():
+        lg = lg.float().contiguous()
+    rows, C = lg.shape
+    lf = None
+    if loss is not None:
+        lf = loss.detach().reshape(1)
+        if lf.dtype != F32:
+            lf = lf.float()
+    check(lib().dfu_metrics_accumulate(ptr(lg), ptr(labels.contiguous()), rows, C, ptr(lf),
+                                       ptr(confusion), ptr(loss_sum), ptr(batches),
+                                       stream_ptr()), "dfu_metrics_accumulate")

@@ -104,6 +104,7 @@ class GradAllReducer:
         self._pending = None
         self._issued = None
         self._hook = None
+        self.issue_log = []  # bucket indices in launch order (ranks must agree: RCCL pairs them)
         if self.overlap:
             self._hook = Fn.register_grad_ready_hook(self._on_ready)
 
@@ -124,6 +125,7 @@ class GradAllReducer:
         else:
             self._reduce(view)
         self._issued[k] = True
+        self.issue_log.append(k)
 
     def _reduce(self, view):
         if self.avg:

@@ -45,9 +45,11 @@ class MultimodalFusionModel(tnn.Module):
     grad_cam_visualization.py:305-320 / extended_metrics.py:353-367 model, 2816->512->2.
     layout='train': attributes ``rgb_branch``, ``thermal_branch``, ``fusion`` (a Sequential
     with hidden_dims=(512, 256)) — train_multimodal_fusion.py:285-326 keys.
+    hidden_dims=None selects each layout's reference head; any sequence (list or tuple) gives
+    exactly those hidden widths.
     """
 
-    def __init__(self, num_classes=2, dropout=0.7, hidden_dims=(512,), layout="eval",
+    def __init__(self, num_classes=2, dropout=0.7, hidden_dims=None, layout="eval",
                  pretrained=False, concurrent_branches=True):
         super().__init__()
         self.layout = layout
@@ -59,11 +61,11 @@ class MultimodalFusionModel(tnn.Module):
             self.resnet = rgb
             self.vit = th
             self.fusion = MLPFusion(2048, 768, num_classes=num_classes, dropout=dropout,
-                                    hidden_dims=hidden_dims)
+                                    hidden_dims=(512,) if hidden_dims is None else hidden_dims)
         elif layout == "train":
             self.rgb_branch = rgb
             self.thermal_branch = th
-            self.fusion = _mlp(2048 + 768, tuple(hidden_dims) if hidden_dims != (512,) else (512, 256),
+            self.fusion = _mlp(2048 + 768, (512, 256) if hidden_dims is None else tuple(hidden_dims),
                                num_classes, dropout)
         else:
             raise ValueError(f"layout must be 'eval' or 'train', got {layout!r}")

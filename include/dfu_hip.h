@@ -320,6 +320,13 @@ int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_a
 int dfu_step_increment(int64_t* step_dev, void* stream);
 /* argmax over C for each row (torch.max(outputs, 1), :384) -> int64. */
 int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t* out, void* stream);
+/* The per-step metrics of train_multimodal_fusion.py:383-388 (loss.item(), torch.max(outputs,
+ * 1), .cpu()) accumulated on the device, read back once per epoch: confusion int64 [C][C]
+ * (row = label, column = argmax, first maximum wins) += 1 per row; *loss_sum (fp64) += *loss
+ * (if loss != NULL); *batches += 1.  Exact, order-independent totals. */
+int dfu_metrics_accumulate(const float* logits, const int64_t* labels, int32_t rows, int32_t C,
+                           const float* loss, int64_t* confusion, double* loss_sum,
+                           int64_t* batches, void* stream);
 
 /* ---------------------------------------------------------------- bf16x3 forward ---- */
 /* The "bf16x3" precision mode (csrc/precise.hip): the forward pass of the training step at

@@ -47,10 +47,10 @@ def _write_image(path, seed):
     Image.fromarray(arr).save(path, format=fmt)
 
 
-def build_tree(root, leak=False):
+def build_tree(root, leak=False, leak_thermal=False):
     """Create the tree under root/{rgb,thermal}/<split>/<class>/.  Every image has distinct
-    content; with leak=True one train RGB image is copied byte-for-byte into val (renamed).
-    Returns (rgb_dir, thermal_dir)."""
+    content; with leak=True one train RGB image is copied byte-for-byte into val (renamed), with
+    leak_thermal=True one val thermal image into test.  Returns (rgb_dir, thermal_dir)."""
     seed = 1
     for split, mods in LAYOUT.items():
         for mod, classes in mods.items():
@@ -69,6 +69,12 @@ def build_tree(root, leak=False):
     if leak:
         src = os.path.join(root, "rgb", "train", "ulcer", "u02.png")
         dst = os.path.join(root, "rgb", "val", "healthy", "copied.png")
+        with open(src, "rb") as f, open(dst, "wb") as g:
+            g.write(f.read())
+    if leak_thermal:
+        src = os.path.join(root, "thermal", "val", "ulcer", "vtu3.png")
+        dst = os.path.join(root, "thermal", "test", "healthy", "dup", "again.PNG")
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
         with open(src, "rb") as f, open(dst, "wb") as g:
             g.write(f.read())
     return os.path.join(root, "rgb"), os.path.join(root, "thermal")

@@ -133,3 +133,23 @@ def test_vit_block_and_embed():
     print(f"\nvit out {rel(out_h, out_r):.3e}")
     assert rel(out_h, out_r) < 2e-2
     _grad_report(hip, ref, 3e-2, "  vit")
+
+
+def test_vit_block_output_hooks_see_true_gradient():
+    """ADVICE r1: ViTBlockFn's backward updates the incoming residual-stream gradient in place;
+    a retain_grad() / tensor hook on a block output must still hold the true gradient."""
+    from models.vit import vit_base_patch16_224
+    torch.manual_seed(0)
+    vit = vit_base_patch16_224(num_classes=0).to(DEV).train()
+    x0 = torch.randn(2, 197, 768, device=DEV)
+    Rg = torch.randn(2, 197, 768, device=DEV)
+    hooked = []
+    out = vit.blocks[0](x0.requires_grad_(True))
+    out.retain_grad()
+    out.register_hook(lambda g: hooked.append(g))
+    (vit.blocks[1](out) * Rg).sum().backward()
+    # reference: the same gradient at a leaf (nothing downstream can touch a leaf's .grad)
+    leaf = out.detach().clone().requires_grad_(True)
+    (vit.blocks[1](leaf) * Rg).sum().backward()
+    assert torch.equal(out.grad, leaf.grad)
+    assert torch.equal(hooked[0], leaf.grad)

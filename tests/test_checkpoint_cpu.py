@@ -87,3 +87,47 @@ def test_fusion_checkpoint_round_trip_with_reference_layout(tmp_path):
     assert len(rep.loaded) == len(hip.state_dict()) and not rep.skipped
     for k, v in hip.state_dict().items():
         assert torch.equal(back.state_dict()[k], v)
+
+
+def test_reference_numpy_metrics_load_weights_only(tmp_path):
+    """The reference saves sklearn results (numpy.float64) in val_f1 / history
+    (train_multimodal_fusion.py:428-439); all three loaders read them with weights_only."""
+    import numpy as np
+    path = tmp_path / "best_model.pt"
+    hist = {"train_loss": [0.7, 0.6], "train_acc": [np.float64(0.5), np.float64(0.625)],
+            "train_f1": [np.float64(0.4), np.float64(0.5)], "val_f1": [np.float64(0.55)],
+            "n": [np.int64(3)]}
+    sd = {"backbone.conv1.weight": torch.ones(2), "fc.weight": torch.zeros(1)}
+    torch.save({"epoch": 4, "model_state_dict": sd, "optimizer_state_dict": {},
+                "val_f1": np.float64(0.7142857), "history": hist}, path)
+    c = ck.load_checkpoint(path)
+    assert isinstance(c["val_f1"], np.float64) and c["val_f1"] == np.float64(0.7142857)
+    assert c["history"]["train_acc"][1] == 0.625 and c["history"]["n"][0] == 3
+    m = _Head("resnet")
+    assert ck.load_checkpoint_flexible(m, path, device="cpu", verbose=False)
+    assert ck.fix_checkpoint_keys(path)["val_f1"] == np.float64(0.7142857)
+
+
+def test_multimodal_vit_backbone_remap(tmp_path):
+    """extended_metrics.py:803-813: backbone.* -> resnet.*, vit_backbone.* -> vit.*."""
+    sd = {"backbone.conv1.weight": torch.ones(1), "vit_backbone.cls_token": torch.zeros(1),
+          "fusion.0.weight": torch.ones(2)}
+    assert ck.remap_multimodal_keys(sd) == {"resnet.conv1.weight": sd["backbone.conv1.weight"],
+                                            "vit.cls_token": sd["vit_backbone.cls_token"],
+                                            "fusion.0.weight": sd["fusion.0.weight"]}
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.resnet = nn.Linear(3, 2)
+            self.vit = nn.Linear(2, 2)
+    src = M()
+    path = tmp_path / "mm.pt"
+    torch.save({"model_state_dict": {("backbone." + k[7:] if k.startswith("resnet.")
+                                      else "vit_backbone." + k[4:]): v
+                                     for k, v in src.state_dict().items()}}, path)
+    dst = M()
+    missing, unexpected = ck.load_multimodal_checkpoint(dst, path, device="cpu")
+    assert not missing and not unexpected
+    for k, v in src.state_dict().items():
+        assert torch.equal(dst.state_dict()[k], v)

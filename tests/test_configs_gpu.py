@@ -1,0 +1,253 @@
+"""BASELINE configs C1 (RGB-only ResNet50, bs=8, ImageFolder plumbing) and C2 (thermal-only
+ViT-B/16, bs=64) on the MI355X path against the CPU oracle, plus the reference's epoch loop
+(training.loop) with device-side metrics.
+
+  * C2: ThermalOnlyModel (train_thermal_only.py:188-205) train step at B=64: bf16x3 logits
+    within north_star's 1e-3 of the fp32 oracle, bf16 logits within the bf16 oracle's own band,
+    and after one AdamW step (lr 1e-4, wd 1e-4) every parameter within one Adam step of the
+    oracle's (the first Adam update is ~lr * sign(g): only gradients of opposite sign differ).
+  * C1: RGBOnlyModel (train_rgb_only.py:200-217) at B=8 on batches produced by the
+    reference's own plumbing: a synthetic ImageFolder of PNGs (16 per class per split, SURVEY
+    §8d), RGBDataset + SHA-256 guard + weighted sampler, decoded and transformed on the GPU
+    (data.gpu_transforms.GpuImageLoader); bf16x3 logits within 1e-3 of the fp32 oracle on the
+    first batch, then the reference's epoch loop for 4 epochs (train, val, save the best
+    checkpoint once epoch >= 3) and the checkpoint read back through the reference's loader.
+  * dfu_metrics_accumulate against sklearn's accuracy_score / f1_score.
+Dropout is identity for the parity comparisons, p = 0.5 in the loop run.
+"""
+import copy
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+LOGIT_ATOL = 1e-3
+
+
+def _maxd(a, b):
+    return (a.detach().float().cpu() - b.detach().float().cpu()).abs().max().item()
+
+
+class _RefThermal(nn.Module):
+    """train_thermal_only.py:188-205 on the oracle ViT."""
+
+    def __init__(self, p=0.0):
+        super().__init__()
+        self.backbone = R.VisionTransformer(num_classes=2)
+        self.backbone.head = nn.Sequential(nn.Dropout(p), nn.Linear(768, 2))
+
+    def forward(self, x):
+        return self.backbone(x)
+
+
+class _RefRGB(nn.Module):
+    """train_rgb_only.py:200-217 on the oracle ResNet50."""
+
+    def __init__(self, p=0.0):
+        super().__init__()
+        self.backbone = R.ResNet()
+        self.backbone.fc = nn.Sequential(nn.Dropout(p), nn.Linear(2048, 2))
+
+    def forward(self, x):
+        return self.backbone(x)
+
+
+def _hip_step(model, x, y, w, precision, opt=None):
+    from dfu_hip import functional as Fn
+    from dfu_hip import nn as hnn
+    model.train()
+    with Fn.precision(precision):
+        if opt is not None:
+            opt.zero_grad()
+        out = model(x)
+        loss = hnn.CrossEntropyLoss(weight=w.to(DEV))(out, y.to(DEV))
+        loss.backward()
+        if opt is not None:
+            opt.step()
+    torch.cuda.synchronize()
+    return out.detach().float().cpu(), loss.item()
+
+
+def _oracle_fwd(ref, x, emu):
+    m = copy.deepcopy(ref).train()
+    R.set_bf16_emulation(emu)
+    try:
+        with torch.no_grad():
+            return m(x)
+    finally:
+        R.set_bf16_emulation(False)
+
+
+def test_c2_thermal_only_train_step_b64():
+    from dfu_hip.optim import FusedAdamW
+    from models.single import ThermalOnlyModel
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    torch.manual_seed(0)
+    ref = _RefThermal()
+    B = 64
+    _, th, y = R.synthetic_batch(B, seed=42)
+    w = R.class_weights(y)
+    # fp32 oracle: one train step (fwd, weighted CE, bwd, AdamW) -- train_thermal_only.py:241-259
+    m = copy.deepcopy(ref).train()
+    opt_ref = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    out_f32 = m(th)
+    loss_f32 = nn.functional.cross_entropy(out_f32, y, weight=w)
+    loss_f32.backward()
+    opt_ref.step()
+    res = {}
+    for precision in ("bf16x3", "bf16"):
+        hip = ThermalOnlyModel(drop_rate=0.0)
+        hip.load_state_dict(ref.state_dict(), strict=True)
+        hip = hip.to(DEV)
+        opt = FusedAdamW(hip.parameters(), lr=1e-4, weight_decay=1e-4)
+        res[precision] = _hip_step(hip, th.to(DEV), y, w, precision, opt) + (hip,)
+    out_x3, loss_x3, hip_x3 = res["bf16x3"]
+    d = _maxd(out_x3, out_f32)
+    emu = _oracle_fwd(ref, th, True)
+    emu_gpu = _oracle_fwd(copy.deepcopy(ref).to(DEV), th.to(DEV), True)
+    band = _maxd(emu_gpu, emu)
+    d_bf = _maxd(res["bf16"][0], emu)
+    print(f"\n[C2 B={B}] bf16x3 vs fp32 oracle {d:.3e} (bar {LOGIT_ATOL}); bf16 vs bf16 oracle "
+          f"{d_bf:.3e} (band {band:.3e}); bf16 vs fp32 oracle {_maxd(res['bf16'][0], out_f32):.3e}")
+    assert d <= LOGIT_ATOL and abs(loss_x3 - loss_f32.item()) <= LOGIT_ATOL
+    assert d_bf <= 2 * band + LOGIT_ATOL
+    # parameters after the AdamW step: within one Adam step (2 lr) of the oracle's, and equal
+    # where the update is decided (|p_oracle - p0| ~ lr: same sign of the step)
+    p0 = dict(ref.named_parameters())
+    pr = dict(m.named_parameters())
+    worst, agree, total = 0.0, 0, 0
+    for n, p in hip_x3.named_parameters():
+        a, b, z = p.detach().cpu(), pr[n].detach(), p0[n].detach()
+        worst = max(worst, (a - b).abs().max().item())
+        same = torch.sign(a - z) == torch.sign(b - z)
+        agree += int(same.sum())
+        total += same.numel()
+    print(f"  after AdamW: max |p_hip - p_oracle| {worst:.3e}; update signs agree on "
+          f"{agree / total:.4%} of {total} parameters")
+    assert worst <= 2.05e-4
+    assert agree / total > 0.97
+
+
+def _write_imagefolder(root, n_per_class=16, seed=0):
+    """the synthetic uint8 images as PNGs under ROOT/{train,val,test}/{healthy,
+    ulcer}/ (the layout train_rgb_only.py:58-81 walks), 16 per class per split."""
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    for split in ("train", "val", "test"):
+        for cls in ("healthy", "ulcer"):
+            d = os.path.join(root, split, cls)
+            os.makedirs(d, exist_ok=True)
+            for i in range(n_per_class):
+                arr = rng.integers(0, 256, size=(224, 224, 3), dtype=np.uint8)
+                if cls == "ulcer":  # a learnable signal: ulcer images are redder
+                    arr[..., 0] = np.maximum(arr[..., 0], 160)
+                Image.fromarray(arr).save(os.path.join(d, f"{cls}_{i:02d}.png"))
+
+
+def test_c1_rgb_only_plumbing_parity_and_epoch_loop(tmp_path):
+    from data import gpu_transforms as GT
+    from data import single_modality as SM
+    from dfu_hip import nn as hnn
+    from dfu_hip.optim import FusedAdamW
+    from models import checkpoint as ck
+    from models.single import RGBOnlyModel
+    from training import loop
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    root = str(tmp_path / "rgb")
+    _write_imagefolder(root)
+    dss = {s: SM.RGBDataset(root, s, verbose=False) for s in ("train", "val", "test")}
+    SM.check_split_hash_leakage(dss["train"], dss["val"], dss["test"], verbose=False)
+    assert [len(d) for d in dss.values()] == [32, 32, 32]
+    # --- parity of the train step on the plumbing's first batch (val transform: deterministic)
+    val_loader = GT.GpuImageLoader(dss["val"], 8, train=False, device=DEV)
+    xb, yb = next(iter(val_loader))
+    assert xb.shape == (8, 3, 224, 224) and xb.dtype == torch.float32 and xb.is_cuda
+    torch.manual_seed(0)
+    ref = _RefRGB()
+    w = SM.class_weights(dss["train"].labels)
+    m = copy.deepcopy(ref).train()
+    out_f32 = m(xb.cpu())
+    hip = RGBOnlyModel(drop_rate=0.0)
+    hip.load_state_dict(ref.state_dict(), strict=True)
+    hip = hip.to(DEV)
+    out_x3, _ = _hip_step(hip, xb, yb.cpu(), w, "bf16x3")
+    d = _maxd(out_x3, out_f32)
+    print(f"\n[C1 B=8] bf16x3 logits vs fp32 oracle {d:.3e} (bar {LOGIT_ATOL})")
+    assert d <= LOGIT_ATOL
+    # --- the reference's epoch loop (train_rgb_only.py:241-328) on the HIP modules
+    torch.manual_seed(1)
+    model = RGBOnlyModel().to(DEV)  # DROP_RATE 0.5
+    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    crit = hnn.CrossEntropyLoss(weight=w.to(DEV))
+    g = torch.Generator().manual_seed(42)
+    train_loader = GT.GpuImageLoader(dss["train"], 8, sampler=SM.make_weighted_sampler(
+        dss["train"], generator=g), train=True, device=DEV, generator=g)
+    ckdir = tmp_path / "ck"
+    ckdir.mkdir()
+    hist, best, path = loop.fit(model, train_loader, val_loader, crit, opt, num_epochs=4,
+                                checkpoint_dir=ckdir, log=None, device=DEV)
+    assert all(len(v) == 4 for v in hist.values())
+    assert all(np.isfinite(v).all() for v in hist.values())
+    late = hist["val_f1"][2:]
+    if max(late) > 0:  # saved iff some epoch >= 3 improved on 0 (the reference's rule)
+        assert path is not None and os.path.exists(path) and best == max(late)
+        c = ck.load_checkpoint(path)
+        assert set(c) == set(ck.CHECKPOINT_KEYS) and c["epoch"] >= 3
+        assert c["val_f1"] == best and c["history"]["val_f1"][:c["epoch"]] == \
+            hist["val_f1"][:c["epoch"]]
+        # the evaluation script's RGBOnlyModel (.resnet, extended_metrics.py:307-317) reads it
+        # through the reference's flexible loader (backbone. -> resnet.)
+        fresh = RGBOnlyModel(layout="eval")
+        rep = ck.load_checkpoint_flexible(fresh, path, device="cpu", verbose=False)
+        assert rep and len(rep.loaded) == len(fresh.state_dict()) and not rep.skipped
+        for k, v in c["model_state_dict"].items():
+            assert torch.equal(fresh.state_dict()["resnet." + k[len("backbone."):]], v.cpu())
+    else:
+        assert path is None
+    # the loop's device metrics equal a host recomputation of the val epoch
+    model.eval()
+    preds, labels, losses = [], [], []
+    with torch.no_grad():
+        for x, yv in val_loader:
+            o = model(x)
+            losses.append(crit(o, yv).item())
+            preds += o.argmax(1).cpu().tolist()
+            labels += yv.cpu().tolist()
+    r = loop.run_epoch(model, val_loader, crit, train=False, device=DEV)
+    from sklearn.metrics import accuracy_score, f1_score
+    assert r["acc"] == accuracy_score(labels, preds)
+    assert r["f1"] == f1_score(labels, preds, average="binary", zero_division=0)
+    assert abs(r["loss"] - sum(losses) / len(losses)) < 1e-6
+
+
+def test_metrics_accumulate_matches_sklearn():
+    from sklearn.metrics import accuracy_score, f1_score
+
+    from training.loop import DeviceMetrics
+    g = torch.Generator().manual_seed(3)
+    met = DeviceMetrics(2, DEV)
+    P, L, loss_sum = [], [], 0.0
+    for b in range(7):
+        B = 5 + b
+        logits = torch.randn(B, 2, generator=g)
+        logits[0, 1] = logits[0, 0]  # a tie: the first maximum (class 0) wins, as torch.max
+        y = torch.randint(0, 2, (B,), generator=g)
+        loss = torch.rand(1, generator=g)
+        met.update(logits.to(DEV), y.to(DEV), loss.to(DEV))
+        P += torch.max(logits, 1)[1].tolist()
+        L += y.tolist()
+        loss_sum += float(loss)
+    r = met.result()
+    assert r["n"] == len(L) and r["batches"] == 7
+    assert r["acc"] == accuracy_score(L, P)
+    assert abs(r["f1"] - f1_score(L, P, average="binary")) < 1e-12
+    assert abs(r["loss"] - loss_sum / 7) < 1e-6
+    empty = DeviceMetrics(2, DEV)
+    empty.update(torch.tensor([[1.0, 0.0]], device=DEV), torch.tensor([0], device=DEV))
+    assert empty.result()["f1"] == 0.0  # no positives predicted or present: sklearn's 0

@@ -112,7 +112,8 @@ def test_input_gradients_match_oracle():
     assert torch.isfinite(gh).all() and _rel(gh, g_fp) < 0.05, _rel(gh, g_fp)
 
 
-def test_gradcam_maps_match_reference_restatement():
+@pytest.mark.parametrize("B", [3, 32])  # 32: BASELINE config C5's batch
+def test_gradcam_maps_match_reference_restatement(B):
     """models.gradcam.GradCAM (batched, HIP) vs the oracle's restatement of the reference's
     GradCAM run image by image (bs=1, as grad_cam_visualization.py:686): the RGB 7x7 CAM from the
     hooked 'layer4.2.relu' output and the thermal input saliency from the 'blocks' fallback.
@@ -120,7 +121,6 @@ def test_gradcam_maps_match_reference_restatement():
     and both maps are all-zero.)"""
     from models.gradcam import GradCAM
     ref, hip = _pair(zero_init_residual=False)
-    B = 3
     rgb, th, _ = R.synthetic_batch(B, seed=31)
     cam_rgb = GradCAM(hip.resnet, ["layer4"])
     assert cam_rgb.target_name() == "layer4.2.relu"

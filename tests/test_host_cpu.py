@@ -140,3 +140,18 @@ def test_gradcam_target_layer_rule():
     rc.remove()
     tc.remove()
     assert not m.resnet.layer4[-1].relu._forward_hooks
+
+
+def test_fusion_head_hidden_dims_list_or_tuple():
+    """the head depends on the hidden widths, not on the container type; None picks
+    each layout's reference head (eval 2816->512->2, train 2816->512->256->2)."""
+    from models.fusion import MultimodalFusionModel
+    from dfu_hip import nn as hnn
+    widths = lambda m: [l.out_features for l in m.fusion.modules() if isinstance(l, hnn.Linear)]  # noqa: E731,E741
+    for layout, ref in (("eval", [512, 2]), ("train", [512, 256, 2])):
+        assert widths(MultimodalFusionModel(layout=layout)) == ref
+        assert widths(MultimodalFusionModel(layout=layout, hidden_dims=[512])) == [512, 2]
+        assert widths(MultimodalFusionModel(layout=layout, hidden_dims=(512,))) == [512, 2]
+    keys = [k for k in MultimodalFusionModel(layout="train").state_dict() if k.startswith("fusion")]
+    assert keys == ["fusion.0.weight", "fusion.0.bias", "fusion.3.weight", "fusion.3.bias",
+                    "fusion.6.weight", "fusion.6.bias"]

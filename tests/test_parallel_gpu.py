@@ -69,3 +69,93 @@ def test_bucket_ready_points_are_final():
             red._pending = red._issued = None
     finally:
         Fn.remove_grad_ready_hook(hook)
+
+
+def _dp_worker(rank, port, q):
+    """One rank of a world-2 data-parallel step on the real fusion model, both ranks on cuda:0
+    over gloo (CUDA tensors; RCCL needs one GPU per rank).  The GPU is touched only here, after
+    the spawn."""
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE="2", LOCAL_RANK=str(rank))
+    try:
+        import bench
+        from dfu_hip import functional as Fn
+        from dfu_hip import nn as hnn
+        from dfu_hip.optim import FusedAdamW
+        from models.fusion import MultimodalFusionModel
+        r, w, _ = parallel.init_from_env(backend="gloo")
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        torch.manual_seed(42 + rank)  # different replicas before the broadcast
+        model = MultimodalFusionModel(num_classes=2, dropout=0.0).to(dev).train()
+        parallel.broadcast_parameters(model)
+        opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+        crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
+        rgb, th, y = bench.synthetic(4, dev, seed=42 + rank)  # each rank its own batch
+
+        def step(red=None):
+            opt.zero_grad()
+            if red is not None:
+                red.start()
+            loss = crit(model(rgb, th), y)
+            loss.backward()
+            Fn.join_grad_streams()
+            if red is not None:
+                red.finish()
+            torch.cuda.synchronize()
+
+        step()  # this rank's own gradient (no exchange)
+        local = opt.flat.grad.clone()
+        red = parallel.GradAllReducer(opt.flat, overlap=True)
+        step(red)  # overlapped bucketed all-reduce launched from the grad-ready hooks
+        got = opt.flat.grad.clone()
+        dist.all_reduce(local)  # the expectation: one plain all-reduce of the local gradients
+        local /= 2
+        torch.cuda.synchronize()
+        diff = (got - local).abs().max().item()
+        scale = local.abs().max().item()
+        g64 = got.double()
+        idx = torch.arange(0, got.numel(), 997, device=dev)
+        q.put((rank, dict(diff=diff, scale=scale, log=list(red.issue_log),
+                          nbuckets=len(red.buckets), sum=g64.sum().item(),
+                          sq=(g64 * g64).sum().item(), sample=got[idx].cpu()), None))
+        red.close()
+    except Exception as e:  # report to the parent instead of hanging it
+        import traceback
+        q.put((rank, None, traceback.format_exc() + repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_fusion_dp_world2_overlapped_reducer():
+    """SURVEY §8e check on the real fusion model with overlap=True: the
+    averaged gradients equal the mean of the per-rank gradients, both ranks issue the buckets
+    in the same order (every one from the hooks), and hold identical averaged gradients."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, d, err = q.get(timeout=240)
+        assert err is None, f"rank {rank}: {err}"
+        res[rank] = d
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a, b = res[0], res[1]
+    print(f"\n[DP world 2] buckets {a['nbuckets']}, issue order r0 {a['log']} r1 {b['log']}; "
+          f"max |avg - mean(local)| {a['diff']:.2e} / {b['diff']:.2e} (scale {a['scale']:.2e})")
+    assert a["log"] == b["log"] and sorted(a["log"]) == list(range(a["nbuckets"]))
+    for d in (a, b):
+        assert d["diff"] <= 1e-6 * max(d["scale"], 1e-30)
+    assert a["sum"] == b["sum"] and a["sq"] == b["sq"] and torch.equal(a["sample"], b["sample"])
