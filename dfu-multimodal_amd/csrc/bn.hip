@@ -17,23 +17,57 @@ constexpr int FIN_WAVES = 16;
 
 // CPW channels per block: a wave's 64 lanes cover CPW channels x (64 / CPW) tile slots, so
 // narrow layers (C = 64 over up to 6272 stem tiles) spread their tile loop over more lanes.
+// Slices (blockIdx.y, gridDim.y = S > 1): each block reduces tiles [y * tps, (y + 1) * tps)
+// and publishes fp64 (sum, sum of squares) per channel with write-through (sc1) stores; one
+// agent-scope counter per channel group counts the slices, and the LAST to arrive (told by the
+// value its add returned; MI355X_MICROARCH.md hand-off table, row 1: sc1 stores, sc1 loads, no
+// fence) sums the S records in slice order and finalizes — the result does not depend on the
+// arrival order.  The counter is returned to zero (ops.tile_counters' invariant).
+DFU_DEV void st_sc1_f64(double* p, double v) {
+  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DFU_DEV double ld_sc1_f64(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Slice hand-off: every block's lane-0 record stores are drained, the block's add is counted;
+// returns (in every thread) whether this block is the last of its channel group.
+DFU_DEV bool last_slice(int* counter, int S, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == S - 1;
+    if (last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 template <int CPW>
 __global__ __launch_bounds__(1024) void k_bn_finalize(
-    const float* __restrict__ stats, int tiles, int M, int C, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ rmean,
-    float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ mean_out,
-    float* __restrict__ invstd_out, float* __restrict__ scale_out, float* __restrict__ shift_out) {
+    const float* __restrict__ stats, int tiles, int tps, int M, int C,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale_out,
+    float* __restrict__ shift_out, double* __restrict__ ws, int* __restrict__ counters) {
   constexpr int TS = 64 / CPW;  // tile slots per wave
   __shared__ double sh_s[FIN_WAVES][64], sh_q[FIN_WAVES][64];
+  __shared__ int flag;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cl = lane % CPW, slot = lane / CPW;
   const int c = blockIdx.x * CPW + cl;
+  const int S = gridDim.y;
+  const int t0 = blockIdx.y * tps, t1 = min(tiles, t0 + tps);
   double sx = 0.0, sxx = 0.0;
   if (c < C) {
     const int last = tiles - 1;
     const double inv_last = 1.0 / (double)(M - last * 128);
 #pragma unroll 4
-    for (int t = w * TS + slot; t < tiles; t += FIN_WAVES * TS) {
+    for (int t = t0 + w * TS + slot; t < t1; t += FIN_WAVES * TS) {
       const double sb = stats[((int64_t)t * 2 + 0) * C + c];
       const double qb = stats[((int64_t)t * 2 + 1) * C + c];
       sx += sb;
@@ -43,13 +77,30 @@ __global__ __launch_bounds__(1024) void k_bn_finalize(
   sh_s[w][lane] = sx;
   sh_q[w][lane] = sxx;
   __syncthreads();
-  if (w == 0 && slot == 0 && c < C) {
+  const bool owner = w == 0 && slot == 0 && c < C;
+  if (owner) {
     sx = sxx = 0.0;
     for (int k = 0; k < FIN_WAVES; ++k)
       for (int j = 0; j < TS; ++j) {
         sx += sh_s[k][j * CPW + cl];
         sxx += sh_q[k][j * CPW + cl];
       }
+  }
+  if (S > 1) {
+    if (owner) {
+      st_sc1_f64(ws + ((int64_t)blockIdx.y * 2 + 0) * C + c, sx);
+      st_sc1_f64(ws + ((int64_t)blockIdx.y * 2 + 1) * C + c, sxx);
+    }
+    if (!last_slice(counters + blockIdx.x, S, &flag)) return;
+    if (owner) {
+      sx = sxx = 0.0;
+      for (int y = 0; y < S; ++y) {
+        sx += ld_sc1_f64(ws + ((int64_t)y * 2 + 0) * C + c);
+        sxx += ld_sc1_f64(ws + ((int64_t)y * 2 + 1) * C + c);
+      }
+    }
+  }
+  if (owner) {
     const double nn = (double)M;
     const double mu = sx / nn;
     const double var = fmax(sxx / nn - mu * mu, 0.0);  // biased, used to normalise
@@ -66,7 +117,7 @@ __global__ __launch_bounds__(1024) void k_bn_finalize(
       rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
     }
   }
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // one finalizing block
 }
 
 __global__ void k_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm,
@@ -208,17 +259,22 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
 
 // 16 waves x 64 channel-lanes per workgroup (coalesced 256-B row segments of the partials, the
 // waves stride the row-blocks); fp64 sums, 16-way LDS reduction.
+// Slices over the row-blocks as k_bn_finalize (blockIdx.y, last arriver sums in slice order).
 __global__ __launch_bounds__(1024) void k_bn_bwd_finalize(
-    const float* __restrict__ partial, int blocks, int64_t M, int C,
+    const float* __restrict__ partial, int blocks, int bps, int64_t M, int C,
     const float* __restrict__ gamma, const float* __restrict__ invstd, int batch_stats,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef) {
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef,
+    double* __restrict__ ws, int* __restrict__ counters) {
   __shared__ double red[2][FIN_WAVES][64];
+  __shared__ int flag;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
+  const int S = gridDim.y;
+  const int b0 = blockIdx.y * bps, b1 = min(blocks, b0 + bps);
   double sg = 0.0, sgx = 0.0;
   if (c < C) {
 #pragma unroll 4
-    for (int b = w; b < blocks; b += FIN_WAVES) {
+    for (int b = b0 + w; b < b1; b += FIN_WAVES) {
       sg += partial[((int64_t)b * 2 + 0) * C + c];
       sgx += partial[((int64_t)b * 2 + 1) * C + c];
     }
@@ -226,8 +282,23 @@ __global__ __launch_bounds__(1024) void k_bn_bwd_finalize(
   red[0][w][lane] = sg;
   red[1][w][lane] = sgx;
   __syncthreads();
-  if (w == 0 && c < C) {
+  if (w == 0 && c < C)
     for (int k = 1; k < FIN_WAVES; ++k) { sg += red[0][k][lane]; sgx += red[1][k][lane]; }
+  if (S > 1) {
+    if (w == 0 && c < C) {
+      st_sc1_f64(ws + ((int64_t)blockIdx.y * 2 + 0) * C + c, sg);
+      st_sc1_f64(ws + ((int64_t)blockIdx.y * 2 + 1) * C + c, sgx);
+    }
+    if (!last_slice(counters + blockIdx.x, S, &flag)) return;
+    if (w == 0 && c < C) {
+      sg = sgx = 0.0;
+      for (int y = 0; y < S; ++y) {
+        sg += ld_sc1_f64(ws + ((int64_t)y * 2 + 0) * C + c);
+        sgx += ld_sc1_f64(ws + ((int64_t)y * 2 + 1) * C + c);
+      }
+    }
+  }
+  if (w == 0 && c < C) {
     if (dbeta) dbeta[c] += (float)sg;
     if (dgamma) dgamma[c] += (float)sgx;
     const float g = gamma ? gamma[c] : 1.f;
@@ -289,21 +360,36 @@ inline unsigned grid_for(int64_t n) {
 
 }  // namespace
 
+namespace {
+constexpr int FIN_TPS = 128;  // stats tiles (or bwd row-blocks) per finalize slice
+inline int fin_cpw(int C) { return C <= 64 ? 16 : (C <= 128 ? 32 : 64); }
+}  // namespace
+
+extern "C" int64_t dfu_bn_finalize_ws_bytes(int32_t tiles, int32_t C) {
+  const int S = (tiles + FIN_TPS - 1) / FIN_TPS;
+  return S > 1 ? (int64_t)S * 2 * C * 8 : 0;
+}
+
 extern "C" int dfu_bn_finalize(const float* stats, int32_t tiles, int32_t M, int32_t C,
                                const float* gamma, const float* beta, float eps, float momentum,
                                float* running_mean, float* running_var, int64_t* num_batches,
                                float* mean_out, float* invstd_out, float* scale_out,
-                               float* shift_out, void* stream) {
+                               float* shift_out, double* ws, int32_t* counters, int32_t ncounters,
+                               void* stream) {
   DFU_CHECK_ARG(stats && tiles == (M + 127) / 128 && C > 0 && mean_out && invstd_out &&
                     scale_out && shift_out,
                 "dfu_bn_finalize: bad args (tiles=%d M=%d)", tiles, M);
-  // aim for >= 4 blocks: 16 channels per block up to C = 64, 32 up to 128, else 64
+  // 16 channels per block up to C = 64, 32 up to 128, else 64; the tiles in slices of FIN_TPS
+  // when a workspace and zeroed counters are given (else one slice: a long serial tile loop)
+  const int cpw = fin_cpw(C);
+  const int gx = (C + cpw - 1) / cpw;
+  int S = (tiles + FIN_TPS - 1) / FIN_TPS;
+  if (ws == nullptr || counters == nullptr || ncounters < gx) S = 1;
+  const int tps = S > 1 ? FIN_TPS : tiles;
   auto kern = C <= 64 ? k_bn_finalize<16> : (C <= 128 ? k_bn_finalize<32> : k_bn_finalize<64>);
-  const int cpw = C <= 64 ? 16 : (C <= 128 ? 32 : 64);
-  hipLaunchKernelGGL(kern, dim3((C + cpw - 1) / cpw), dim3(64 * FIN_WAVES), 0,
-                     (hipStream_t)stream, stats,
-                     tiles, M, C, gamma, beta, eps, momentum, running_mean, running_var,
-                     num_batches, mean_out, invstd_out, scale_out, shift_out);
+  hipLaunchKernelGGL(kern, dim3(gx, S), dim3(64 * FIN_WAVES), 0, (hipStream_t)stream, stats,
+                     tiles, tps, M, C, gamma, beta, eps, momentum, running_mean, running_var,
+                     num_batches, mean_out, invstd_out, scale_out, shift_out, ws, counters);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
@@ -358,13 +444,23 @@ extern "C" int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* ou
   return DFU_OK;
 }
 
+extern "C" int64_t dfu_bn_bwd_finalize_ws_bytes(int32_t blocks, int32_t C) {
+  const int S = (blocks + FIN_TPS - 1) / FIN_TPS;
+  return S > 1 ? (int64_t)S * 2 * C * 8 : 0;
+}
+
 extern "C" int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t M, int32_t C,
                                    const float* gamma, const float* invstd, int32_t batch_stats,
-                                   float* dgamma, float* dbeta, float* coef, void* stream) {
+                                   float* dgamma, float* dbeta, float* coef, double* ws,
+                                   int32_t* counters, int32_t ncounters, void* stream) {
   DFU_CHECK_ARG(partial && invstd && coef && blocks > 0 && C > 0, "dfu_bn_bwd_finalize: bad args");
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 63) / 64), dim3(64 * FIN_WAVES), 0,
-                     (hipStream_t)stream,
-                     partial, blocks, M, C, gamma, invstd, batch_stats, dgamma, dbeta, coef);
+  const int gx = (C + 63) / 64;
+  int S = (blocks + FIN_TPS - 1) / FIN_TPS;
+  if (ws == nullptr || counters == nullptr || ncounters < gx) S = 1;
+  const int bps = S > 1 ? FIN_TPS : blocks;
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(gx, S), dim3(64 * FIN_WAVES), 0, (hipStream_t)stream,
+                     partial, blocks, bps, M, C, gamma, invstd, batch_stats, dgamma, dbeta, coef,
+                     ws, counters);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

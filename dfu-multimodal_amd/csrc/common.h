@@ -85,6 +85,12 @@ DFU_DEV CdfPdf gauss_cdf_pdf(float u) {
   return r;
 }
 DFU_DEV float gelu_f(float x) { return x * gauss_cdf_pdf(x).cdf; }
+// GELU(x) and GELU'(x) = Phi(x) + x phi(x) from one evaluation.
+DFU_DEV void gelu_and_grad(float x, float& g, float& d) {
+  const CdfPdf c = gauss_cdf_pdf(x);
+  g = x * c.cdf;
+  d = fmaf(x, c.pdf, c.cdf);
+}
 DFU_DEV float gelu_grad_f(float x) {
   const CdfPdf c = gauss_cdf_pdf(x);
   return c.cdf + x * c.pdf;

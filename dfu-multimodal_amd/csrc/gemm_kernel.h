@@ -778,12 +778,14 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
         }
         st_row_bf16<FN>(rc, mo * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
       } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
-        float g[FN][4];
+        // GELU and its derivative from one erfc/exp evaluation: the backward's dGELU
+        // epilogue then only multiplies (no transcendental work in the dgrad GEMM)
+        float g[FN][4], d[FN][4];
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) g[j][r] = gelu_f(v[j][r]);
-        st_row_bf16<FN>(ro, mo * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, v);
+          for (int r = 0; r < 4; ++r) gelu_and_grad(v[j][r], g[j][r], d[j][r]);
+        st_row_bf16<FN>(ro, mo * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
         st_row_bf16<FN>(rc, mo * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
       } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
 #pragma unroll
@@ -793,7 +795,7 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
           ld4_bf16(ra, mo * p.ldaux + n, okm, n, N, n4, x);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            v[j][r] = (EPI == DFU_EPI_BF16_DGELU) ? v[j][r] * gelu_grad_f(x[r]) : v[j][r] + x[r];
+            v[j][r] = (EPI == DFU_EPI_BF16_DGELU) ? v[j][r] * x[r] : v[j][r] + x[r];
         }
         st_row_bf16<FN>(rc, mo * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
       } else {

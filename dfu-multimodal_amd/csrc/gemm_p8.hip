@@ -21,7 +21,7 @@
 // One workgroup per CU; workgroups walk tiles (grouped raster, XCD-aware) one at a time.
 // A and B K-contiguous (forward), B MN-major (dgrad), or both MN-major (wgrad, split-K units
 // into fp32 slabs) -- MN-major halves are 128-column tr16 sub-images.
-// Epilogues: BF16 (+bias), BF16_GELU (pre-activation to aux_out), F32_RESID; dgrad: BF16,
+// Epilogues: BF16 (+bias), BF16_GELU (GELU'(pre) to aux_out), F32_RESID; dgrad: BF16,
 // BF16_DGELU, BF16_ADD.
 #include "gemm_table.h"
 
@@ -92,17 +92,17 @@ DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
       if constexpr (EPI == DFU_EPI_BF16) {
         st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
       } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
-        float g[4];
+        float g[4], d[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) g[r] = gelu_f(v[r]);
-        st4_bf16(ro, mc * p.ldaux_out + n, okm, n, N, n4, v);
+        for (int r = 0; r < 4; ++r) gelu_and_grad(v[r], g[r], d[r]);
+        st4_bf16(ro, mc * p.ldaux_out + n, okm, n, N, n4, d);
         st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, g);
       } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
         float x[4];
         ld4_bf16(ra, mc * p.ldaux + n, okm, n, N, n4, x);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          v[r] = EPI == DFU_EPI_BF16_DGELU ? v[r] * gelu_grad_f(x[r]) : v[r] + x[r];
+          v[r] = EPI == DFU_EPI_BF16_DGELU ? v[r] * x[r] : v[r] + x[r];
         st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
       } else if constexpr (EPI == DFU_EPI_F32_ACC) {  // split-K slab, or C += acc unsplit
         if (p.slab != nullptr) {

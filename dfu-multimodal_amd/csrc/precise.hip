@@ -265,23 +265,27 @@ __global__ void k_ln_fwd_x3(const float* __restrict__ x, int64_t ldx, int rows, 
 
 // ---------------------------------------------------------------- GELU
 // h = gelu(hpre) (exact erf, timm nn.GELU) from the fp32 fc1 output -> h triple [rows][3N],
-// plain bf16 h and hpre (the backward's fc2-wgrad operand and dGELU input).
+// plain bf16 h and gelu'(hpre) (the backward's fc2-wgrad operand and dGELU factor).
 __global__ void k_gelu_x3(const float* __restrict__ hpre, int64_t rows, int N,
                           bf16_t* __restrict__ h3, bf16_t* __restrict__ h_bf,
-                          bf16_t* __restrict__ hpre_bf) {
+                          bf16_t* __restrict__ dg_bf) {
   const int cv = N / 8;
   const int64_t n = rows * cv;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / cv;
     const int c = (int)(i - r * cv) * 8;
-    float f[8], g[8];
+    float f[8], g[8], d[8];
     ld8_f32(hpre + r * N + c, f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = 0.5f * f[e] * erfcf(-f[e] * 0.70710678118654752f);
+    for (int e = 0; e < 8; ++e) {
+      const float cdf = 0.5f * erfcf(-f[e] * 0.70710678118654752f);
+      g[e] = f[e] * cdf;
+      d[e] = fmaf(f[e], 0.39894228040143268f * expf(-0.5f * f[e] * f[e]), cdf);
+    }
     st_triple8(h3 + r * 3 * N, N, c, g, 0);
     *(u32x4*)(h_bf + r * N + c) = pack8(g);
-    *(u32x4*)(hpre_bf + r * N + c) = pack8(f);
+    *(u32x4*)(dg_bf + r * N + c) = pack8(d);
   }
 }
 
@@ -489,12 +493,12 @@ extern "C" int dfu_layernorm_fwd_x3(const float* x, int64_t ldx, int32_t rows, i
 }
 
 extern "C" int dfu_gelu_x3(const float* hpre, int64_t rows, int32_t N, void* h3, void* h_bf16,
-                           void* hpre_bf16, void* stream) {
-  DFU_CHECK_ARG(hpre && h3 && h_bf16 && hpre_bf16 && N % 8 == 0, "dfu_gelu_x3: bad args");
+                           void* dgelu_bf16, void* stream) {
+  DFU_CHECK_ARG(hpre && h3 && h_bf16 && dgelu_bf16 && N % 8 == 0, "dfu_gelu_x3: bad args");
   const int64_t n = rows * (N / 8);
   if (n == 0) return DFU_OK;
   hipLaunchKernelGGL(k_gelu_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, hpre, rows,
-                     N, (bf16_t*)h3, (bf16_t*)h_bf16, (bf16_t*)hpre_bf16);
+                     N, (bf16_t*)h3, (bf16_t*)h_bf16, (bf16_t*)dgelu_bf16);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -746,17 +746,17 @@ class ViTBlockFn(torch.autograd.Function):
         # MLP branch
         xn2 = _empty((rows, D), BF16, dev)
         m2, r2 = _ln_fwd(xm, blk.norm2, rows, D, xn2)
-        hpre = _empty((rows, Dh), BF16, dev)
+        dgl = _empty((rows, Dh), BF16, dev)
         h = _empty((rows, Dh), BF16, dev)
         ops.gemm(rows, Dh, D, xn2, D, wfc1, D, h, Dh, epilogue=L.EPI_BF16_GELU, bias=bias(mlp.fc1),
-                 aux_out=hpre, ldaux_out=Dh)
+                 aux_out=dgl, ldaux_out=Dh)
         xo = _empty((B, T, D), F32, dev)
         ops.gemm(rows, D, Dh, h, Dh, wfc2, Dh, xo.view(rows, D), D, epilogue=L.EPI_F32_RESID,
                  bias=bias(mlp.fc2), aux=xm, ldaux=D)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
-        ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv,
+        ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
 
@@ -794,7 +794,7 @@ class ViTBlockFn(torch.autograd.Function):
         ops.gemm(rows, Dh, 3 * D, xn2_3, 3 * D, weight_x3_rows(mlp.fc1.weight), 3 * D, hf, Dh,
                  epilogue=L.EPI_F32, bias=bias(mlp.fc1))
         del xn2_3
-        h3, h, hpre = ops.gelu_x3(hf)
+        h3, h, dgl = ops.gelu_x3(hf)  # dgl = bf16 gelu'(pre): the DGELU factor
         del hf
         xo = _empty((B, T, D), F32, dev)
         ops.gemm(rows, D, 3 * Dh, h3, 3 * Dh, weight_x3_rows(mlp.fc2.weight), 3 * Dh,
@@ -803,13 +803,13 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
-        ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv,
+        ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
 
     @staticmethod
     def backward(ctx, gout):
-        (x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, hpre, h, wqkv, wproj, wfc1,
+        (x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv, wproj, wfc1,
          wfc2) = ctx.saved_tensors
         blk = ctx.blk
         attn, mlp = blk.attn, blk.mlp
@@ -832,7 +832,7 @@ class ViTBlockFn(torch.autograd.Function):
         # ---- MLP branch: x_out = x_mid + fc2(gelu(fc1(norm2(x_mid))))
         dh_pre = _empty((rows, Dh), BF16, dev)
         ops.gemm(rows, Dh, D, gb, D, wfc2, Dh, dh_pre, Dh, b_mode=L.OPND_MNMAJOR,
-                 epilogue=L.EPI_BF16_DGELU, aux=hpre, ldaux=Dh)
+                 epilogue=L.EPI_BF16_DGELU, aux=dgl, ldaux=Dh)
         if _wants(mlp.fc2.weight):
             _linear_wgrad(gb, h, mlp.fc2.weight, rows)
         if _wants(mlp.fc2.bias):

@@ -310,12 +310,21 @@ def saliency(dx):
 
 
 # ----------------------------------------------------------------------------- BatchNorm
+def _slice_ws(nbytes, device):
+    """(workspace, per-stream zeroed counters) for a sliced finalize, or (None, None)."""
+    if nbytes <= 0:
+        return None, None
+    return torch.empty(nbytes // 8, dtype=torch.float64, device=device), tile_counters(device)
+
+
 def bn_finalize(stats, M, C, gamma, beta, eps, momentum, running_mean, running_var, nbt,
                 mean_out, invstd_out, scale_out, shift_out):
     tiles = stats_tiles(M)
+    ws, cnt = _slice_ws(lib().dfu_bn_finalize_ws_bytes(tiles, C), stats.device)
     check(lib().dfu_bn_finalize(ptr(stats), tiles, M, C, ptr(gamma), ptr(beta), eps, momentum,
                                 ptr(running_mean), ptr(running_var), ptr(nbt), ptr(mean_out),
-                                ptr(invstd_out), ptr(scale_out), ptr(shift_out), stream_ptr()),
+                                ptr(invstd_out), ptr(scale_out), ptr(shift_out), ptr(ws), ptr(cnt),
+                                0 if cnt is None else cnt.numel(), stream_ptr()),
           "dfu_bn_finalize")
 
 
@@ -345,8 +354,10 @@ def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbet
     check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
                                   ptr(mean), ptr(invstd), M, C, ptr(partial), s),
           "dfu_bn_bwd_reduce")
+    ws, cnt = _slice_ws(lib().dfu_bn_bwd_finalize_ws_bytes(blocks, C), y.device)
     check(lib().dfu_bn_bwd_finalize(ptr(partial), blocks, M, C, ptr(gamma), ptr(invstd),
-                                    int(batch_stats), ptr(dgamma), ptr(dbeta), ptr(coef), s),
+                                    int(batch_stats), ptr(dgamma), ptr(dbeta), ptr(coef),
+                                    ptr(ws), ptr(cnt), 0 if cnt is None else cnt.numel(), s),
           "dfu_bn_bwd_finalize")
     check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
                                  ptr(mean), ptr(invstd), ptr(coef), M, C, ptr(dy), ptr(dres), s),

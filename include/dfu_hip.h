@@ -52,10 +52,10 @@ enum dfu_operand_mode {
 enum dfu_epilogue {
   DFU_EPI_BF16 = 0,          /* C bf16 = alpha*acc + bias                                  */
   DFU_EPI_BF16_RELU = 1,     /* C bf16 = relu(alpha*acc + bias)                             */
-  DFU_EPI_BF16_GELU = 2,     /* aux_out bf16 = pre = acc + bias; C bf16 = gelu(pre fp32)    */
+  DFU_EPI_BF16_GELU = 2,     /* pre = acc + bias: C bf16 = gelu(pre), aux_out bf16 = gelu'(pre) */
   DFU_EPI_F32 = 3,           /* C f32 = alpha*acc + bias                                    */
   DFU_EPI_F32_RESID = 4,     /* C f32 = aux f32 + alpha*acc + bias  (residual stream)       */
-  DFU_EPI_BF16_DGELU = 5,    /* C bf16 = acc * gelu'(aux bf16)                              */
+  DFU_EPI_BF16_DGELU = 5,    /* C bf16 = acc * aux bf16 (aux = the GELU epilogue's gelu')   */
   DFU_EPI_BF16_ADD = 6,      /* C bf16 = acc + aux bf16                                     */
   DFU_EPI_F32_ACC = 7,       /* C f32 += acc   (split-K: fp32 slabs + reduce, or atomics)   */
   DFU_EPI_F32_ACC_CONVW = 8, /* retired: conv wgrad accumulates KRSC + dfu_conv_grad_krsc... */
@@ -189,7 +189,12 @@ int dfu_saliency(const float* dx, int32_t B, int32_t C, int32_t HW, float* out, 
 int dfu_bn_finalize(const float* stats, int32_t tiles, int32_t M, int32_t C, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean,
                     float* running_var, int64_t* num_batches, float* mean_out,
-                    float* invstd_out, float* scale_out, float* shift_out, void* stream);
+                    float* invstd_out, float* scale_out, float* shift_out, double* ws,
+                    int32_t* counters, int32_t ncounters, void* stream);
+/* With ws (dfu_bn_finalize_ws_bytes) and >= C/16 zeroed int32 counters (returned zeroed), the
+ * tiles are reduced in parallel slices whose last block combines them in slice order (same
+ * result for any arrival order); ws or counters NULL: one serial pass per channel group. */
+int64_t dfu_bn_finalize_ws_bytes(int32_t tiles, int32_t C);
 /* Eval-mode BN: scale/shift from running stats. */
 int dfu_bn_eval_coeffs(const float* gamma, const float* beta, const float* running_mean,
                        const float* running_var, float eps, int32_t C, float* scale_out,
@@ -210,7 +215,10 @@ int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* out, int32_t 
  * statistics are constants: dy = gamma*invstd*g). */
 int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t M, int32_t C,
                         const float* gamma, const float* invstd, int32_t batch_stats,
-                        float* dgamma, float* dbeta, float* coef, void* stream);
+                        float* dgamma, float* dbeta, float* coef, double* ws, int32_t* counters,
+                        int32_t ncounters, void* stream);
+/* Workspace of dfu_bn_bwd_finalize's sliced form (as dfu_bn_finalize's). */
+int64_t dfu_bn_bwd_finalize_ws_bytes(int32_t blocks, int32_t C);
 /* dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); optionally dres = g (bf16). */
 int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t relu,
                      const float* scale, const float* shift, const float* mean,
@@ -364,9 +372,10 @@ int dfu_avgpool_fwd_x3(const void* x3, int32_t B, int32_t HW, int32_t C, float* 
 int dfu_layernorm_fwd_x3(const float* x, int64_t ldx, int32_t rows, int32_t D,
                          const float* gamma, const float* beta, float eps, void* out3,
                          void* out_bf16, float* mean, float* rstd, void* stream);
-/* exact GELU of the fp32 fc1 output -> triple [rows][3N], bf16 h and bf16 pre-activation. */
+/* exact GELU of the fp32 fc1 output -> triple [rows][3N], bf16 h and bf16 gelu'(pre) (the
+ * DFU_EPI_BF16_DGELU operand, as DFU_EPI_BF16_GELU's aux_out). */
 int dfu_gelu_x3(const float* hpre, int64_t rows, int32_t N, void* h3, void* h_bf16,
-                void* hpre_bf16, void* stream);
+                void* dgelu_bf16, void* stream);
 /* fp32 softmax attention (SDPA) on fp32 qkv [B*N][3][H][dh] -> o triple [B*N][3*H*dh], o bf16,
  * lse fp32 [B*H][npad] (as dfu_attention_fwd's: the bf16 backward's inputs).  dh == 64,
  * N <= 208. */

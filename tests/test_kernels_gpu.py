@@ -136,8 +136,10 @@ def test_gemm_epilogues(tile):
     close(C, torch.relu(acc + bias), atol=3e-2, rtol=1e-2, what="relu")
     pre = torch.empty_like(C)
     gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_GELU, bias=bias, aux_out=pre, ldaux_out=N)
-    close(pre, acc + bias, atol=3e-2, rtol=1e-2, what="gelu pre")
-    close(C, F.gelu(acc + bias), atol=3e-2, rtol=1e-2, what="gelu")
+    u = acc + bias  # aux_out carries gelu'(pre) (the DGELU epilogue's factor)
+    dgu = 0.5 * (1 + torch.erf(u / math.sqrt(2))) + u * torch.exp(-0.5 * u * u) / math.sqrt(2 * math.pi)
+    close(pre, dgu, atol=3e-2, rtol=1e-2, what="gelu derivative")
+    close(C, F.gelu(u), atol=3e-2, rtol=1e-2, what="gelu")
     res = rnd(M, N, dtype=torch.float32, seed=11)
     Cf = torch.empty(M, N, dtype=torch.float32, device=DEV)
     gemm(M, N, K, A, K, B, K, Cf, N, epilogue=L.EPI_F32_RESID, bias=bias, aux=res, ldaux=N)
@@ -147,9 +149,7 @@ def test_gemm_epilogues(tile):
     acc2 = A.float() @ Bkn.float()
     h = rnd(M, N, seed=13)
     gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N)
-    x = h.float()
-    dg = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
-    close(C, acc2 * dg, atol=5e-2, rtol=1e-2, what="dgelu")
+    close(C, acc2 * h.float(), atol=5e-2, rtol=1e-2, what="dgelu")  # acc * aux (aux = gelu')
     gemm(M, N, K, A, K, Bkn, N, C, N, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16_ADD, aux=h, ldaux=N)
     close(C, acc2 + h.float(), atol=5e-2, rtol=1e-2, what="add")
 

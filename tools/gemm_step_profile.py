@@ -50,6 +50,10 @@ def main():
     ap.add_argument("--ab", action="store_true", help="also time the one-shot schedule")
     ap.add_argument("--tail-ab", action="store_true",
                     help="also time without the tail split (in the '1shot' column)")
+    ap.add_argument("--markers", default=None,
+                    help="PMC mode: before each distinct GEMM, launch one k_argmax_rows marker "
+                         "kernel, then the GEMM 1 + iters times; write the shape list (in "
+                         "launch order) to this JSON for tools/gemm_shape_traffic.py")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(42)
@@ -70,7 +74,14 @@ def main():
         e = uniq.setdefault(key(d), [d, flops, nbytes, refs, 0])
         e[4] += 1
     rows = []
+    marks = []
+    mk = torch.zeros((1, 2), device=dev)
     for d, flops, nbytes, refs, n in uniq.values():
+        if a.markers:
+            torch.cuda.synchronize()
+            ops.argmax_rows(mk)  # segment delimiter in the dispatch trace
+            marks.append({"key": list(key(d)), "per_step": n, "flops": flops, "bytes": nbytes,
+                          "launches": 2 + a.iters})
         us = time_desc(d, a.iters)
         us1 = None
         if a.ab:
@@ -88,6 +99,13 @@ def main():
         t, sk = ctypes.c_int32(), ctypes.c_int32()
         ops.check(ops.lib().dfu_gemm_plan(ctypes.byref(d), ctypes.byref(t), ctypes.byref(sk)), "plan")
         rows.append((n * us, n, us, us1, flops, nbytes, d, t.value, sk.value))
+    if a.markers:
+        import json
+        for m, r in zip(marks, rows):
+            m["us"] = r[2]
+            m["plan"] = [r[7], r[8]]
+        with open(a.markers, "w") as f:
+            json.dump(marks, f)
     rows.sort(key=lambda r: -r[0])
     tot = sum(r[0] for r in rows)
     fl = sum(r[1] * r[4] for r in rows)
