@@ -173,16 +173,18 @@ inline bool fixed_channels(int C) {
 }
 
 // ---------------------------------------------------------------- backward
-// Block of 256 threads = CT column-threads (8 channels each) x (256/CT) row-lanes.
-// Rows per block: each thread walks ~16 rows, and at most ~512 row-blocks exist, so the
-// finalize reduction over blocks stays short.
+// Block of 256 threads = CT column-threads (8 channels each) x (256/CT) row-lanes; each thread
+// keeps RED_U rows' loads in flight per iteration.  Rows per block: a multiple of
+// rl_n * RED_U, grown until at most ~2048 row-blocks exist (8 per CU: the loop is latency-bound,
+// parallelism is what feeds it); the sliced finalize reduces any number of them in parallel.
+constexpr int RED_U = 4;
 inline int bwd_rows_per_block(int64_t M, int C) {
   const int cv = C / 8;
   const int ct_n = cv < 64 ? cv : 64;
   const int rl_n = 256 / ct_n;
-  int64_t rpb = (int64_t)rl_n * 16;
+  int64_t rpb = (int64_t)rl_n * RED_U;
   const int64_t col_groups = cv / ct_n;
-  while ((M + rpb - 1) / rpb * col_groups > 1024 && rpb < M) rpb *= 2;
+  while ((M + rpb - 1) / rpb * col_groups > 2048 && rpb < M) rpb *= 2;
   return (int)rpb;
 }
 
@@ -223,20 +225,32 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; }
   }
-  for (int64_t r = r0 + rl; r < r1; r += rl_n) {
-    const int64_t o = r * C + c0;
-    float g[8], yy[8], oo[8];
-    const u32x4 gv = *(const u32x4*)(dout + o), yv = *(const u32x4*)(y + o);
-    u32x4 ov = {};
-    if constexpr (RELU == 1) ov = *(const u32x4*)(out + o);
-    unpack8(gv, g);
-    unpack8(yv, yy);
-    unpack8(ov, oo);
-    relu_mask8<RELU>(oo, yy, sc, sf, g);
+  // RED_U rows per iteration, every load of the iteration issued before any is used (rows past
+  // r1 load row r0 again and are masked out of the sums)
+  for (int64_t rb = r0 + rl; rb < r1; rb += (int64_t)rl_n * RED_U) {
+    u32x4 gv[RED_U], yv[RED_U], ov[RED_U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      sg[e] += g[e];
-      sgx[e] += g[e] * (yy[e] - mu[e]) * is[e];
+    for (int u = 0; u < RED_U; ++u) {
+      const int64_t r = rb + (int64_t)u * rl_n;
+      const int64_t o = (r < r1 ? r : r0) * C + c0;
+      gv[u] = *(const u32x4*)(dout + o);
+      yv[u] = *(const u32x4*)(y + o);
+      ov[u] = (u32x4){0u, 0u, 0u, 0u};
+      if constexpr (RELU == 1) ov[u] = *(const u32x4*)(out + o);
+    }
+#pragma unroll
+    for (int u = 0; u < RED_U; ++u) {
+      if (rb + (int64_t)u * rl_n >= r1) continue;
+      float g[8], yy[8], oo[8];
+      unpack8(gv[u], g);
+      unpack8(yv[u], yy);
+      unpack8(ov[u], oo);
+      relu_mask8<RELU>(oo, yy, sc, sf, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sg[e] += g[e];
+        sgx[e] += g[e] * (yy[e] - mu[e]) * is[e];
+      }
     }
   }
 #pragma unroll

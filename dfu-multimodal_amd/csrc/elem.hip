@@ -561,6 +561,42 @@ __global__ void k_metrics_accumulate(const float* __restrict__ logits,
   }
 }
 
+// Up to DFU_REDUCE_BATCH independent "sum the per-block partials into a gradient vector"
+// reductions in ONE launch (a ViT block's backward has eight: two LayerNorms' dgamma / dbeta and
+// four bias column sums).  Block j works on entry e = the one whose [first_block, +ceil(D/8))
+// range holds j, 8 columns x 32 row-lanes as k_reduce_partials, same summation order.
+struct ReduceBatch {
+  const float* partial[DFU_REDUCE_BATCH];
+  int64_t stride[DFU_REDUCE_BATCH];
+  float* out[DFU_REDUCE_BATCH];
+  int blocks[DFU_REDUCE_BATCH];
+  int D[DFU_REDUCE_BATCH];
+  int first[DFU_REDUCE_BATCH + 1];
+  int n;
+};
+
+__global__ void k_reduce_partials_batch(const ReduceBatch b) {
+  __shared__ float red[32][8];
+  int e = 0;
+  while (e + 1 < b.n && (int)blockIdx.x >= b.first[e + 1]) ++e;
+  const int cl = threadIdx.x & 7, bl = threadIdx.x >> 3;
+  const int d = ((int)blockIdx.x - b.first[e]) * 8 + cl;
+  const bool ok = d < b.D[e];
+  const float* p = b.partial[e];
+  const int64_t st = b.stride[e];
+  float s = 0.f;
+  if (ok) {
+#pragma unroll 8
+    for (int r = bl; r < b.blocks[e]; r += 32) s += p[(int64_t)r * st + d];
+  }
+  red[bl][cl] = s;
+  __syncthreads();
+  if (bl == 0 && ok) {
+    for (int l = 1; l < 32; ++l) s += red[l][cl];
+    b.out[e][d] += s;
+  }
+}
+
 }  // namespace
 
 #define LAUNCH(kern, n, stream, ...)                                                     \
@@ -695,7 +731,7 @@ extern "C" int dfu_colsum_blocks(int32_t rows) { return (rows + CS_ROWS - 1) / C
 
 extern "C" int dfu_colsum(const void* x, int32_t is_bf16, int64_t ld, int32_t rows, int32_t N,
                           float* out, float* partial, void* stream) {
-  DFU_CHECK_ARG(x && out && partial && rows > 0 && N > 0, "dfu_colsum: bad args");
+  DFU_CHECK_ARG(x && partial && rows > 0 && N > 0, "dfu_colsum: bad args");
   if (is_bf16) DFU_CHECK_ARG(ld % 8 == 0 && ((uintptr_t)x & 15) == 0, "dfu_colsum: bf16 needs ld%%8==0");
   const int blocks = dfu_colsum_blocks(rows);
   dim3 grid((N + 511) / 512, blocks);
@@ -704,6 +740,7 @@ extern "C" int dfu_colsum(const void* x, int32_t is_bf16, int64_t ld, int32_t ro
   else
     hipLaunchKernelGGL(k_colsum<false>, grid, dim3(256), 0, (hipStream_t)stream, x, ld, rows, N, partial);
   DFU_LAUNCH_CHECK();
+  if (out == nullptr) return DFU_OK;  // partials only (reduced later, dfu_reduce_partials_batch)
   hipLaunchKernelGGL(k_reduce_partials, dim3((N + 7) / 8), dim3(256), 0, (hipStream_t)stream,
                      partial, blocks, 1, N, out, (float*)nullptr);
   DFU_LAUNCH_CHECK();
@@ -818,6 +855,31 @@ extern "C" int dfu_metrics_accumulate(const float* logits, const int64_t* labels
   hipLaunchKernelGGL(k_metrics_accumulate, dim3(1), dim3(256), 0, (hipStream_t)stream, logits,
                      labels, rows, C, loss, (unsigned long long*)confusion, loss_sum,
                      (unsigned long long*)batches);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_reduce_partials_batch(const dfu_reduce_entry* entries, int32_t n, void* stream) {
+  DFU_CHECK_ARG(entries && n >= 0 && n <= DFU_REDUCE_BATCH,
+                "dfu_reduce_partials_batch: 0..%d entries", DFU_REDUCE_BATCH);
+  if (n == 0) return DFU_OK;
+  ReduceBatch b;
+  b.n = n;
+  int total = 0;
+  for (int i = 0; i < n; ++i) {
+    const dfu_reduce_entry& en = entries[i];
+    DFU_CHECK_ARG(en.partial && en.out && en.blocks > 0 && en.D > 0 && en.stride >= en.D,
+                  "dfu_reduce_partials_batch: bad entry %d", i);
+    b.partial[i] = en.partial;
+    b.stride[i] = en.stride;
+    b.out[i] = en.out;
+    b.blocks[i] = en.blocks;
+    b.D[i] = en.D;
+    b.first[i] = total;
+    total += (en.D + 7) / 8;
+  }
+  b.first[n] = total;
+  hipLaunchKernelGGL(k_reduce_partials_batch, dim3(total), dim3(256), 0, (hipStream_t)stream, b);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -54,6 +54,13 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class ReduceEntry(ctypes.Structure):
+    """Mirror of `dfu_reduce_entry` (include/dfu_hip.h)."""
+    _fields_ = [("partial", c_void_p), ("stride", c_int64), ("out", c_void_p),
+                ("blocks", c_int32), ("D", c_int32)]
+
+
+REDUCE_BATCH = 8
 P = c_void_p
 I32 = c_int32
 I64 = c_int64
@@ -100,6 +107,7 @@ PROTOTYPES = {
     "dfu_ln_bwd_blocks": [I32],
     "dfu_layernorm_bwd": [P, I64, I32, P, I64, P, P, P, I32, I32, P, I64, P, P, P, P],
     "dfu_reduce_partials": [P, I32, I32, I32, P, P, P],
+    "dfu_reduce_partials_batch": [ctypes.POINTER(ReduceEntry), I32, P],
     "dfu_attention_fwd": [P, I32, I32, I32, I32, F, P, P, P],
     "dfu_attention_bwd": [P, P, P, P, I32, I32, I32, I32, F, P, P, P],
     "dfu_attention_npad": [I32],

@@ -683,22 +683,28 @@ def _ln_fwd(x2d, norm, rows, D, out_bf):
     return mean, rstd
 
 
-def _ln_bwd(dy_bf, x2d, mean, rstd, norm, rows, D, g, g_bf, gsum=False):
+def _ln_bwd(dy_bf, x2d, mean, rstd, norm, rows, D, g, g_bf, gsum=False, batch=None):
+    """LayerNorm backward; dgamma / dbeta reductions go to `batch` (a PartialReductions) when
+    given (the caller reports the parameters done after flushing it)."""
     gsp = ops.layernorm_bwd(dy_bf, D, True, x2d, D, mean, rstd, norm.weight, rows, D, g, D, g_bf,
                             grad_buffer(norm.weight) if _wants(norm.weight) else None,
-                            grad_buffer(norm.bias) if _wants(norm.bias) else None, gsum=gsum)
-    grads_done(norm.weight, norm.bias)
+                            grad_buffer(norm.bias) if _wants(norm.bias) else None, gsum=gsum,
+                            batch=batch)
+    if batch is None:
+        grads_done(norm.weight, norm.bias)
     return gsp
 
 
-def _colsum_of_grad(g, out):
+def _colsum_of_grad(g, out, batch=None):
     """out += column sums of an fp32 residual-stream gradient: from the partial sums its
     producing LayerNorm backward emitted (stashed on the tensor), else a colsum pass."""
     gsp = getattr(g, "_dfu_colsum", None)
-    if gsp is not None:
-        ops.reduce_partials_add(gsp, out)
+    if gsp is None:
+        gsp = ops.colsum_partial(g.reshape(-1, g.shape[-1]))
+    if batch is not None:
+        batch.add(gsp, out, gsp.shape[1])
     else:
-        ops.colsum_add(g.reshape(-1, g.shape[-1]), out)
+        ops.reduce_partials_add(gsp, out)
 
 
 def _bf16_of_grad(g):
@@ -829,6 +835,9 @@ class ViTBlockFn(torch.autograd.Function):
             g = g.clone()
         g2 = g.view(rows, D)
         gb = _bf16_of_grad(gout if gout.dtype == F32 else g).view(rows, D)
+        # the block's eight "sum per-block partials into a gradient vector" reductions (bias
+        # column sums, LayerNorm dgamma / dbeta) run as one launch at the end (PartialReductions)
+        red = ops.PartialReductions()
         # ---- MLP branch: x_out = x_mid + fc2(gelu(fc1(norm2(x_mid))))
         dh_pre = _empty((rows, Dh), BF16, dev)
         ops.gemm(rows, Dh, D, gb, D, wfc2, Dh, dh_pre, Dh, b_mode=L.OPND_MNMAJOR,
@@ -836,27 +845,27 @@ class ViTBlockFn(torch.autograd.Function):
         if _wants(mlp.fc2.weight):
             _linear_wgrad(gb, h, mlp.fc2.weight, rows)
         if _wants(mlp.fc2.bias):
-            _colsum_of_grad(gout if gout.dtype == F32 else g, grad_buffer(mlp.fc2.bias))
-        grads_done(mlp.fc2.weight, mlp.fc2.bias)
+            _colsum_of_grad(gout if gout.dtype == F32 else g, grad_buffer(mlp.fc2.bias), red)
+        grads_done(mlp.fc2.weight)
         dxn2 = _empty((rows, D), BF16, dev)
         ops.gemm(rows, D, Dh, dh_pre, Dh, wfc1, D, dxn2, D, b_mode=L.OPND_MNMAJOR,
                  epilogue=L.EPI_BF16)
         if _wants(mlp.fc1.weight):
             _linear_wgrad(dh_pre, xn2, mlp.fc1.weight, rows)
         if _wants(mlp.fc1.bias):
-            ops.colsum_add(dh_pre, grad_buffer(mlp.fc1.bias))
-        grads_done(mlp.fc1.weight, mlp.fc1.bias)
+            red.add(ops.colsum_partial(dh_pre), grad_buffer(mlp.fc1.bias), Dh)
+        grads_done(mlp.fc1.weight)
         gmb = _empty((rows, D), BF16, dev)
         gsp = _ln_bwd(dxn2, xm, m2, r2, blk.norm2, rows, D, g2, gmb,
-                      gsum=_wants(attn.proj.bias))  # g2 := g_mid (in place)
+                      gsum=_wants(attn.proj.bias), batch=red)  # g2 := g_mid (in place)
         # ---- attention branch: x_mid = x_in + proj(attn(norm1(x_in)))
         do = _empty((rows, D), BF16, dev)
         ops.gemm(rows, D, D, gmb, D, wproj, D, do, D, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_BF16)
         if _wants(attn.proj.weight):
             _linear_wgrad(gmb, o, attn.proj.weight, rows)
         if _wants(attn.proj.bias):
-            ops.reduce_partials_add(gsp, grad_buffer(attn.proj.bias))
-        grads_done(attn.proj.weight, attn.proj.bias)
+            red.add(gsp, grad_buffer(attn.proj.bias), D)
+        grads_done(attn.proj.weight)
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, T, H, dh, attn.scale)
         dxn1 = _empty((rows, D), BF16, dev)
         ops.gemm(rows, D, 3 * D, dqkv, 3 * D, wqkv, D, dxn1, D, b_mode=L.OPND_MNMAJOR,
@@ -864,11 +873,14 @@ class ViTBlockFn(torch.autograd.Function):
         if _wants(attn.qkv.weight):
             _linear_wgrad(dqkv, xn1, attn.qkv.weight, rows)
         if _wants(attn.qkv.bias):
-            ops.colsum_add(dqkv, grad_buffer(attn.qkv.bias))
-        grads_done(attn.qkv.weight, attn.qkv.bias)
+            red.add(ops.colsum_partial(dqkv), grad_buffer(attn.qkv.bias), 3 * D)
+        grads_done(attn.qkv.weight)
         gib = _empty((B, T, D), BF16, dev)
         gsp = _ln_bwd(dxn1, x2, m1, r1, blk.norm1, rows, D, g2, gib.view(rows, D),
-                      gsum=True)  # g2 := g_in
+                      gsum=True, batch=red)  # g2 := g_in
+        red.flush()
+        grads_done(mlp.fc2.bias, mlp.fc1.bias, blk.norm2.weight, blk.norm2.bias,
+                   attn.proj.bias, attn.qkv.bias, blk.norm1.weight, blk.norm1.bias)
         gin = g.view(B, T, D)
         gin._dfu_bf16 = gib
         gin._dfu_colsum = gsp  # the previous block's fc2.bias gradient, pre-reduced

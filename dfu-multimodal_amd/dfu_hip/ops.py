@@ -402,9 +402,10 @@ def layernorm_fwd(x, ldx, rows, D, gamma, beta, eps, out, ldo, out_bf16, mean, r
 
 
 def layernorm_bwd(dy, lddy, dy_bf16, x, ldx, mean, rstd, gamma, rows, D, gx, ldg, gx_bf16,
-                  dgamma, dbeta, gsum=False):
+                  dgamma, dbeta, gsum=False, batch=None):
     """LayerNorm backward (gx += dx).  With gsum=True also returns the [blocks][D] partial
-    column sums of the updated gx (reduce with reduce_partials_add)."""
+    column sums of the updated gx (reduce with reduce_partials_add).  batch: a
+    PartialReductions that takes the dgamma / dbeta reductions instead of a launch here."""
     blocks = lib().dfu_ln_bwd_blocks(rows)
     partial = torch.empty((blocks, 2, D), dtype=F32, device=x.device)
     gsp = torch.empty((blocks, D), dtype=F32, device=x.device) if gsum else None
@@ -412,10 +413,55 @@ def layernorm_bwd(dy, lddy, dy_bf16, x, ldx, mean, rstd, gamma, rows, D, gx, ldg
     check(lib().dfu_layernorm_bwd(ptr(dy), lddy, int(dy_bf16), ptr(x), ldx, ptr(mean), ptr(rstd),
                                   ptr(gamma), rows, D, ptr(gx), ldg, ptr(gx_bf16), ptr(partial),
                                   ptr(gsp), s), "dfu_layernorm_bwd")
-    if dgamma is not None or dbeta is not None:
+    if batch is not None:
+        batch.add(partial, dgamma, D, stride=2 * D, offset=0)
+        batch.add(partial, dbeta, D, stride=2 * D, offset=D)
+    elif dgamma is not None or dbeta is not None:
         check(lib().dfu_reduce_partials(ptr(partial), blocks, 2, D, ptr(dgamma), ptr(dbeta), s),
               "dfu_reduce_partials")
     return gsp
+
+
+class PartialReductions:
+    """Collects "out += sum over blocks of partial" reductions and runs them as ONE launch
+    (dfu_reduce_partials_batch) per flush; the partial slabs stay referenced until then."""
+
+    def __init__(self):
+        self.entries = []
+        self.keep = []
+
+    def add(self, partial, out, D, stride=None, offset=0, blocks=None):
+        if out is None:
+            return
+        blocks = partial.shape[0] if blocks is None else blocks
+        stride = D if stride is None else stride
+        self.entries.append((partial.data_ptr() + 4 * offset, stride, out.data_ptr(), blocks, D))
+        self.keep.append(partial)
+        if len(self.entries) == L.REDUCE_BATCH:
+            self.flush()
+
+    def flush(self):
+        if not self.entries:
+            return
+        arr = (L.ReduceEntry * len(self.entries))()
+        for i, (p, st, o, b, d) in enumerate(self.entries):
+            arr[i].partial, arr[i].stride, arr[i].out, arr[i].blocks, arr[i].D = p, st, o, b, d
+        check(lib().dfu_reduce_partials_batch(arr, len(self.entries), stream_ptr()),
+              "dfu_reduce_partials_batch")
+        self.entries = []
+        self.keep = []
+
+
+def colsum_partial(x, is_bf16=None):
+    """Per-block partial column sums of x[rows, N] (the first half of colsum_add)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    rows, N = x2.shape
+    bf = (x.dtype == BF16) if is_bf16 is None else is_bf16
+    blocks = lib().dfu_colsum_blocks(rows)
+    partial = torch.empty((blocks, N), dtype=F32, device=x.device)
+    check(lib().dfu_colsum(ptr(x2), int(bf), x2.stride(0), rows, N, None, ptr(partial),
+                           stream_ptr()), "dfu_colsum")
+    return partial
 
 
 def reduce_partials_add(partial, out):

@@ -254,6 +254,17 @@ int dfu_layernorm_bwd(const void* dy, int64_t lddy, int32_t dy_bf16, const float
 /* Sum a [blocks][nvec][D] partial slab over blocks and ADD into out[v] (v < nvec). */
 int dfu_reduce_partials(const float* partial, int32_t blocks, int32_t nvec, int32_t D,
                         float* out0, float* out1, void* stream);
+/* Several such reductions in one launch: out[d] += sum_b partial[b * stride + d], d < D, per
+ * entry (host array of n <= DFU_REDUCE_BATCH entries; same sums as dfu_reduce_partials). */
+#define DFU_REDUCE_BATCH 8
+typedef struct dfu_reduce_entry {
+  const float* partial;
+  int64_t stride; /* elements between consecutive blocks' rows */
+  float* out;
+  int32_t blocks;
+  int32_t D;
+} dfu_reduce_entry;
+int dfu_reduce_partials_batch(const dfu_reduce_entry* entries, int32_t n, void* stream);
 
 /* ---------------------------------------------------------------- attention --------- */
 /* timm Attention with F.scaled_dot_product_attention: qkv bf16 [B*N][3][H][dh] (the qkv
@@ -277,7 +288,8 @@ int dfu_vit_embed_bwd(const float* gx, int32_t B, int32_t T, int32_t D, float* d
                       float* dpos, float* dbias, void* gpatch, float* partial, void* stream);
 
 /* ---------------------------------------------------------------- elementwise ------- */
-/* Column sums of a bf16/fp32 [rows][N] matrix ADDED into out fp32 [N] (bias grads). */
+/* Column sums of a bf16/fp32 [rows][N] matrix ADDED into out fp32 [N] (bias grads); out NULL:
+ * only the per-block partials [dfu_colsum_blocks(rows)][N] are written. */
 int dfu_colsum(const void* x, int32_t is_bf16, int64_t ld, int32_t rows, int32_t N, float* out,
                float* partial, void* stream);
 int dfu_colsum_blocks(int32_t rows);
