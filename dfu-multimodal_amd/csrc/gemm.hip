@@ -71,8 +71,10 @@ const TunedPlan kTuned[] = {
 
 const TunedPlan* find_tuned(const dfu_gemm_desc* d) {
   const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
+  // the BN-statistics dgrad runs the tile its plain-bf16 twin was tuned to
+  const int epi = d->epilogue == DFU_EPI_BF16_DSTATS ? DFU_EPI_BF16 : d->epilogue;
   for (const TunedPlan& t : kTuned) {
-    if (t.a != d->a_mode || t.b != d->b_mode || t.e != d->epilogue || t.M != d->M ||
+    if (t.a != d->a_mode || t.b != d->b_mode || t.e != epi || t.M != d->M ||
         t.N != d->N || t.K != d->K)
       continue;
     if (conv && (t.cn != d->conv_n || t.ch != d->conv_h || t.cw != d->conv_w ||
@@ -381,6 +383,13 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
     DFU_CHECK_ARG(d->ldb >= round8(d->N), "dfu_gemm: MN-major B needs ldb >= round8(N)");
   if (d->epilogue == DFU_EPI_BF16_STATS || d->epilogue == DFU_EPI_F32_STATS)
     DFU_CHECK_ARG(d->stats != nullptr, "dfu_gemm: STATS epilogue needs a stats slab");
+  if (d->epilogue == DFU_EPI_BF16_DSTATS) {
+    DFU_CHECK_ARG(d->stats != nullptr && d->aux != nullptr && d->bn_coef != nullptr &&
+                      d->ldaux >= d->N,
+                  "dfu_gemm: DSTATS epilogue needs a stats slab, aux (y) and bn_coef");
+    DFU_CHECK_ARG(d->a_mode != DFU_OPND_CONV_DGRAD || d->conv_stride == 1,
+                  "dfu_gemm: DSTATS epilogue on a strided dgrad is not supported");
+  }
 
   const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
   if (conv) {
@@ -463,6 +472,7 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   a.aux = d->aux; a.ldaux = d->ldaux;
   a.aux_out = d->aux_out; a.ldaux_out = d->ldaux_out;
   a.stats = d->stats;
+  a.bn_coef = d->bn_coef;
   a.split = splits;
   a.n4 = (d->N % 4 == 0 && d->ldc % 4 == 0 && (d->aux == nullptr || d->ldaux % 4 == 0) &&
           (d->aux_out == nullptr || d->ldaux_out % 4 == 0))

@@ -23,7 +23,8 @@ c_char_p = ctypes.c_char_p
 OPND_KMAJOR, OPND_MNMAJOR, OPND_CONV_FWD, OPND_CONV_DGRAD, OPND_CONV_DGRAD_W, OPND_CONV_WGRAD_X = range(6)
 # enum dfu_epilogue
 (EPI_BF16, EPI_BF16_RELU, EPI_BF16_GELU, EPI_F32, EPI_F32_RESID, EPI_BF16_DGELU, EPI_BF16_ADD,
- EPI_F32_ACC, EPI_F32_ACC_CONVW, EPI_BF16_STATS, EPI_PATCH, EPI_F32_STATS) = range(12)
+ EPI_F32_ACC, EPI_F32_ACC_CONVW, EPI_BF16_STATS, EPI_PATCH, EPI_F32_STATS,
+ EPI_BF16_DSTATS) = range(13)
 
 DFU_E_INVALID = 1001
 DFU_E_UNSUPPORTED = 1002
@@ -51,6 +52,7 @@ class GemmDesc(ctypes.Structure):
         ("tile", c_int32),
         ("workspace", c_void_p), ("workspace_bytes", c_int64),
         ("tile_counters", c_void_p), ("tile_counters_len", c_int32),
+        ("bn_coef", c_void_p),
     ]
 
 

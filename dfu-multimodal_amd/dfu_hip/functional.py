@@ -21,6 +21,7 @@ Conventions:
     (the producer of every such tensor is a Function in this file).
 """
 import math
+import os
 import weakref
 
 import torch
@@ -226,10 +227,10 @@ class _BN:
         self.bn = bn
         self.M, self.C = M, C
         self.training = bn.training or not bn.track_running_stats
-        self.mean = _empty((C,), F32, device)
-        self.invstd = _empty((C,), F32, device)
-        self.scale = _empty((C,), F32, device)
-        self.shift = _empty((C,), F32, device)
+        # one [4][C] block (rows scale, shift, mean, invstd): the DSTATS dgrad epilogue's
+        # bn_coef operand (include/dfu_hip.h DFU_EPI_BF16_DSTATS)
+        self.coef4 = _empty((4, C), F32, device)
+        self.scale, self.shift, self.mean, self.invstd = self.coef4.unbind(0)
 
     def forward_coeffs(self, stats):
         bn = self.bn
@@ -258,6 +259,17 @@ class _BN:
         ops.bn_bwd(dout, y, out, relu, self.mean, self.invstd, bn.weight, self.M, self.C, dy,
                    dres, dgamma, dbeta, batch_stats=self.training, scale=self.scale,
                    shift=self.shift)
+        grads_done(bn.weight, bn.bias)
+
+    def backward_from_dstats(self, dstats, dout, y, dy):
+        """BN + ReLU (no residual) backward whose reduction already ran in the epilogue of the
+        dgrad that produced `dout` (conv_dgrad(..., bn=self)): finalize + apply only."""
+        bn = self.bn
+        dgamma = grad_buffer(bn.weight) if _wants(bn.weight) else None
+        dbeta = grad_buffer(bn.bias) if _wants(bn.bias) else None
+        ops.bn_bwd_finish(dstats, dstats.shape[0], dout, y, None, 2, self.mean, self.invstd,
+                          bn.weight, self.M, self.C, dy, None, dgamma, dbeta,
+                          batch_stats=self.training, scale=self.scale, shift=self.shift)
         grads_done(bn.weight, bn.bias)
 
 
@@ -290,19 +302,28 @@ def conv_fwd_x3(x3_rows, geom, w3, y, stats):
                  epilogue=L.EPI_F32_STATS, stats=stats, conv=g3)
 
 
-def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None):
-    """dx[N*H*W, C] = dgrad(dy) (+ add, bf16)."""
+def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, bn=None, y=None):
+    """dx[N*H*W, C] = dgrad(dy) (+ add, bf16).  With bn (a _BN whose input y is this conv's
+    input, BN + ReLU without residual; stride 1): the epilogue also reduces that BN's
+    backward sums over dx (DFU_EPI_BF16_DSTATS); returns the [tiles][2][C] records for
+    _BN.backward_from_dstats."""
     g = geom
     Mx = g.n * g.h * g.w
     epi = L.EPI_BF16_ADD if add is not None else L.EPI_BF16
-    ld_add = g.c if add is not None else 0
+    aux, ld_aux, stats = add, (g.c if add is not None else 0), None
+    if bn is not None:
+        assert add is None and g.stride == 1 and y is not None and y.shape == (Mx, g.c)
+        epi, aux, ld_aux = L.EPI_BF16_DSTATS, y, g.c
+        stats = _empty((ops.stats_tiles(Mx), 2, g.c), F32, dx.device)
+    coef = bn.coef4 if bn is not None else None
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
         ops.gemm(Mx, g.c, g.k, dy_rows, g.k, w_krsc, g.c, dx, g.c, b_mode=L.OPND_MNMAJOR,
-                 epilogue=epi, aux=add, ldaux=ld_add)
+                 epilogue=epi, aux=aux, ldaux=ld_aux, stats=stats, bn_coef=coef)
     else:
         ops.gemm(Mx, g.c, g.r * g.s * g.k, dy_rows, 0, w_krsc, g.r * g.s * g.c, dx, g.c,
-                 a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=epi, aux=add,
-                 ldaux=ld_add, conv=g)
+                 a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=epi, aux=aux,
+                 ldaux=ld_aux, conv=g, stats=stats, bn_coef=coef)
+    return stats
 
 
 def conv_wgrad(dy_rows, x_rows, geom, dw):
@@ -420,6 +441,18 @@ def _fire_grad_hooks(probe, grad):
     gradient the fused backward computed for the tensor it stands for."""
     for hook in list((probe._backward_hooks or {}).values()):
         hook(grad)
+
+
+# BN + ReLU backward sums of bn1 / bn2 in the epilogue of the dgrad producing their output
+# gradient (DFU_EPI_BF16_DSTATS) instead of a separate dfu_bn_bwd_reduce pass, for BNs of at
+# least FUSE_BN_DSTATS_MIN_C channels (tools/dstats_time.py on MI355X: layer3's 12544 x 256
+# dgrads gain ~4 us net, layer1's 200704 x 64 ones lose ~5 us: their many small-N tiles pay
+# the epilogue's VALU work more than the separate 13 us pass costs).  Off by default: in the
+# two-stream fusion step every threshold measured slower (20.70-20.76 ms vs 20.62 ms per step,
+# same box), the longer dgrads delaying the ResNet stream more than the small reduce passes
+# that overlap the ViT stream.  DFU_FUSE_BN_DSTATS=1 enables it.
+FUSE_BN_DSTATS = os.environ.get("DFU_FUSE_BN_DSTATS", "0") != "0"
+FUSE_BN_DSTATS_MIN_C = int(os.environ.get("DFU_FUSE_BN_DSTATS_MIN_C", "128"))
 
 
 class BottleneckFn(torch.autograd.Function):
@@ -549,9 +582,10 @@ class BottleneckFn(torch.autograd.Function):
             if _wants(dconv.weight):
                 conv_wgrad(dyd, xr, gd, grad_buffer(dconv.weight))
                 grads_done(dconv.weight)
-        # conv3
+        # conv3 (bf16 mode: bn2's backward sums reduced in its dgrad epilogue)
+        fuse = not ctx.x3 and FUSE_BN_DSTATS and g2.k >= FUSE_BN_DSTATS_MIN_C
         da2 = torch.empty_like(a2)
-        conv_dgrad(dy3, g3, w3, da2)
+        st2 = conv_dgrad(dy3, g3, w3, da2, bn=s2 if fuse else None, y=y2)
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[1], from_rows(da2, B, g2.p, g2.q, g2.k))
         if _wants(mod.conv3.weight):
@@ -561,9 +595,12 @@ class BottleneckFn(torch.autograd.Function):
         # BN + ReLU masks: recomputed from y (bf16), or in bf16x3 mode (fp32 pre-activations)
         # read from the forward's outputs
         dy2 = torch.empty_like(y2)
-        s2.backward(da2, y2, a2 if ctx.x3 else None, 1 if ctx.x3 else 2, dy2, None)
+        if st2 is not None:
+            s2.backward_from_dstats(st2, da2, y2, dy2)
+        else:
+            s2.backward(da2, y2, a2 if ctx.x3 else None, 1 if ctx.x3 else 2, dy2, None)
         da1 = torch.empty_like(a1)
-        conv_dgrad(dy2, g2, w2, da1)
+        st1 = conv_dgrad(dy2, g2, w2, da1, bn=s1 if fuse and g2.stride == 1 else None, y=y1)
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[0], from_rows(da1, B, g1.p, g1.q, g1.k))
         if _wants(mod.conv2.weight):
@@ -571,7 +608,10 @@ class BottleneckFn(torch.autograd.Function):
             grads_done(mod.conv2.weight)
         # bn1 + relu, conv1 (+ identity gradient fused in the dgrad epilogue)
         dy1 = torch.empty_like(y1)
-        s1.backward(da1, y1, a1 if ctx.x3 else None, 1 if ctx.x3 else 2, dy1, None)
+        if st1 is not None:
+            s1.backward_from_dstats(st1, da1, y1, dy1)
+        else:
+            s1.backward(da1, y1, a1 if ctx.x3 else None, 1 if ctx.x3 else 2, dy1, None)
         dx = None
         if ctx.x_requires_grad:
             dxr = _empty((M1, Cin), BF16, dev)

@@ -68,7 +68,8 @@ def _algorithmic_bytes(d, conv):
     b = act_in if d.b_mode == L.OPND_CONV_WGRAD_X else 2 * N * K
     e = d.epilogue
     c = {L.EPI_F32: 4, L.EPI_F32_RESID: 8, L.EPI_F32_ACC: 8, L.EPI_PATCH: 4, L.EPI_F32_STATS: 4,
-         L.EPI_BF16_GELU: 4, L.EPI_BF16_DGELU: 4, L.EPI_BF16_ADD: 4}.get(e, 2) * M * N
+         L.EPI_BF16_GELU: 4, L.EPI_BF16_DGELU: 4, L.EPI_BF16_ADD: 4,
+         L.EPI_BF16_DSTATS: 4}.get(e, 2) * M * N
     return a + b + c
 
 
@@ -82,7 +83,8 @@ def gemm_replay(records, stream=None):
 
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
          epilogue=L.EPI_BF16, alpha=1.0, bias=None, aux=None, ldaux=0, aux_out=None,
-         ldaux_out=0, stats=None, split_k=0, ep_tokens=0, conv=None, tile=0, workspace=None):
+         ldaux_out=0, stats=None, split_k=0, ep_tokens=0, conv=None, tile=0, workspace=None,
+         bn_coef=None):
     """C = epilogue(A @ B^T).  `split_k` (F32_ACC only): 0 = library cost model, 1 = none.
     `tile`: 0 = library cost model, else a TILES id.  Split-K partials go to fp32 slabs in
     `workspace` (allocated here from the stream-ordered caching allocator when None) and are
@@ -103,6 +105,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
     d.aux_out = aux_out.data_ptr() if aux_out is not None else None
     d.ldaux_out = int(ldaux_out)
     d.stats = stats.data_ptr() if stats is not None else None
+    d.bn_coef = bn_coef.data_ptr() if bn_coef is not None else None
     d.split_k = int(split_k)
     d.ep_tokens = int(ep_tokens)
     d.tile = int(tile)
@@ -124,7 +127,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
         if a_mode == L.OPND_CONV_DGRAD and conv is not None:
             flops /= conv.stride * conv.stride  # algorithmic: only the 1/stride^2 live taps
         gemm_record.append((d, flops, _algorithmic_bytes(d, conv),
-                            (A, B, C, bias, aux, aux_out, stats, workspace)))
+                            (A, B, C, bias, aux, aux_out, stats, workspace, bn_coef)))
 
 
 _COUNTERS = {}
@@ -339,6 +342,23 @@ def bn_apply(y, scale, shift, residual, relu, out, M, C):
                              M, C, stream_ptr()), "dfu_bn_apply")
 
 
+def bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres,
+                  dgamma, dbeta, batch_stats=True, scale=None, shift=None):
+    """BN backward after the reduction: finalize the [blocks][2][C] partial sums (from
+    dfu_bn_bwd_reduce, or a DSTATS dgrad epilogue's per-128-row records) -> apply."""
+    relu = int(relu)
+    coef = torch.empty((C, 3), dtype=F32, device=y.device)
+    s = stream_ptr()
+    ws, cnt = _slice_ws(lib().dfu_bn_bwd_finalize_ws_bytes(blocks, C), y.device)
+    check(lib().dfu_bn_bwd_finalize(ptr(partial), blocks, M, C, ptr(gamma), ptr(invstd),
+                                    int(batch_stats), ptr(dgamma), ptr(dbeta), ptr(coef),
+                                    ptr(ws), ptr(cnt), 0 if cnt is None else cnt.numel(), s),
+          "dfu_bn_bwd_finalize")
+    check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
+                                 ptr(mean), ptr(invstd), ptr(coef), M, C, ptr(dy), ptr(dres), s),
+          "dfu_bn_bwd_apply")
+
+
 def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta,
            batch_stats=True, scale=None, shift=None):
     """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply.  relu: False/0 none;
@@ -349,19 +369,11 @@ def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbet
         raise ValueError("bn_bwd: relu=2 needs the forward scale/shift")
     blocks = lib().dfu_bn_bwd_blocks(M, C)
     partial = torch.empty((blocks, 2, C), dtype=F32, device=y.device)
-    coef = torch.empty((C, 3), dtype=F32, device=y.device)
-    s = stream_ptr()
     check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
-                                  ptr(mean), ptr(invstd), M, C, ptr(partial), s),
+                                  ptr(mean), ptr(invstd), M, C, ptr(partial), stream_ptr()),
           "dfu_bn_bwd_reduce")
-    ws, cnt = _slice_ws(lib().dfu_bn_bwd_finalize_ws_bytes(blocks, C), y.device)
-    check(lib().dfu_bn_bwd_finalize(ptr(partial), blocks, M, C, ptr(gamma), ptr(invstd),
-                                    int(batch_stats), ptr(dgamma), ptr(dbeta), ptr(coef),
-                                    ptr(ws), ptr(cnt), 0 if cnt is None else cnt.numel(), s),
-          "dfu_bn_bwd_finalize")
-    check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
-                                 ptr(mean), ptr(invstd), ptr(coef), M, C, ptr(dy), ptr(dres), s),
-          "dfu_bn_bwd_apply")
+    bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres,
+                  dgamma, dbeta, batch_stats, scale, shift)
 
 
 # ------------------------------------------------------------------------------- pooling

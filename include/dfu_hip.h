@@ -61,8 +61,16 @@ enum dfu_epilogue {
   DFU_EPI_F32_ACC_CONVW = 8, /* retired: conv wgrad accumulates KRSC + dfu_conv_grad_krsc... */
   DFU_EPI_BF16_STATS = 9,    /* C bf16 = acc; per-column (sum, M2) of each 128-row tile     */
   DFU_EPI_PATCH = 10,        /* ViT patch-embed: C f32 [B][T+1][N] row 1+p = acc+bias+pos   */
-  DFU_EPI_F32_STATS = 11     /* C f32 = acc; per-column (sum, M2) of each 128-row tile (the
+  DFU_EPI_F32_STATS = 11,    /* C f32 = acc; per-column (sum, M2) of each 128-row tile (the
                                 split-bf16 "bf16x3" forward: BN statistics of unrounded y)  */
+  DFU_EPI_BF16_DSTATS = 12   /* BatchNorm backward statistics in the dgrad that produces the
+                                BN output's gradient: C bf16 = g = alpha*acc; per column of
+                                each 128-row tile, stats[tile][0] = sum g', stats[tile][1] =
+                                sum g' (y - mean) invstd over g' = g masked by the forward's
+                                ReLU (fma(y, scale, shift) > 0), y = aux bf16 (the BN input),
+                                bn_coef = fp32 [4][N] rows scale, shift, mean, invstd.  The
+                                records feed dfu_bn_bwd_finalize (blocks = ceil(M/128)) in
+                                place of dfu_bn_bwd_reduce.  Stride-1 launches only.         */
 };
 
 typedef struct dfu_gemm_desc {
@@ -100,6 +108,7 @@ typedef struct dfu_gemm_desc {
    * buffer per stream (launches on one stream never overlap). */
   int32_t* tile_counters;
   int32_t tile_counters_len;
+  const float* bn_coef; /* DFU_EPI_BF16_DSTATS: fp32 [4][N] scale, shift, mean, invstd      */
 } dfu_gemm_desc;
 
 int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
