@@ -13,10 +13,13 @@ using namespace dfu;
 namespace {
 
 constexpr int kCUs = 256;
-constexpr int kTM[NTILES] = {128, 256, 128, 256, 128, 128, 256};
-constexpr int kTN[NTILES] = {128, 128, 256, 256, 128, 128, 256};
-constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 2, 1};  // workgroups per CU
-constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false};  // kTail
+constexpr int kTM[NTILES] = {128, 256, 128, 256, 128, 128, 256, 128, 256, 128, 128, 128, 256};
+constexpr int kTN[NTILES] = {128, 128, 256, 256, 128, 128, 256, 128, 128, 256, 128, 128, 256};
+constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 2, 2, 1};  // workgroups per CU
+// the tile a pipelined twin shares its geometry (and fitted step time) with
+constexpr int kBase[NTILES] = {0, 1, 2, 3, 4, 5, 6, 0, 1, 2, 4, 5, 6};
+constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false,
+                                  true, false, false, true, false, false};  // kTail
 // Wave-quantisation cost model: a launch takes ceil(tiles * splits / 256) rounds (one 512-thread
 // workgroup per CU), each costing kRoundUs (prologue fill + epilogue) + k-steps * kStepUs.
 // Fitted on MI355X to tools/gemm_bench.py --sweep (ViT qkv K=768 vs fc2 K=3072 forward rows,
@@ -24,14 +27,18 @@ constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false}
 // 256x256 moves 1.62x more MFMA work per microsecond than 128x128.
 // The 2-per-CU 128x128 variant: two co-resident workgroups share the MFMA pipe (step cost per
 // workgroup ~doubles) but hide each other's fill and epilogue.
-// (the phased 256x256 is priced high: only the offline-tuned table selects it)
-constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70, 0.65, 3.0};
-constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1, 6.1, 20.0};
+// (the phased 256x256 and the pipelined twins are priced high: only the offline-tuned table
+// selects them)
+constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70, 0.65, 3.0,
+                                    3.0, 3.0, 3.0, 3.0, 3.0, 3.0};
+constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1, 6.1, 20.0,
+                                     20.0, 20.0, 20.0, 20.0, 20.0, 20.0};
 constexpr double kSlabGBs = 5000.0;  // split-K: slab write + reduce (read slabs, RMW C)
 constexpr double kReduceLaunchUs = 2.0;
 // Persistent schedule (gemm_kernel.h): a workgroup owning several work units pays one
 // prologue fill for all of them plus, per unit, the epilogue time its MFMAs do not hide.
-constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0};
+constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0, 3.0, 3.0, 3.0, 3.0, 3.0,
+                                    3.0};
 int g_persistent = 1;       // dfu_gemm_set_persistent
 int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
@@ -40,9 +47,13 @@ int g_tail_split = 1;       // dfu_gemm_set_tail_split
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
-                               kTable128x128o2, kTable128x128w4, kTable256x256p8};
+                               kTable128x128o2, kTable128x128w4, kTable256x256p8,
+                               kTable128x128pp, kTable256x128pp, kTable128x256pp,
+                               kTable128x128o2pp, kTable128x128w4pp, kTable256x256ps};
   const int ns[NTILES] = {kTable128x128N, kTable256x128N, kTable128x256N, kTable256x256N,
-                          kTable128x128o2N, kTable128x128w4N, kTable256x256p8N};
+                          kTable128x128o2N, kTable128x128w4N, kTable256x256p8N,
+                          kTable128x128ppN, kTable256x128ppN, kTable128x256ppN,
+                          kTable128x128o2ppN, kTable128x128w4ppN, kTable256x256psN};
   for (int i = 0; i < ns[tile]; ++i) {
     const Entry& en = tabs[tile][i];
     if (en.a == a && en.b == b && en.e == e) return &en;
@@ -247,7 +258,7 @@ Tail tail_for(const dfu_gemm_desc* d, const Plan& pl) {
   if (!pl.entry || d->epilogue == DFU_EPI_F32_ACC || !kTailOK[pl.tile]) return Tail();
   const int tiles = cdiv(d->M, kTM[pl.tile]) * cdiv(d->N, kTN[pl.tile]);
   return tail_plan(tiles, kCUs * kOcc[pl.tile], cdiv(d->K, BK), kTM[pl.tile], kTN[pl.tile],
-                   kStepUs[pl.tile]);
+                   kStepUs[kBase[pl.tile]]);
 }
 
 }  // namespace
@@ -489,10 +500,12 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   // in-kernel split-K reduction: the last split of a tile to finish adds the slabs into C
   a.counters = nullptr;
   if (a.slab != nullptr && g_inkernel_reduce && splits <= 8 && d->tile_counters != nullptr &&
-      d->tile_counters_len >= a.tiles_m * a.tiles_n && pl.tile != T256x256p8)
+      d->tile_counters_len >= a.tiles_m * a.tiles_n && pl.tile != T256x256p8 &&
+      pl.tile != T256x256ps)
     a.counters = d->tile_counters;
   // the phased kernel has neither fp32 atomics nor the in-kernel reduction: split-K needs slabs
-  DFU_CHECK_ARG(!(pl.tile == T256x256p8 && acc_epi && splits > 1 && a.slab == nullptr),
+  DFU_CHECK_ARG(!((pl.tile == T256x256p8 || pl.tile == T256x256ps) && acc_epi && splits > 1 &&
+                  a.slab == nullptr),
                 "dfu_gemm: split-K on the phased 256x256 tile needs a workspace "
                 "(dfu_gemm_workspace_bytes)");
   a.ep_tokens = d->ep_tokens;
@@ -512,6 +525,18 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   a.dbg = dbg;
   a.m_ld_bound = round8(d->M);
   a.n_ld_bound = round8(d->N);
+  {
+    // operand extents (elements): K-contiguous [MN][ld], MN-major [K][ld]
+    const int64_t ea = d->a_mode == DFU_OPND_MNMAJOR ? (int64_t)(d->K - 1) * d->lda + a.m_ld_bound
+                                                     : (int64_t)(d->M - 1) * d->lda + d->K;
+    const int64_t eb = d->b_mode == DFU_OPND_MNMAJOR ? (int64_t)(d->K - 1) * d->ldb + a.n_ld_bound
+                                                     : (int64_t)(d->N - 1) * d->ldb + d->K;
+    if (pl.tile == T256x256ps)
+      DFU_CHECK_ARG(2 * ea < kRsrcBytes && 2 * eb < kRsrcBytes,
+                    "dfu_gemm: operands over 2 GiB need another tile than the buffer-DMA 256x256");
+    a.a_bytes = (int)(2 * ea < kRsrcBytes ? 2 * ea : kRsrcBytes);
+    a.b_bytes = (int)(2 * eb < kRsrcBytes ? 2 * eb : kRsrcBytes);
+  }
   if (d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD) {
     a.div_pq = make_fastdiv(a.cp * a.cq);
     a.div_q = make_fastdiv(a.cq);
@@ -540,7 +565,8 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   a.tail_full = a.tail_r = a.tail_s = a.tail_kps = 0;
   a.tslab = nullptr;
   if (!acc_epi && splits == 1 && kTailOK[pl.tile]) {
-    const Tail t = tail_plan(a.tiles_m * a.tiles_n, slots, a.ktiles, TM, TN, kStepUs[pl.tile]);
+    const Tail t =
+        tail_plan(a.tiles_m * a.tiles_n, slots, a.ktiles, TM, TN, kStepUs[kBase[pl.tile]]);
     if (t.r > 0 && d->workspace != nullptr && d->workspace_bytes >= t.bytes &&
         d->tile_counters != nullptr && d->tile_counters_len >= t.r) {
       a.tail_full = t.full; a.tail_r = t.r; a.tail_s = t.s; a.tail_kps = t.kps;

@@ -1,0 +1,380 @@
+// Persistent phased 256x256 GEMM (tile 13): the K-step body of gemm_p8.hip (four 16-MFMA
+// quadrant phases, the next K-step's half-tile DMA issued in phases 1-2, one barrier per K-step)
+// run over ONE continuous stream of K-steps per workgroup, across its work units: the DMA of a
+// unit's first K-step is issued during the previous unit's last K-step, so the 64 KiB stage
+// fill never starts cold after the first unit, and the epilogue's stores drain under the next
+// unit's MFMAs (the K-step wait counts them, as gemm_kernel.h's persistent loop does).
+//
+// Geometry (as gemm_p8): 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns rows
+// {h*128 + wr*64 + 0..63 : h = 0,1} and columns {h*128 + wc*32 + 0..31 : h = 0,1}.  Two LDS
+// buffers of 64 KiB (A 256 x 64, B 256 x 64).  Work units as gemm_kernel: output tile x K-split
+// (F32_ACC split-K into fp32 slabs), XCD-aware bijective remap, grouped raster.
+//   RAW: the K-step g barrier follows every wave's wait for its own DMA of K-step g (issued in
+//        K-step g-1, phases 1-2; younger than it are only the stores of an epilogue run at the
+//        end of K-step g-1: a fixed count per wave).
+//   WAR: buffer (g+1)&1 is refilled after the K-step g barrier, which every wave passes only
+//        after its K-step g-1 MFMAs consumed every fragment read from that buffer.
+// Epilogue stores are buffer stores masked by an out-of-range offset (a fixed count per wave).
+#include "gemm_table.h"
+
+namespace dfu {
+namespace {
+
+constexpr int PS_IMG = 256 * 128;   // one operand image: 256 rows x 64 k x 2 B
+constexpr int PS_BUF = 2 * PS_IMG;  // A + B
+constexpr int PS_LDS = 2 * PS_BUF;  // two buffers: 128 KiB
+
+// DMA of one operand half-tile by buffer_load ... lds (a buffer resource over the operand, 32-bit
+// per-lane byte offsets): a lane out of range carries offset kOOB and the hardware fills its 16
+// bytes with zeros -- no per-lane pointer select, no branch.  Per-lane state for the current
+// issue unit (computed once per unit; the K-step loop adds a wave-uniform k offset):
+//   K-contiguous: image row (tid>>3) + 64i (i = 0..3; half h = rows 128h.. = i in {2h, 2h+1}),
+//     this lane's 16-B chunk kc_lane_chunk(lane) of the K-step (gemm_kernel.h's KMAJOR image);
+//   MN-major: half h = 128 columns from col0 + 128h (lane chunk mn_lane_chunk(tid)), k-rows
+//     (tid>>4) + 32i (i = 0, 1) of the K-step (gemm_kernel.h's MN sub-images).
+template <bool KC>
+struct PsSrc {
+  uint32_t off[4];  // byte offset of this lane's first element (K-contiguous: row base + chunk)
+  bool ok[4];
+};
+
+template <bool KC>
+DFU_DEV void ps_src_init(PsSrc<KC>& s, int64_t ld, int mn0, int bound, int tid) {
+  if constexpr (KC) {
+    const int kc = kc_lane_chunk(tid & 63) * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = mn0 + (tid >> 3) + 64 * i;
+      s.ok[i] = row < bound;
+      s.off[i] = (uint32_t)(((int64_t)(s.ok[i] ? row : 0) * ld + kc) * 2);
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = mn0 + 128 * h + 8 * mn_lane_chunk(tid);
+      s.ok[h] = col < bound;
+      s.off[h] = (uint32_t)((s.ok[h] ? col : 0) * 2);
+    }
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+DFU_DEV void bl16(rsrc_t r, uint32_t off, char* lds_dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_dst, 16, off, 0, 0, 0);
+}
+
+// Half-tile h of K-step k0 into `img` (two wave-instructions per thread; wave = tid >> 6, kept
+// wave-uniform by the caller so the LDS destination is scalar).
+template <bool KC>
+DFU_DEV void ps_issue(const PsSrc<KC>& s, rsrc_t r, int64_t ld, int k0, int K, int h, char* img,
+                      int tid, int wave) {
+  if constexpr (KC) {
+    // (bitwise &, not &&: no short-circuit control flow around the loads)
+    const bool kin = k0 + kc_lane_chunk(tid & 63) * 8 < K;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = kin & s.ok[2 * h + i];
+      bl16(r, ok ? s.off[2 * h + i] + 2u * (uint32_t)k0 : kOOB,
+           img + h * 16384 + i * 8192 + wave * 1024);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = k0 + (tid >> 4) + 32 * i;
+      const bool ok = s.ok[h] & (k < K);
+      bl16(r, ok ? s.off[h] + (uint32_t)((int64_t)k * ld * 2) : kOOB,
+           img + 16384 * h + 8192 * i + 1024 * wave);
+    }
+  }
+}
+
+// Vector-memory instructions a wave issues in one epilogue after its last waited load.
+template <int EPI>
+DFU_DEV int ps_epi_stores(const GemmArgs& p) {
+  constexpr bool bf16_out = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_GELU ||
+                            EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD;
+  const int per = bf16_out && p.n8 ? 16 : 32 * (p.n4 ? 1 : 4);
+  return EPI == DFU_EPI_BF16_GELU ? 2 * per : per;
+}
+
+// lane holds C[m0 + (i>>2)*128 + wr*64 + (i&3)*16 + (lane&15)]
+//              [n0 + (j>>1)*128 + wc*32 + (j&1)*16 + 4*(lane>>4) + r]
+template <int EPI>
+DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc,
+                         int lane, int sidx) {
+  const bool n4 = p.n4 != 0;
+  const int M = p.M, N = p.N;
+  const rsrc_t rc = make_rsrc(p.C);
+  const rsrc_t ra = make_rsrc(p.aux);
+  const rsrc_t ro = make_rsrc(p.aux_out);
+  float bias[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
+  constexpr bool kBias = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_GELU ||
+                         EPI == DFU_EPI_F32_RESID;
+  if (kBias && p.bias) {
+    float b2[2][4];
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      load_bias<2>(p.bias, n0 + hb * 128 + wc * 32, N, lane, b2);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bias[2 * hb][r] = b2[0][r];
+        bias[2 * hb + 1][r] = b2[1][r];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + (i >> 2) * 128 + wr * 64 + (i & 3) * 16 + (lane & 15);
+    const bool okm = m < M;
+    const int64_t mc = okm ? m : 0;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      const int n0w = n0 + hb * 128 + wc * 32;
+      float v[2][4];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[jj][r] = acc[i][2 * hb + jj][r] * p.alpha + bias[2 * hb + jj][r];
+      if constexpr (EPI == DFU_EPI_BF16) {
+        st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+      } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
+        float g[2][4], d[2][4];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
+        st_row_bf16<2>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
+        st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+      } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int n = n0w + jj * 16 + 4 * (lane >> 4);
+          float x[4];
+          ld4_bf16(ra, mc * p.ldaux + n, okm, n, N, n4, x);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            v[jj][r] = EPI == DFU_EPI_BF16_DGELU ? v[jj][r] * x[r] : v[jj][r] + x[r];
+        }
+        st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+      } else if constexpr (EPI == DFU_EPI_F32_ACC) {  // split-K slab, or C += acc unsplit
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int n = n0w + jj * 16 + 4 * (lane >> 4);
+          if (p.slab != nullptr) {
+            st4_f32(make_rsrc(p.slab), ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v[jj]);
+          } else {
+            float c[4];
+            ld4_f32(rc, mc * p.ldc + n, okm, n, N, n4, c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[jj][r] += c[r];
+            st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+          }
+        }
+      } else {  // DFU_EPI_F32_RESID
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int n = n0w + jj * 16 + 4 * (lane >> 4);
+          float x[4];
+          ld4_f32(ra, mc * p.ldaux + n, okm, n, N, n4, x);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[jj][r] += x[r];
+          st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+        }
+      }
+    }
+  }
+}
+
+template <int AMODE, int BMODE, int EPI>
+__global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
+  constexpr bool AK_ = AMODE == DFU_OPND_KMAJOR;  // A K-contiguous (else MN-major: wgrad)
+  constexpr bool BK_ = BMODE == DFU_OPND_KMAJOR;  // B K-contiguous (else MN-major)
+  __shared__ __attribute__((aligned(16))) char smem[PS_LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int units = tiles * p.split;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  int wg = bid;
+  if (nwg >= 16) {  // bijective XCD-aware remap: blocks b and b+8 share an XCD
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  // rounds: in complete rounds workgroup b takes unit i*G + wg(b); in the last, partial round
+  // unit i*G + b (spread over every XCD)
+  const int full = units / nwg;
+  const int rounds = full + (bid < units - full * nwg ? 1 : 0);
+  if (rounds == 0) return;
+  auto unit_at = [&](int i) { return i * nwg + (i < full ? wg : bid); };
+  auto unit_geom = [&](int u, int& m0, int& n0, int& kb, int& nk) {
+    constexpr int GROUP_M = 4;
+    const int s = u / tiles, t = u - s * tiles;
+    const int band = GROUP_M * p.tiles_n;
+    const int g0 = (t / band) * GROUP_M;
+    const int gm = min(GROUP_M, p.tiles_m - g0);
+    const int within = t - (t / band) * band;
+    m0 = (g0 + within % gm) * 256;
+    n0 = (within / gm) * 256;
+    kb = s * p.kt_per_split;
+    nk = min(p.ktiles, kb + p.kt_per_split) - kb;
+  };
+  int total = 0;
+  for (int i = 0; i < rounds; ++i) {
+    int a_, b_, c_, nk_;
+    unit_geom(unit_at(i), a_, b_, c_, nk_);
+    total += nk_;
+  }
+  PsSrc<AK_> sa;
+  PsSrc<BK_> sb;
+  auto src_init = [&](int m0_, int n0_) {
+    ps_src_init<AK_>(sa, p.lda, m0_, AK_ ? p.M : p.m_ld_bound, tid);
+    ps_src_init<BK_>(sb, p.ldb, n0_, BK_ ? p.N : p.n_ld_bound, tid);
+  };
+  const rsrc_t ra_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), (short)0,
+                                                        p.a_bytes, 0x00020000);
+  const rsrc_t rb_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.B), (short)0,
+                                                        p.b_bytes, 0x00020000);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto issue_a = [&](int k0_, int h, char* img) {
+    ps_issue<AK_>(sa, ra_, p.lda, k0_, p.K, h, img, tid, wave_u);
+  };
+  auto issue_b = [&](int k0_, int h, char* img) {
+    ps_issue<BK_>(sb, rb_, p.ldb, k0_, p.K, h, img, tid, wave_u);
+  };
+
+  // issue cursor (the K-step whose DMA goes out next) and compute cursor
+  int iu = 0, ik = 0, im0, in0, ikb, ink;
+  unit_geom(unit_at(0), im0, in0, ikb, ink);
+  src_init(im0, in0);
+  int ci = 0, ck = 0, cm0, cn0, ckb, cnk;
+  int cu = unit_at(0);
+  unit_geom(cu, cm0, cn0, ckb, cnk);
+  auto advance_issue = [&]() {
+    if (++ik == ink) {
+      ik = 0;
+      if (++iu < rounds) {
+        unit_geom(unit_at(iu), im0, in0, ikb, ink);
+        src_init(im0, in0);
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-step 0 into buffer 0, in first-use order (A-top, B-left, B-right, A-bottom)
+  {
+    const int k0 = (ikb + ik) * BK;
+    issue_a(k0, 0, smem);
+    issue_b(k0, 0, smem + PS_IMG);
+    issue_b(k0, 1, smem + PS_IMG);
+    issue_a(k0, 1, smem);
+    advance_issue();
+  }
+  const int E = ps_epi_stores<EPI>(p);
+  bool epi_last = false;  // an epilogue ran at the end of the previous K-step
+  for (int g = 0; g < total; ++g) {
+    const char* la = smem + (g & 1) * PS_BUF;
+    const char* lb = la + PS_IMG;
+    char* na = smem + ((g & 1) ^ 1) * PS_BUF;
+    char* nb = na + PS_IMG;
+    const bool nxt = g + 1 < total;
+    const int k1 = (ikb + ik) * BK;  // the next K-step (issue cursor)
+    // Fragment registers hold one A half (fa) and one B half (fb); each phase's MFMAs run one
+    // k-half (ks) at a time, and the reads the NEXT group needs go out as soon as the group
+    // before it has consumed the registers they overwrite, so every read has a group of 8
+    // MFMAs (this wave's and its SIMD partner's) to land under instead of stalling the pipe
+    // (the compiler's lgkmcnt waits are the exact ones: each read's consumer is known).
+    bf16x8 fa[4][2], fb[2][2];
+    auto rd_a = [&](int h, int ks) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i][ks] = read_frag<AK_>(la, h * 128 + wr * 64 + i * 16, ks, lane);
+    };
+    auto rd_b = [&](int h, int ks) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
+    };
+    auto mf = [&](int ha, int hb, int ks) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              fb[j][ks], fa[i][ks], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // this K-step's DMA landed (younger: only the previous epilogue's stores), then published
+    if (epi_last)
+      wait_vm_le<63>(E);
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    rd_a(0, 0);
+    rd_b(0, 0);
+    rd_a(0, 1);
+    rd_b(0, 1);
+    if (nxt) {
+      issue_a(k1, 0, na);
+      issue_b(k1, 0, nb);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mf(0, 0, 0);   // A-top x B-left
+    rd_b(1, 0);
+    mf(0, 0, 1);
+    rd_b(1, 1);
+    if (nxt) {
+      issue_b(k1, 1, nb);
+      issue_a(k1, 1, na);
+      advance_issue();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mf(0, 1, 0);   // A-top x B-right
+    rd_a(1, 0);
+    mf(0, 1, 1);
+    rd_a(1, 1);
+    mf(1, 1, 0);   // A-bottom x B-right
+    rd_b(0, 0);
+    mf(1, 1, 1);
+    rd_b(0, 1);
+    mf(1, 0, 0);   // A-bottom x B-left
+    mf(1, 0, 1);
+    epi_last = false;
+    if (++ck == cnk) {
+      ps_epilogue<EPI>(p, acc, cm0, cn0, wr, wc, lane, cu / tiles);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      epi_last = true;
+      ck = 0;
+      if (++ci < rounds) {
+        cu = unit_at(ci);
+        unit_geom(cu, cm0, cn0, ckb, cnk);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+#define PS(A, B, E) {A, B, E, T256x256ps, &gemm_ps<A, B, E>, PS_LDS, 512}
+const Entry kTable256x256ps[] = {
+    PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
+    PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_GELU),
+    PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_RESID),
+    PS(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16),
+    PS(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_DGELU),
+    PS(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_ADD),
+    PS(DFU_OPND_MNMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_F32_ACC),  // weight gradients (split-K slabs)
+};
+#undef PS
+const int kTable256x256psN = sizeof(kTable256x256ps) / sizeof(Entry);
+
+}  // namespace dfu

@@ -56,7 +56,7 @@ static void check_plan(const dfu_gemm_desc& d, const char* what) {
   const int rc = dfu_gemm_plan(&d, &tile, &split);
   EXPECT(rc == DFU_OK, "%s: plan rc %d (%s)", what, rc, dfu_last_error_string());
   if (rc != DFU_OK) return;
-  EXPECT(tile >= 1 && tile <= 7, "%s: tile %d", what, tile);
+  EXPECT(tile >= 1 && tile <= 13, "%s: tile %d", what, tile);
   EXPECT(split >= 1 && split <= 256, "%s: split %d", what, split);
   EXPECT(split == 1 || d.epilogue == DFU_EPI_F32_ACC, "%s: split %d on a non-ACC epilogue", what,
          split);
@@ -170,7 +170,7 @@ static void gemm_rejects() {
   d = ok; d.lda = 260; d.K = 256; d.lda = 257; bad.push_back({"lda%8", d});
   d = ok; d.split_k = -1; bad.push_back({"split<0", d});
   d = ok; d.split_k = 4; bad.push_back({"split on BF16", d});
-  d = ok; d.tile = 9; bad.push_back({"tile 9", d});
+  d = ok; d.tile = 99; bad.push_back({"tile 99", d});
   d = ok; d.epilogue = DFU_EPI_BF16_STATS; bad.push_back({"stats slab", d});
   d = ok; d.a_mode = DFU_OPND_MNMAJOR; d.lda = 8; bad.push_back({"lda < M", d});
   d = ok; d.a_mode = DFU_OPND_CONV_FWD; bad.push_back({"conv geometry", d});

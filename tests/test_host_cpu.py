@@ -55,7 +55,7 @@ def _desc(**kw):
 @pytest.mark.parametrize("kw,msg", [
     (dict(M=0), "bad shape"),
     (dict(K=100), "multiple of 8"),
-    (dict(tile=9), "bad tile"),
+    (dict(tile=99), "bad tile"),
     (dict(split_k=4), "needs the F32_ACC"),
     (dict(lda=100), "lda"),
     (dict(epilogue=L.EPI_BF16_STATS), "stats slab"),

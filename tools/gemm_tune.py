@@ -70,9 +70,14 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "dfu-multimodal_amd", "csrc",
                                                   "gemm_tuned.inc"))
     ap.add_argument("--append", action="store_true", help="keep entries already in --out")
+    ap.add_argument("--tiles", default="1-12", help="tile ids to try, e.g. 1-12 or 6,11")
     ap.add_argument("--dump", default=None,
                     help="also write every timing (shape -> {tile/split: us}) to this JSON")
     a = ap.parse_args()
+    tiles = []
+    for part in a.tiles.split(","):
+        lo, _, hi = part.partition("-")
+        tiles += list(range(int(lo), int(hi or lo) + 1))
     dev = torch.device("cuda", 0)
     torch.manual_seed(42)
     from dfu_hip import nn as hnn
@@ -103,7 +108,7 @@ def main():
         best = (t_auto, 0, 0)
         ktiles = (d0.K + 63) // 64
         splits = [s for s in SPLITS if s <= ktiles] if d0.epilogue == L.EPI_F32_ACC else [1]
-        for tile in range(1, 8):
+        for tile in tiles:
             for sk in splits:
                 d = copy_desc(d0)
                 d.tile, d.split_k = tile, sk
@@ -140,7 +145,7 @@ def main():
     with open(a.out, "w") as f:
         f.write("// Generated by tools/gemm_tune.py on MI355X (gfx950): fastest tile/split-K per GEMM of\n"
                 "// the DFU training step. Fields: a_mode, b_mode, epilogue, M, N, K, conv n,h,w,c,k,r,s,"
-                "stride,pad,\n// tile (1..5), split.\n")
+                "stride,pad,\n// tile (1..12), split.\n")
         for ln in keep + lines:
             f.write(ln + "\n")
     print(f"wrote {len(keep) + len(lines)} entries to {a.out}")
