@@ -13,13 +13,12 @@ using namespace dfu;
 namespace {
 
 constexpr int kCUs = 256;
-constexpr int kTM[NTILES] = {128, 256, 128, 256, 128, 128, 256, 128, 256, 128, 128, 128, 256};
-constexpr int kTN[NTILES] = {128, 128, 256, 256, 128, 128, 256, 128, 128, 256, 128, 128, 256};
-constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 2, 2, 1};  // workgroups per CU
-// the tile a pipelined twin shares its geometry (and fitted step time) with
-constexpr int kBase[NTILES] = {0, 1, 2, 3, 4, 5, 6, 0, 1, 2, 4, 5, 6};
-constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false,
-                                  true, false, false, true, false, false};  // kTail
+constexpr int kTM[NTILES] = {128, 256, 128, 256, 128, 128, 256, 256};
+constexpr int kTN[NTILES] = {128, 128, 256, 256, 128, 128, 256, 256};
+constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 2, 1, 1};  // workgroups per CU
+// the tile whose fitted step time a variant borrows (the persistent phased 256x256: the phased)
+constexpr int kBase[NTILES] = {0, 1, 2, 3, 4, 5, 6, 6};
+constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false, false};
 // Wave-quantisation cost model: a launch takes ceil(tiles * splits / 256) rounds (one 512-thread
 // workgroup per CU), each costing kRoundUs (prologue fill + epilogue) + k-steps * kStepUs.
 // Fitted on MI355X to tools/gemm_bench.py --sweep (ViT qkv K=768 vs fc2 K=3072 forward rows,
@@ -27,18 +26,14 @@ constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false,
 // 256x256 moves 1.62x more MFMA work per microsecond than 128x128.
 // The 2-per-CU 128x128 variant: two co-resident workgroups share the MFMA pipe (step cost per
 // workgroup ~doubles) but hide each other's fill and epilogue.
-// (the phased 256x256 and the pipelined twins are priced high: only the offline-tuned table
-// selects them)
-constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70, 0.65, 3.0,
-                                    3.0, 3.0, 3.0, 3.0, 3.0, 3.0};
-constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1, 6.1, 20.0,
-                                     20.0, 20.0, 20.0, 20.0, 20.0, 20.0};
+// (the phased 256x256 kernels are priced high: only the offline-tuned table selects them)
+constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70, 0.65, 3.0, 3.0};
+constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1, 6.1, 20.0, 20.0};
 constexpr double kSlabGBs = 5000.0;  // split-K: slab write + reduce (read slabs, RMW C)
 constexpr double kReduceLaunchUs = 2.0;
 // Persistent schedule (gemm_kernel.h): a workgroup owning several work units pays one
 // prologue fill for all of them plus, per unit, the epilogue time its MFMAs do not hide.
-constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0, 3.0, 3.0, 3.0, 3.0, 3.0,
-                                    3.0};
+constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0, 3.0};
 int g_persistent = 1;       // dfu_gemm_set_persistent
 int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
@@ -48,12 +43,10 @@ int g_tail_split = 1;       // dfu_gemm_set_tail_split
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
                                kTable128x128o2, kTable128x128w4, kTable256x256p8,
-                               kTable128x128pp, kTable256x128pp, kTable128x256pp,
-                               kTable128x128o2pp, kTable128x128w4pp, kTable256x256ps};
+                               kTable256x256ps};
   const int ns[NTILES] = {kTable128x128N, kTable256x128N, kTable128x256N, kTable256x256N,
                           kTable128x128o2N, kTable128x128w4N, kTable256x256p8N,
-                          kTable128x128ppN, kTable256x128ppN, kTable128x256ppN,
-                          kTable128x128o2ppN, kTable128x128w4ppN, kTable256x256psN};
+                          kTable256x256psN};
   for (int i = 0; i < ns[tile]; ++i) {
     const Entry& en = tabs[tile][i];
     if (en.a == a && en.b == b && en.e == e) return &en;

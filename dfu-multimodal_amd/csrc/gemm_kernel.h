@@ -998,11 +998,7 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
 }
 
 // ------------------------------------------------------------------------------ kernel
-// PIPE = 1: software-pipelined K-loop (see the PIPE branch at the end of the kernel): the
-// fragment reads of K-step g+1's first k-half are issued under K-step g's second-half MFMAs,
-// with the one barrier per K-step placed mid-step (after the first-half MFMAs).
-template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0, int NW = 8,
-          int PIPE = 0>
+template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0, int NW = 8>
 __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   using T = Tile<TM, TN, OCC, NST, NW>;
   constexpr int WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
@@ -1155,82 +1151,6 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   unsigned hist = 0;
   int ci = 0, cu = unit_at(0), ck = 0, cm0, cn0, ckb, cnk;
   unit_geom(cu, cm0, cn0, ckb, cnk);
-  // end of a work unit: epilogue (or tail hand-off), reset the accumulators, next unit
-  auto unit_done = [&]() {
-    bool epi = true;
-    if constexpr (kTail)
-      if (p.tail_r && cu >= p.tail_full) epi = tail_reduce<T>(p, acc, cu - p.tail_full, red, tid);
-    if (epi && !(p.dbg & 1)) epilogue<AMODE, EPI, T>(p, acc, cm0, cn0, cu / tiles, red, tid, pre);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    hist |= 1u;
-    ck = 0;
-    if (++ci < rounds) {
-      cu = unit_at(ci);
-      unit_geom(cu, cm0, cn0, ckb, cnk);
-    }
-  };
-
-  if constexpr (PIPE) {
-    // Software-pipelined stream.  Iteration g: issue the reads of K-step g's k-half 1 (F1);
-    // MFMAs on k-half 0 (F0, read one iteration earlier); wait for K-step g+1's DMA, retire F1's
-    // reads and pass the barrier (publishes g+1; every wave is done reading slot g); refill slot g
-    // with K-step g+NSTAGE; read K-step g+1's k-half 0 into F0; MFMAs on F1.  The DMA of K-step
-    // g+1 went out NSTAGE-1 iterations earlier, each iteration's MFMAs cover the next
-    // iteration's first fragment reads, and the barrier sits between two MFMA halves.
-    bf16x8 f0a[FM], f0b[FN], f1a[FM], f1b[FN];
-    auto read_half = [&](const char* la, int ks, bf16x8 (&fa)[FM], bf16x8 (&fb)[FN]) {
-      const char* lb = la + T::A_BYTES;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = read_frag<AK>(la, wr * WTM + i * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
-    };
-    auto mfma_half = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
-      if (p.dbg & 2) return;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-    };
-#pragma unroll
-    for (int s = 0; s < NSTAGE; ++s)
-      if (s < total) issue_next(smem + s * T::STAGE_BYTES);
-    wait_vm_le<63>(T::DMA_PER_STAGE * min(NSTAGE - 1, total - 1));
-    __builtin_amdgcn_s_barrier();
-    read_half(smem, 0, f0a, f0b);
-    int slot = 0;
-    for (int g = 0; g < total; ++g) {
-      char* cur = smem + slot * T::STAGE_BYTES;
-      const int nslot = slot == NSTAGE - 1 ? 0 : slot + 1;
-      read_half(cur, 1, f1a, f1b);
-      if constexpr (aux_prefetch<EPI, T>())
-        if (ck + 1 == cnk) aux_load<AMODE, EPI, T>(p, cm0, cn0, tid, pre);
-      mfma_half(f0a, f0b);
-      if (g + 1 < total) {
-        // K-step g+1 landed: younger are the DMA of min(NSTAGE-2, total-g-2) later K-steps and
-        // the stores of every epilogue run since K-step g+1 was issued (NSTAGE-1 iterations)
-        const int later = min(NSTAGE - 2, total - g - 2);
-        const unsigned win = hist & ((1u << (NSTAGE - 1)) - 1u);
-        if (win == 0 && later == NSTAGE - 2)
-          wait_vmcnt<T::DMA_PER_STAGE * (NSTAGE - 2)>();
-        else
-          wait_vm_le<63>(T::DMA_PER_STAGE * later + E * __builtin_popcount(win));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (g + NSTAGE < total) issue_next(cur);
-        read_half(smem + nslot * T::STAGE_BYTES, 0, f0a, f0b);
-      }
-      mfma_half(f1a, f1b);
-      slot = nslot;
-      hist <<= 1;
-      if (++ck == cnk) unit_done();
-    }
-    return;
-  }
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
     if (s < total) issue_next(smem + s * T::STAGE_BYTES);

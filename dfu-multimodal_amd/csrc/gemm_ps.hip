@@ -1,4 +1,4 @@
-// Persistent phased 256x256 GEMM (tile 13): the K-step body of gemm_p8.hip (four 16-MFMA
+// Persistent phased 256x256 GEMM (tile 8): the K-step body of gemm_p8.hip (four 16-MFMA
 // quadrant phases, the next K-step's half-tile DMA issued in phases 1-2, one barrier per K-step)
 // run over ONE continuous stream of K-steps per workgroup, across its work units: the DMA of a
 // unit's first K-step is issued during the previous unit's last K-step, so the 64 KiB stage
@@ -19,6 +19,22 @@
 
 namespace dfu {
 namespace {
+
+// Timing ablations (tools/build_ablate.sh builds a separate library with -DDFU_PS_ABLATE=mask;
+// the product build is 0): 1 no epilogue, 2 no MFMA, 4 no DMA, 8 no fragment reads (zero
+// fragments), 16 no K-step barrier.  Results are wrong in every ablated build.
+#ifndef DFU_PS_ABLATE
+#define DFU_PS_ABLATE 0
+#endif
+constexpr int kAbl = DFU_PS_ABLATE;
+// Schedule experiments (same mechanism): bit 0 = the two wave rows issue their whole DMA share at
+// different points (wr 0 before the first MFMA group, wr 1 after the second), bit 1 =
+// s_setprio(1) around every MFMA group, bit 2 = both B halves kept in registers, bit 3 = the
+// partial last round of units in contiguous runs per XCD.
+#ifndef DFU_PS_SCHED
+#define DFU_PS_SCHED 0
+#endif
+constexpr int kSched = DFU_PS_SCHED;
 
 constexpr int PS_IMG = 256 * 128;   // one operand image: 256 rows x 64 k x 2 B
 constexpr int PS_BUF = 2 * PS_IMG;  // A + B
@@ -207,9 +223,21 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   // rounds: in complete rounds workgroup b takes unit i*G + wg(b); in the last, partial round
   // unit i*G + b (spread over every XCD)
   const int full = units / nwg;
-  const int rounds = full + (bid < units - full * nwg ? 1 : 0);
+  int rounds = full + (bid < units - full * nwg ? 1 : 0);
+  int tail_slot = bid;  // this workgroup's unit in the last, partial round (if any)
+  if constexpr ((kSched & 8) != 0) {
+    // the R units of the partial round in 8 contiguous runs, run x on XCD x (blocks b = x mod
+    // 8): neighbouring tiles of the grouped raster share their A / B panels in one L2
+    const int R = units - full * nwg;
+    if (nwg >= 16 && R > 0) {
+      const int x = bid & 7, j = bid >> 3;
+      const int r0 = (x * R) >> 3, r1 = ((x + 1) * R) >> 3;
+      rounds = full + (j < r1 - r0 ? 1 : 0);
+      tail_slot = r0 + j;
+    }
+  }
   if (rounds == 0) return;
-  auto unit_at = [&](int i) { return i * nwg + (i < full ? wg : bid); };
+  auto unit_at = [&](int i) { return i * nwg + (i < full ? wg : tail_slot); };
   auto unit_geom = [&](int u, int& m0, int& n0, int& kb, int& nk) {
     constexpr int GROUP_M = 4;
     const int s = u / tiles, t = u - s * tiles;
@@ -240,10 +268,10 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
                                                         p.b_bytes, 0x00020000);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto issue_a = [&](int k0_, int h, char* img) {
-    ps_issue<AK_>(sa, ra_, p.lda, k0_, p.K, h, img, tid, wave_u);
+    if constexpr (!(kAbl & 4)) ps_issue<AK_>(sa, ra_, p.lda, k0_, p.K, h, img, tid, wave_u);
   };
   auto issue_b = [&](int k0_, int h, char* img) {
-    ps_issue<BK_>(sb, rb_, p.ldb, k0_, p.K, h, img, tid, wave_u);
+    if constexpr (!(kAbl & 4)) ps_issue<BK_>(sb, rb_, p.ldb, k0_, p.K, h, img, tid, wave_u);
   };
 
   // issue cursor (the K-step whose DMA goes out next) and compute cursor
@@ -278,7 +306,7 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     issue_a(k0, 1, smem);
     advance_issue();
   }
-  const int E = ps_epi_stores<EPI>(p);
+  const int E = (kAbl & 1) ? 0 : ps_epi_stores<EPI>(p);
   bool epi_last = false;  // an epilogue ran at the end of the previous K-step
   for (int g = 0; g < total; ++g) {
     const char* la = smem + (g & 1) * PS_BUF;
@@ -292,35 +320,61 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     // before it has consumed the registers they overwrite, so every read has a group of 8
     // MFMAs (this wave's and its SIMD partner's) to land under instead of stalling the pipe
     // (the compiler's lgkmcnt waits are the exact ones: each read's consumer is known).
-    bf16x8 fa[4][2], fb[2][2];
+    // kSched bit 2: both B halves stay in registers (fbh[hb]), so phase 4 does not re-read B-left
+    constexpr bool kB2 = (kSched & 4) != 0;
+    bf16x8 fa[4][2], fbh[2][2][2];
+    if constexpr ((kAbl & 8) != 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i][0] = fa[i][1] = (bf16x8){};
+      fbh[0][0][0] = fbh[0][0][1] = fbh[0][1][0] = fbh[0][1][1] = (bf16x8){};
+      fbh[1][0][0] = fbh[1][0][1] = fbh[1][1][0] = fbh[1][1][1] = (bf16x8){};
+    }
     auto rd_a = [&](int h, int ks) {
+      if constexpr ((kAbl & 8) != 0) return;
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i][ks] = read_frag<AK_>(la, h * 128 + wr * 64 + i * 16, ks, lane);
     };
     auto rd_b = [&](int h, int ks) {
+      if constexpr ((kAbl & 8) != 0) return;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
+      for (int j = 0; j < 2; ++j)
+        fbh[kB2 ? h : 0][j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
     };
     auto mf = [&](int ha, int hb, int ks) {
+      if constexpr ((kAbl & 2) != 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        return;
+      }
+      if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              fb[j][ks], fa[i][ks], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+              fbh[kB2 ? hb : 0][j][ks], fa[i][ks], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+      if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
+    const bool row0 = __builtin_amdgcn_readfirstlane(wr) == 0;
     // this K-step's DMA landed (younger: only the previous epilogue's stores), then published
     if (epi_last)
       wait_vm_le<63>(E);
     else
       wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!(kAbl & 16)) __builtin_amdgcn_s_barrier();
     rd_a(0, 0);
     rd_b(0, 0);
     rd_a(0, 1);
     rd_b(0, 1);
-    if (nxt) {
+    if constexpr (kSched & 1) {
+      if (nxt && row0) {
+        issue_a(k1, 0, na);
+        issue_b(k1, 0, nb);
+        issue_b(k1, 1, nb);
+        issue_a(k1, 1, na);
+        advance_issue();
+      }
+    } else if (nxt) {
       issue_a(k1, 0, na);
       issue_b(k1, 0, nb);
     }
@@ -329,7 +383,15 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     rd_b(1, 0);
     mf(0, 0, 1);
     rd_b(1, 1);
-    if (nxt) {
+    if constexpr (kSched & 1) {
+      if (nxt && !row0) {
+        issue_a(k1, 0, na);
+        issue_b(k1, 0, nb);
+        issue_b(k1, 1, nb);
+        issue_a(k1, 1, na);
+        advance_issue();
+      }
+    } else if (nxt) {
       issue_b(k1, 1, nb);
       issue_a(k1, 1, na);
       advance_issue();
@@ -340,14 +402,21 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     mf(0, 1, 1);
     rd_a(1, 1);
     mf(1, 1, 0);   // A-bottom x B-right
-    rd_b(0, 0);
+    if constexpr (!kB2) rd_b(0, 0);
     mf(1, 1, 1);
-    rd_b(0, 1);
+    if constexpr (!kB2) rd_b(0, 1);
     mf(1, 0, 0);   // A-bottom x B-left
     mf(1, 0, 1);
     epi_last = false;
     if (++ck == cnk) {
-      ps_epilogue<EPI>(p, acc, cm0, cn0, wr, wc, lane, cu / tiles);
+      if constexpr (!(kAbl & 1)) {
+        ps_epilogue<EPI>(p, acc, cm0, cn0, wr, wc, lane, cu / tiles);
+      } else {  // keep the accumulators (and so every MFMA) alive without storing them
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll

@@ -13,10 +13,8 @@ struct Entry {
 enum TileId {
   T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, T128x128o2 = 4, T128x128w4 = 5,
   T256x256p8 = 6,  // phased 256x256 (gemm_p8.hip): K-contiguous A and B only
-  // software-pipelined K-loop (gemm_kernel PIPE = 1) twins of tiles 0, 1, 2, 4, 5
-  T128x128pp = 7, T256x128pp = 8, T128x256pp = 9, T128x128o2pp = 10, T128x128w4pp = 11,
-  T256x256ps = 12,  // persistent phased 256x256 (gemm_ps.hip)
-  NTILES = 13
+  T256x256ps = 7,  // persistent phased 256x256 (gemm_ps.hip)
+  NTILES = 8
 };
 extern const Entry kTable128x128[];
 extern const int kTable128x128N;
@@ -32,16 +30,6 @@ extern const Entry kTable128x128w4[];
 extern const int kTable128x128w4N;
 extern const Entry kTable256x256p8[];
 extern const int kTable256x256p8N;
-extern const Entry kTable128x128pp[];
-extern const int kTable128x128ppN;
-extern const Entry kTable256x128pp[];
-extern const int kTable256x128ppN;
-extern const Entry kTable128x256pp[];
-extern const int kTable128x256ppN;
-extern const Entry kTable128x128o2pp[];
-extern const int kTable128x128o2ppN;
-extern const Entry kTable128x128w4pp[];
-extern const int kTable128x128w4ppN;
 extern const Entry kTable256x256ps[];
 extern const int kTable256x256psN;
 }  // namespace dfu
@@ -66,10 +54,4 @@ extern const int kTable256x256psN;
   {                                                                             \
     A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv, OCCv, 0, 4>,             \
         dfu::Tile<TMv, TNv, OCCv, 0, 4>::LDS_BYTES, dfu::Tile<TMv, TNv, OCCv, 0, 4>::NT \
-  }
-// software-pipelined K-loop (PIPE = 1), NWv waves, OCCv workgroups per CU
-#define DFU_ENTRY_PIPE(A, B, E, TMv, TNv, OCCv, NWv, TID)                             \
-  {                                                                                   \
-    A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv, OCCv, 0, NWv, 1>,              \
-        dfu::Tile<TMv, TNv, OCCv, 0, NWv>::LDS_BYTES, dfu::Tile<TMv, TNv, OCCv, 0, NWv>::NT \
   }

@@ -99,8 +99,8 @@ typedef struct dfu_gemm_desc {
   int32_t conv_p, conv_q;                 /* output H,W                            */
   int32_t tile;        /* 0 = auto; 1..7 = 128x128, 256x128, 128x256, 256x256,
                           128x128 at 2 workgroups/CU (8 waves, 4 waves), phased
-                          256x256 (K-contiguous A and B only); 8..12 = tiles 1, 2,
-                          3, 5, 6 with the software-pipelined K-loop            */
+                          256x256 (K-contiguous A and B only); 8 = persistent
+                          phased 256x256 (K-contiguous or MN-major A and B)     */
   void* workspace;     /* split-K fp32 slabs (dfu_gemm_workspace_bytes); NULL =  */
   int64_t workspace_bytes; /*   split-K partials accumulate with fp32 atomics     */
   /* Split-K with slabs: NULL = a second kernel adds the slabs into C.  Otherwise a zeroed

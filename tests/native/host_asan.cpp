@@ -56,7 +56,7 @@ static void check_plan(const dfu_gemm_desc& d, const char* what) {
   const int rc = dfu_gemm_plan(&d, &tile, &split);
   EXPECT(rc == DFU_OK, "%s: plan rc %d (%s)", what, rc, dfu_last_error_string());
   if (rc != DFU_OK) return;
-  EXPECT(tile >= 1 && tile <= 13, "%s: tile %d", what, tile);
+  EXPECT(tile >= 1 && tile <= 8, "%s: tile %d", what, tile);
   EXPECT(split >= 1 && split <= 256, "%s: split %d", what, split);
   EXPECT(split == 1 || d.epilogue == DFU_EPI_F32_ACC, "%s: split %d on a non-ACC epilogue", what,
          split);

@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "dfu-multimodal_amd", "csrc",
                                                   "gemm_tuned.inc"))
     ap.add_argument("--append", action="store_true", help="keep entries already in --out")
-    ap.add_argument("--tiles", default="1-12", help="tile ids to try, e.g. 1-12 or 6,11")
+    ap.add_argument("--tiles", default="1-8", help="tile ids to try, e.g. 1-8 or 6,8")
     ap.add_argument("--dump", default=None,
                     help="also write every timing (shape -> {tile/split: us}) to this JSON")
     a = ap.parse_args()

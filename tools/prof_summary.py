@@ -17,7 +17,7 @@ import json
 import re
 
 CATS = [
-    ("GEMM (MFMA template)", r"gemm_kernel<|gemm_p8<"),
+    ("GEMM (MFMA template)", r"gemm_kernel<|gemm_p8<|gemm_ps<"),
     ("GEMM split-K reduce", r"k_splitk_reduce"),
     ("fp32 head GEMM", r"k_gemm_f32"),
     ("BatchNorm", r"k_bn_"),
@@ -33,14 +33,15 @@ CATS = [
 
 
 def is_gemm(name):
-    """The MFMA GEMM template's kernels: gemm_kernel<...> and the phased gemm_p8<...>."""
-    return "gemm_kernel<" in name or "gemm_p8<" in name
+    """The MFMA GEMM template's kernels: gemm_kernel<...>, the phased gemm_p8<...> and the
+    persistent phased gemm_ps<...>."""
+    return "gemm_kernel<" in name or "gemm_p8<" in name or "gemm_ps<" in name
 
 
 def short(name):
     n = name.replace("void dfu::", "").replace("(dfu::GemmArgs)", "")
     n = re.sub(r"\(anonymous namespace\)::", "", n)
-    n = re.sub(r"\(.*", "", n) if "gemm_kernel" not in n else n
+    n = re.sub(r"\(.*", "", n) if "gemm_kernel" not in n and "gemm_p" not in n else n
     return n.strip()[:70]
 
 
@@ -53,13 +54,15 @@ def cat(name):
 
 OPND = ["KM", "MN", "CONV_FWD", "CONV_DGRAD", "CONV_DGRAD_W", "CONV_WGRAD_X"]
 EPI = ["BF16", "BF16_RELU", "BF16_GELU", "F32", "F32_RESID", "BF16_DGELU", "BF16_ADD", "F32_ACC",
-       "F32_ACC_CONVW", "BF16_STATS", "PATCH"]
+       "F32_ACC_CONVW", "BF16_STATS", "PATCH", "F32_STATS", "BF16_DSTATS"]
 
 
 def gemm_label(name):
-    m8 = re.search(r"gemm_p8<(\d+), (\d+)>", name)
+    m8 = re.search(r"gemm_p(8|s)<(\d+), (\d+), (\d+)>", name)
     if m8:
-        return f"gemm KM x {OPND[int(m8.group(1))]} -> {EPI[int(m8.group(2))]} 256x256 phased"
+        kind = "phased" if m8.group(1) == "8" else "persistent phased"
+        return (f"gemm {OPND[int(m8.group(2))]} x {OPND[int(m8.group(3))]} -> "
+                f"{EPI[int(m8.group(4))]} 256x256 {kind}")
     m = re.search(r"gemm_kernel<(\d+), (\d+), (\d+), (\d+), (\d+)(?:, (\d+))?(?:, \d+)?>", name)
     if not m:
         return short(name)
