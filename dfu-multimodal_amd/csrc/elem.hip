@@ -620,6 +620,58 @@ extern "C" int dfu_conv_grad_krsc_to_oihw(const float* krsc, float* oihw, int32_
   return DFU_OK;
 }
 
+// Batched bf16 transpose (include/dfu_hip.h dfu_transpose_bf16): one 256-thread workgroup per
+// 64x64 tile; the tile goes through LDS as 16-B row chunks and leaves as 16-B column chunks
+// (row stride 65 dwords of bf16 pairs: the column reads of a 16-lane group hit distinct banks).
+__global__ __launch_bounds__(256) void k_transpose_bf16(const dfu_transpose_job* __restrict__ jobs,
+                                                        int njobs) {
+  __shared__ uint16_t t[64][66];
+  const int tile = blockIdx.x;
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].tile0 <= tile) ++j;
+  const dfu_transpose_job jb = jobs[j];
+  const int tn = (jb.cols + 63) / 64;
+  const int lt = tile - jb.tile0;
+  const int r0 = (lt / tn) * 64, c0 = (lt % tn) * 64;
+  const uint16_t* src = (const uint16_t*)jb.src;
+  uint16_t* dst = (uint16_t*)jb.dst;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // 64 rows x 8 chunks of 8 columns
+    const int q = threadIdx.x + 256 * h;
+    const int r = q >> 3, cc = (q & 7) * 8;
+    if (r0 + r < jb.rows && c0 + cc < jb.cols) {
+      const u32x4 v = *(const u32x4*)(src + (int64_t)(r0 + r) * jb.cols + c0 + cc);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        t[r][cc + 2 * e] = (uint16_t)(v[e] & 0xffffu);
+        t[r][cc + 2 * e + 1] = (uint16_t)(v[e] >> 16);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // 64 dst rows (src columns) x 8 chunks of 8 src rows
+    const int q = threadIdx.x + 256 * h;
+    const int c = q >> 3, rr = (q & 7) * 8;
+    if (c0 + c < jb.cols && r0 + rr < jb.rows) {
+      u32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = (uint32_t)t[rr + 2 * e][c] | ((uint32_t)t[rr + 2 * e + 1][c] << 16);
+      *(u32x4*)(dst + (int64_t)(c0 + c) * jb.rows + r0 + rr) = v;
+    }
+  }
+}
+
+extern "C" int dfu_transpose_bf16(const dfu_transpose_job* jobs, int32_t njobs, int32_t ntiles,
+                                  void* stream) {
+  DFU_CHECK_ARG(jobs && njobs > 0 && ntiles > 0, "dfu_transpose_bf16: bad args");
+  hipLaunchKernelGGL(k_transpose_bf16, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, jobs,
+                     njobs);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
 extern "C" int dfu_cast_rows_bf16(const float* in, int64_t ld_in, void* out, int64_t ld_out,
                                   int32_t rows, int32_t cols, void* stream) {
   DFU_CHECK_ARG(in && out && rows > 0 && cols > 0 && ld_out >= cols && ld_in >= cols,

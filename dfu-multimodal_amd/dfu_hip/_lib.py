@@ -85,6 +85,7 @@ PROTOTYPES = {
     "dfu_pack_conv_weight": [P, P, I32, I32, I32, I32, P],
     "dfu_conv_grad_krsc_to_oihw": [P, P, I32, I32, I32, I32, P],
     "dfu_cast_rows_bf16": [P, I64, P, I64, I32, I32, P],
+    "dfu_transpose_bf16": [P, I32, I32, P],
     "dfu_cast_rows_f32": [P, I64, P, I64, I32, I32, P],
     "dfu_im2col_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],
     "dfu_patchify_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],

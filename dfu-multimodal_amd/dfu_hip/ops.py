@@ -227,6 +227,40 @@ def cast_rows_bf16(x, ld_out=None, out=None):
     return out
 
 
+class TransposeJobs:
+    """A device table of bf16 transposes (dfu_transpose_bf16: dst[c][r] = src[r][c]) built once
+    and launched as ONE kernel each time (the transposed weight shadows, optim.FlatParams)."""
+
+    def __init__(self, pairs):
+        import struct
+        raw, tile0 = bytearray(), 0
+        for src, dst in pairs:
+            _req(src, BF16, "transpose_bf16")
+            _req(dst, BF16, "transpose_bf16")
+            r, c = src.shape
+            if dst.shape != (c, r) or r % 8 or c % 8 or not (src.is_contiguous() and
+                                                            dst.is_contiguous()):
+                raise ValueError(f"transpose_bf16: [{r}, {c}] -> {tuple(dst.shape)} unsupported")
+            raw += struct.pack("<QQiiii", src.data_ptr(), dst.data_ptr(), r, c, tile0, 0)
+            tile0 += ((r + 63) // 64) * ((c + 63) // 64)
+        self.pairs = list(pairs)  # keep the buffers alive as long as the table
+        self.njobs, self.ntiles = len(self.pairs), tile0
+        dev = self.pairs[0][0].device
+        self.table = torch.frombuffer(bytes(raw), dtype=torch.uint8).to(dev)
+
+    def launch(self):
+        check(lib().dfu_transpose_bf16(ptr(self.table), self.njobs, self.ntiles, stream_ptr()),
+              "dfu_transpose_bf16")
+
+
+def transpose_bf16(src, out=None):
+    """bf16 [rows, cols] -> bf16 [cols, rows] (one launch)."""
+    if out is None:
+        out = torch.empty((src.shape[1], src.shape[0]), dtype=BF16, device=src.device)
+    TransposeJobs([(src, out)]).launch()
+    return out
+
+
 def cast_rows_f32(x, out=None):
     _req(x, BF16, "cast_rows_f32")
     x2 = x.reshape(-1, x.shape[-1])

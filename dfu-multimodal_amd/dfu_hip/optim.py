@@ -10,7 +10,10 @@ view) and ``p.grad`` into a matching flat gradient buffer, so:
     contiguous slices are what data-parallel all-reduce buckets send (dfu_hip.parallel);
   * the step counter lives on the device, so the whole step can be captured in a HIP graph;
   * the same kernel writes a bf16 shadow of every updated parameter (``FlatParams.shadow``):
-    Linear and 1x1-conv weights are consumed by the GEMMs straight from it (no cast kernels).
+    Linear and 1x1-conv weights are consumed by the GEMMs straight from it (no cast kernels);
+    weights whose input-gradient GEMM asked for it (functional.weight_bf16_T: the ViT Linears)
+    also get a transposed bf16 copy, refreshed right after the AdamW kernel by ONE batched
+    transpose launch, so that GEMM reads its weight operand K-contiguous.
     A parameter changed outside the optimizer (load_state_dict, in-place edits through the
     parameter) bumps its version counter and is re-cast on its next use
     (functional.weight_bf16_rows); edits through ``p.data`` bypass that counter — call
@@ -48,6 +51,9 @@ class FlatParams:
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
         self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=dev) if dev.type == "cuda" \
             else None
+        self.gen = 0         # bumped whenever every shadow is rewritten (step, refresh)
+        self.t_params = []   # parameters with a transposed shadow (p._dfu_shadow_T)
+        self.t_jobs = None
         with torch.no_grad():
             for p, o in zip(self.params, self.offsets):
                 view = self.data[o:o + p.numel()].view_as(p)
@@ -56,6 +62,7 @@ class FlatParams:
                 p.grad = self.grad[o:o + p.numel()].view_as(p)
                 if self.shadow is not None:
                     p._dfu_shadow = self.shadow[o:o + p.numel()].view(p.shape[0], -1)
+                    p._dfu_flat = self
         self.refresh_shadow()
 
     def refresh_shadow(self):
@@ -65,6 +72,23 @@ class FlatParams:
         ops.cast_rows_bf16(self.data.view(1, -1), out=self.shadow.view(1, -1))
         for p in self.params:
             p._dfu_shadow_version = p._version
+        self.shadows_rewritten()
+
+    def add_transposed(self, p):
+        """Give parameter p a transposed bf16 shadow, kept current from now on."""
+        sh = p._dfu_shadow
+        p._dfu_shadow_T = torch.empty((sh.shape[1], sh.shape[0]), dtype=sh.dtype,
+                                      device=sh.device)
+        self.t_params.append(p)
+        self.t_jobs = ops.TransposeJobs([(q._dfu_shadow, q._dfu_shadow_T) for q in self.t_params])
+
+    def shadows_rewritten(self):
+        """Every shadow was just rewritten (AdamW, refresh): re-derive the transposed ones."""
+        self.gen += 1
+        if self.t_jobs is not None:
+            self.t_jobs.launch()
+        for p in self.t_params:
+            p._dfu_sgen = p._dfu_tgen = self.gen
 
     def grad_view(self, i):
         p, o = self.params[i], self.offsets[i]
@@ -115,6 +139,7 @@ class FusedAdamW(torch.optim.Optimizer):
         ops.step_increment(self.step_dev)
         ops.adamw_flat(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, g["lr"], b1,
                        b2, g["eps"], g["weight_decay"], self.step_dev, shadow=self.flat.shadow)
+        self.flat.shadows_rewritten()
         return loss
 
     def state_dict(self):

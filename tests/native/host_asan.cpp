@@ -138,14 +138,14 @@ static void random_sweep() {
     const int a = rand() % 2, b = rand() % 2;
     const int e = epis[rand() % 11];
     dfu_gemm_desc d = linear(M, N, K, a, b, e);
-    if (rand() % 4 == 0) d.tile = 1 + rand() % 7;
+    if (rand() % 4 == 0) d.tile = 1 + rand() % 8;
     if (e == DFU_EPI_F32_ACC && rand() % 3 == 0) d.split_k = 1 + rand() % 64;
     int32_t tile = 0, split = 0;
     const int rc = dfu_gemm_plan(&d, &tile, &split);
     EXPECT(rc == DFU_OK || rc == DFU_E_UNSUPPORTED, "sweep: rc %d", rc);
     if (rc == DFU_OK) {
       ++planned;
-      EXPECT(tile >= 1 && tile <= 7 && split >= 1, "sweep: tile %d split %d", tile, split);
+      EXPECT(tile >= 1 && tile <= 8 && split >= 1, "sweep: tile %d split %d", tile, split);
       EXPECT(dfu_gemm_workspace_bytes(&d) >= 0, "sweep: workspace");
     } else {
       EXPECT(strlen(dfu_last_error_string()) > 0, "sweep: empty error");

@@ -153,3 +153,53 @@ def test_vit_block_output_hooks_see_true_gradient():
     (vit.blocks[1](leaf) * Rg).sum().backward()
     assert torch.equal(out.grad, leaf.grad)
     assert torch.equal(hooked[0], leaf.grad)
+
+
+@pytest.mark.parametrize("shape", [(2304, 768), (768, 3072), (64, 8), (200, 136)])
+def test_transpose_bf16(shape):
+    from dfu_hip import ops
+    x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    assert torch.equal(ops.transpose_bf16(x), x.t().contiguous())
+    y = torch.randn(shape[1], shape[0], device=DEV).to(torch.bfloat16)
+    outs = [torch.empty(shape[1], shape[0], dtype=torch.bfloat16, device=DEV),
+            torch.empty(shape[0], shape[1], dtype=torch.bfloat16, device=DEV)]
+    jobs = ops.TransposeJobs([(x, outs[0]), (y, outs[1])])  # one launch, two jobs
+    jobs.launch()
+    assert torch.equal(outs[0], x.t()) and torch.equal(outs[1], y.t())
+
+
+def test_vit_dgrad_on_transposed_shadow_is_bitwise_equal():
+    """The ViT input-gradient GEMMs read the weight K-contiguous from the transposed bf16 shadow
+    (FusedAdamW-managed weights, functional.weight_bf16_T) or MN-major from the shadow itself:
+    the same products in the same K order, so every gradient is bitwise equal; after an
+    optimizer step the batched transpose keeps the copy current."""
+    from models.vit import vit_base_patch16_224
+    from dfu_hip.optim import FusedAdamW
+    torch.manual_seed(0)
+    a = vit_base_patch16_224(num_classes=0).to(DEV).train()
+    b = vit_base_patch16_224(num_classes=0).to(DEV).train()
+    b.load_state_dict(a.state_dict())
+    blocks_a, blocks_b = a.blocks[:2], b.blocks[:2]
+    opt = FusedAdamW(blocks_a.parameters(), lr=1e-3, weight_decay=1e-4)  # a: shadows + T copies
+    x0 = torch.randn(4, 197, 768, device=DEV)
+    Rg = torch.randn(4, 197, 768, device=DEV)
+    for step in range(2):
+        for blocks in (blocks_a, blocks_b):
+            for p in blocks.parameters():
+                p.grad = None if blocks is blocks_b else p.grad
+            xa = x0.clone().requires_grad_(True)
+            (blocks[1](blocks[0](xa)) * Rg).sum().backward()
+            blocks.xgrad = xa.grad
+        torch.cuda.synchronize()
+        assert getattr(blocks_a[0].mlp.fc1.weight, "_dfu_shadow_T", None) is not None
+        assert torch.equal(blocks_a.xgrad, blocks_b.xgrad), step
+        for (n, pa), pb in zip(blocks_a.named_parameters(), blocks_b.parameters()):
+            assert torch.equal(pa.grad, pb.grad), (step, n)
+        # same update on both sides: the T copies must follow the new weights
+        opt.step()
+        opt.zero_grad()
+        with torch.no_grad():
+            for pa, pb in zip(blocks_a.parameters(), blocks_b.parameters()):
+                pb.copy_(pa)
+        w = blocks_a[1].attn.qkv.weight
+        assert torch.equal(w._dfu_shadow_T, w._dfu_shadow.t())

@@ -45,6 +45,17 @@ def build(case, tile):
         A, B, C = T(M, K), T(K, N), T(M, N)
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, N, C, N, b_mode=L.OPND_MNMAJOR,
                                                epilogue=L.EPI_BF16, tile=tile)
+    if case in ("fc1_dgrad_t", "qkv_dgrad_t", "fc2_dgrad_t"):
+        # the dgrads with a pre-transposed weight: B K-contiguous (KM x KM)
+        M, N, K = {"fc1_dgrad_t": (12608, 768, 3072), "qkv_dgrad_t": (12608, 768, 2304),
+                   "fc2_dgrad_t": (12608, 3072, 768)}[case]
+        A, B, C, h = T(M, K), T(N, K), T(M, N), T(M, N)
+        if case == "fc2_dgrad_t":
+            return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N,
+                                                   epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N,
+                                                   tile=tile)
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16,
+                                               tile=tile)
     if case == "fc1_wgrad":
         M, N, K = 3072, 768, 12608
         A, B = T(K, M), T(K, N)
