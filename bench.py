@@ -75,7 +75,10 @@ def build(config, device):
     from models.fusion import MultimodalFusionModel
     from models.single import RGBOnlyModel, ThermalOnlyModel
     if config == "fusion":
-        model = MultimodalFusionModel(num_classes=2, dropout=0.7)
+        # DFU_SERIAL_BRANCHES=1: both encoders on one stream (measures the side-stream overlap)
+        model = MultimodalFusionModel(
+            num_classes=2, dropout=0.7,
+            concurrent_branches=os.environ.get("DFU_SERIAL_BRANCHES", "0") != "1")
         fwd = lambda m, r, t: m(r, t)  # noqa: E731
     elif config == "thermal":  # train_thermal_only.py:188-205
         model = ThermalOnlyModel(num_classes=2)

@@ -171,11 +171,26 @@ def from_rows(r, B, H, W, C):
     return r.view(B, H, W, C).permute(0, 3, 1, 2)
 
 
+def _krsc_strided(w):
+    """A 4-D OIHW-shaped tensor whose memory is KRSC (channels-last), as optim.FlatParams
+    stores spatial conv weights."""
+    return (w.dim() == 4 and not w.is_contiguous()
+            and w.is_contiguous(memory_format=torch.channels_last))
+
+
+def _rows2d(w):
+    """[N, K] rows of w in its storage order (KRSC for a channels-last conv weight: a view)."""
+    if _krsc_strided(w):
+        return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+    return w.reshape(w.shape[0], -1)
+
+
 def weight_bf16_rows(w, ld=None):
-    """fp32 [N, K...] parameter -> bf16 [N, ld] GEMM operand.  Parameters managed by FusedAdamW
-    have a bf16 shadow the optimizer kernel keeps current (optim.FlatParams): returned as a
-    view, re-cast only if the parameter changed outside the optimizer (version counter)."""
-    w2 = w.detach().reshape(w.shape[0], -1)
+    """fp32 [N, K...] parameter -> bf16 [N, ld] GEMM operand, rows in the parameter's storage
+    order.  Parameters managed by FusedAdamW have a bf16 shadow the optimizer kernel keeps
+    current (optim.FlatParams): returned as a view, re-cast only if the parameter changed
+    outside the optimizer (version counter)."""
+    w2 = _rows2d(w.detach())
     sh = getattr(w, "_dfu_shadow", None)
     if sh is not None and (ld is None or ld == w2.shape[1]):
         if w._version != getattr(w, "_dfu_shadow_version", -1):
@@ -206,8 +221,9 @@ def weight_bf16_T(w):
 
 
 def conv_weight_bf16(w):
-    """fp32 OIHW conv weight -> bf16 KRSC GEMM operand (1x1: OIHW == KRSC, the shadow view)."""
-    if w.shape[2] == 1 and w.shape[3] == 1:
+    """fp32 OIHW conv weight -> bf16 KRSC GEMM operand: the shadow view for a 1x1 conv (OIHW ==
+    KRSC) and for a FusedAdamW-managed weight stored channels-last; else a packing kernel."""
+    if (w.shape[2] == 1 and w.shape[3] == 1) or _krsc_strided(w):
         return weight_bf16_rows(w)
     return ops.pack_conv_weight(w.detach())
 
@@ -347,15 +363,20 @@ def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, bn=None, y=None):
 
 
 def conv_wgrad(dy_rows, x_rows, geom, dw):
-    """dw (fp32 OIHW) += wgrad(dy, x)."""
+    """dw (fp32 OIHW shape) += wgrad(dy, x).  The GEMM accumulates in KRSC order (contiguous
+    n' = (r, s, c): coalesced epilogue stores): straight into dw when dw is stored KRSC (a 1x1
+    conv, or optim.FlatParams' channels-last conv weights), else into a scratch buffer that is
+    permute-added into the OIHW gradient."""
     g = geom
     M = g.n * g.p * g.q
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
         ops.gemm(g.k, g.c, M, dy_rows, g.k, x_rows, g.c, dw, g.c, a_mode=L.OPND_MNMAJOR,
                  b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+    elif _krsc_strided(dw):
+        N = g.r * g.s * g.c
+        ops.gemm(g.k, N, M, dy_rows, g.k, x_rows, 0, _rows2d(dw), N, a_mode=L.OPND_MNMAJOR,
+                 b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC, conv=g)
     else:
-        # accumulate in KRSC order (contiguous n' = (r, s, c): coalesced epilogue atomics),
-        # then permute-add into the OIHW fp32 parameter gradient
         N = g.r * g.s * g.c
         acc = _empty((g.k, N), F32, dy_rows.device)
         ops.zero_(acc)

@@ -13,7 +13,11 @@ view) and ``p.grad`` into a matching flat gradient buffer, so:
     Linear and 1x1-conv weights are consumed by the GEMMs straight from it (no cast kernels);
     weights whose input-gradient GEMM asked for it (functional.weight_bf16_T: the ViT Linears)
     also get a transposed bf16 copy, refreshed right after the AdamW kernel by ONE batched
-    transpose launch, so that GEMM reads its weight operand K-contiguous.
+    transpose launch, so that GEMM reads its weight operand K-contiguous;
+  * spatial conv weights (4-D, R*S > 1, C % 8 == 0) are STORED channels-last, i.e. in the
+    implicit-GEMM order KRSC, while keeping their OIHW shape (``p`` is a permuted view): the
+    shadow is then the 3x3 conv's bf16 weight operand as is, and the weight-gradient GEMM
+    accumulates straight into ``p.grad`` (no per-step pack / zero / permute-add kernels).
     A parameter changed outside the optimizer (load_state_dict, in-place edits through the
     parameter) bumps its version counter and is re-cast on its next use
     (functional.weight_bf16_rows); edits through ``p.data`` bypass that counter — call
@@ -31,6 +35,21 @@ def _aligned(n):
     return (n + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
+def stores_krsc(p):
+    """Whether FlatParams stores parameter p channels-last (KRSC): spatial conv weights whose
+    channel count the implicit-GEMM conv takes (the stem's 3-channel 7x7 keeps OIHW)."""
+    return p.dim() == 4 and p.shape[2] * p.shape[3] > 1 and p.shape[1] % 8 == 0
+
+
+def _view(flat, o, p, krsc):
+    """Parameter-shaped view of flat[o:o+n]: OIHW order, or KRSC memory seen as OIHW."""
+    v = flat[o:o + p.numel()]
+    if krsc:
+        K, C, R, S = p.shape
+        return v.view(K, R, S, C).permute(0, 3, 1, 2)
+    return v.view_as(p)
+
+
 class FlatParams:
     """Contiguous fp32 storage for a list of parameters and their gradients."""
 
@@ -40,6 +59,7 @@ class FlatParams:
             raise ValueError("FlatParams: no trainable parameters")
         dev = self.params[0].device
         self.offsets = []
+        self.krsc = [stores_krsc(p) for p in self.params]
         off = 0
         for p in self.params:
             if p.dtype != torch.float32:
@@ -55,12 +75,13 @@ class FlatParams:
         self.t_params = []   # parameters with a transposed shadow (p._dfu_shadow_T)
         self.t_jobs = None
         with torch.no_grad():
-            for p, o in zip(self.params, self.offsets):
-                view = self.data[o:o + p.numel()].view_as(p)
+            for p, o, kr in zip(self.params, self.offsets, self.krsc):
+                view = _view(self.data, o, p, kr)
                 view.copy_(p.data)
                 p.data = view
-                p.grad = self.grad[o:o + p.numel()].view_as(p)
+                p.grad = _view(self.grad, o, p, kr)
                 if self.shadow is not None:
+                    # [out][in...] rows in storage order (KRSC for channels-last conv weights)
                     p._dfu_shadow = self.shadow[o:o + p.numel()].view(p.shape[0], -1)
                     p._dfu_flat = self
         self.refresh_shadow()
@@ -90,9 +111,13 @@ class FlatParams:
         for p in self.t_params:
             p._dfu_sgen = p._dfu_tgen = self.gen
 
+    def view(self, buf, i):
+        """Parameter i's slice of a flat buffer (data, grad or an optimizer moment), shaped and
+        strided like the parameter."""
+        return _view(buf, self.offsets[i], self.params[i], self.krsc[i])
+
     def grad_view(self, i):
-        p, o = self.params[i], self.offsets[i]
-        return self.grad[o:o + p.numel()].view_as(p)
+        return self.view(self.grad, i)
 
     def rebind_grads(self):
         """Re-attach p.grad to the flat buffer if user code replaced or cleared it (eager)."""
@@ -150,11 +175,10 @@ class FusedAdamW(torch.optim.Optimizer):
         step = torch.tensor(float(self.step_dev.item()))
         index = {id(p): i for i, p in enumerate(self.param_groups[0]["params"])}
         for j, p in enumerate(self.flat.params):
-            o, n = self.flat.offsets[j], p.numel()
             sd["state"][index[id(p)]] = {
                 "step": step.clone(),
-                "exp_avg": self.exp_avg[o:o + n].view_as(p),
-                "exp_avg_sq": self.exp_avg_sq[o:o + n].view_as(p),
+                "exp_avg": self.flat.view(self.exp_avg, j),
+                "exp_avg_sq": self.flat.view(self.exp_avg_sq, j),
             }
         return sd
 
@@ -170,9 +194,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 st = state.get(index[id(p)])
                 if not st:
                     continue
-                o, n = self.flat.offsets[j], p.numel()
-                self.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
-                self.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                self.flat.view(self.exp_avg, j).copy_(st["exp_avg"].reshape(p.shape))
+                self.flat.view(self.exp_avg_sq, j).copy_(st["exp_avg_sq"].reshape(p.shape))
                 steps.add(int(float(st["step"])))
         if len(steps) > 1:
             raise ValueError(f"FusedAdamW: parameters at different steps {sorted(steps)}")

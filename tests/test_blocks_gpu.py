@@ -203,3 +203,46 @@ def test_vit_dgrad_on_transposed_shadow_is_bitwise_equal():
                 pb.copy_(pa)
         w = blocks_a[1].attn.qkv.weight
         assert torch.equal(w._dfu_shadow_T, w._dfu_shadow.t())
+
+
+def test_resnet_stage_with_channels_last_conv_weights_is_bitwise_equal():
+    """FusedAdamW stores the 3x3 conv weights channels-last (KRSC, optim.FlatParams): the
+    forward reads the bf16 shadow as the GEMM operand and the weight-gradient GEMM accumulates
+    straight into p.grad.  Against unmanaged weights (per-call OIHW -> KRSC packing, gradient
+    permute-added from a scratch buffer) every gradient and output is bitwise equal, before and
+    after an optimizer step."""
+    from models.resnet import resnet50
+    from dfu_hip.optim import FusedAdamW
+    torch.manual_seed(0)
+    a = resnet50(num_classes=0).to(DEV).train()
+    b = resnet50(num_classes=0).to(DEV).train()
+    b.load_state_dict(a.state_dict())
+    sa, sb = a.layer2, b.layer2  # stride-2 3x3 conv, downsample, stride-1 3x3 convs
+    opt = FusedAdamW(sa.parameters(), lr=1e-3, weight_decay=1e-4)
+    w = sa[0].conv2.weight
+    assert w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous()
+    x0 = torch.randn(4, 256, 56, 56, device=DEV).contiguous(memory_format=torch.channels_last)
+    for step in range(2):
+        outs = []
+        for s in (sa, sb):
+            if s is sb:
+                for p in s.parameters():
+                    p.grad = None
+            y = s(x0)
+            Rg = torch.randn(y.shape, device=DEV,
+                             generator=torch.Generator(device=DEV).manual_seed(step))
+            (y.float() * Rg).sum().backward()
+            outs.append(y.detach().float())
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), step
+        for (n, pa), pb in zip(sa.named_parameters(), sb.parameters()):
+            assert torch.equal(pa.grad, pb.grad), (step, n)
+        opt.step()
+        opt.zero_grad()
+        with torch.no_grad():
+            for pa, pb in zip(sa.parameters(), sb.parameters()):
+                pb.copy_(pa)
+        for bn_a, bn_b in zip(sa.modules(), sb.modules()):
+            if isinstance(bn_a, torch.nn.BatchNorm2d):
+                bn_b.running_mean.copy_(bn_a.running_mean)
+                bn_b.running_var.copy_(bn_a.running_var)

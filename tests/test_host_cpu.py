@@ -126,6 +126,38 @@ def test_flat_params_layout():
     assert fp.numel == 4 + 8 + 8 + 4
 
 
+def test_flat_params_store_spatial_conv_weights_krsc():
+    """Spatial conv weights live channels-last (KRSC) in the flat buffers with their OIHW shape
+    and values; 1x1 and 3-channel (stem) weights and everything else keep the plain order; the
+    optimizer's state_dict moments read back in parameter order."""
+    from dfu_hip.optim import FlatParams
+    w3 = torch.nn.Parameter(torch.randn(16, 8, 3, 3))
+    w1 = torch.nn.Parameter(torch.randn(16, 8, 1, 1))
+    stem = torch.nn.Parameter(torch.randn(4, 3, 7, 7))
+    lin = torch.nn.Parameter(torch.randn(5, 7))
+    vals = [p.detach().clone() for p in (w3, w1, stem, lin)]
+    fp = FlatParams([w3, w1, stem, lin])
+    assert fp.krsc == [True, False, False, False]
+    for p, v in zip((w3, w1, stem, lin), vals):
+        assert torch.equal(p.detach(), v)
+    o = fp.offsets[0]
+    krsc = fp.data[o:o + w3.numel()].view(16, 3, 3, 8)
+    assert torch.equal(krsc, vals[0].permute(0, 2, 3, 1))
+    assert w3.is_contiguous(memory_format=torch.channels_last) and not w3.is_contiguous()
+    assert w3.grad.stride() == w3.stride() and w3.grad.data_ptr() == fp.grad.data_ptr() + 4 * o
+    assert fp.grad_view(0).stride() == w3.stride()
+    # a gradient written through the parameter-shaped view lands in KRSC order
+    g = torch.randn(16, 8, 3, 3)
+    w3.grad.copy_(g)
+    assert torch.equal(fp.grad[o:o + w3.numel()].view(16, 3, 3, 8), g.permute(0, 2, 3, 1))
+    # FusedAdamW.state_dict's moments are these views of its flat moment buffers
+    m = torch.zeros_like(fp.data)
+    m[o:o + w3.numel()] = torch.arange(w3.numel(), dtype=torch.float32)
+    v = fp.view(m, 0)
+    assert v.shape == w3.shape and torch.equal(v.permute(0, 2, 3, 1).reshape(-1),
+                                               torch.arange(w3.numel(), dtype=torch.float32))
+
+
 def test_gradcam_target_layer_rule():
     """grad_cam_visualization.py:389-392: the target is the LAST module name containing the
     target string — the block output ReLU of layer4 and the ViT's last drop_path2 (a 3-D token
