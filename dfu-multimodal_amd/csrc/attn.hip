@@ -35,6 +35,17 @@ DFU_DEV bf16x8 tr_frag(const char* lds, int u, int d0, int lane) {
   bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
   return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// The same fragment by asm reads (common.h lds_tr16_b64), for kernels that stage by LDS-DMA:
+// retire them (lds_reads_retired + pin) before the first use.
+DFU_DEV bf16x8 tr_frag_asm(const char* lds, int u, int d0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = d0 + 4 * p;
+  const int chunk = col >> 3, half = (col >> 2) & 1;
+  const int r0 = 32 * u + 4 * g + q;
+  bf16x4 x0 = lds_tr16_b64(lds + r128_off(r0, chunk) + half * 8);
+  bf16x4 x1 = lds_tr16_b64(lds + r128_off(r0 + 16, chunk) + half * 8);
+  return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 DFU_DEV bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
   u32x4 w;
   w[0] = pack2(a[0], a[1]);
@@ -90,283 +101,196 @@ constexpr float LOG2E = 1.4426950408889634f;
 // range-reduction code (cmp, cndmask, ldexp) that made the attention kernels VALU-bound.
 DFU_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// NW waves share the (b, h) slice: 13 query tiles of 16 at N = 197, at most 2 per wave with 8
-// (the LDS images allow 2 workgroups per CU, so waves, not workgroups, carry the parallelism).
+// 16 zero bytes: the LDS-DMA source of padding rows
+__device__ __attribute__((aligned(16))) const uint32_t g_attn_zero16[4] = {0u, 0u, 0u, 0u};
+
+typedef __attribute__((address_space(3))) void attn_lds_void;
+typedef const __attribute__((address_space(1))) void attn_glb_void;
+
+// Issue this wave's share of the LDS-DMA that stages the K and V images of one (b, h) slice
+// (rows >= N zero) into `img` (K at 0, V at NPAD*128).  One wave instruction fills 1 KiB = 8 rows
+// of an r128 image at a wave-uniform base, lane l at base + 16 l: row 8j + (l >> 3), position
+// l & 7, which in the r128 image holds 16-B chunk (l & 7) ^ swizzle(row).  The images' 4*KT
+// instructions are spread over the NW waves, KT/2 each (KT even: NPAD is a multiple of 32).
+template <int KT, int NW>
+DFU_DEV void stage_kv_dma(char* img, const bf16_t* kbase, const bf16_t* vbase,
+                          int64_t tok_stride, int N, int wave, int lane) {
+  constexpr int PER_IMG = 2 * KT;  // NPAD * 128 / 1024
+  constexpr int PER_WAVE = 4 * KT / NW;
+  static_assert((4 * KT) % NW == 0, "DMA instructions split evenly over the waves");
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int j = wave + NW * i;
+    const int im = j / PER_IMG, blk = j - im * PER_IMG;
+    const int row = 8 * blk + (lane >> 3);
+    const int chunk = (lane & 7) ^ (((row >> 1) & 3) << 1);
+    const bf16_t* base = im ? vbase : kbase;
+    const void* src = row < N ? (const void*)(base + (int64_t)row * tok_stride + chunk * 8)
+                              : (const void*)g_attn_zero16;
+    char* dst = img + im * (KT * 16 * 128) + blk * 1024;
+    __builtin_amdgcn_global_load_lds((attn_glb_void*)src, (attn_lds_void*)dst, 16, 0, 0);
+  }
+}
+
+// Persistent forward: one 8-wave workgroup per CU walks the (b, h) slices blockIdx.x,
+// + gridDim.x, ...; the K/V images live in two LDS buffers, and the next slice's images are
+// DMA'd (global_load_lds, no register round trip) while this one is computed, so the staging
+// latency that a one-slice-per-workgroup launch exposed (216 VGPRs: one workgroup per CU)
+// overlaps the math.  13 query tiles of 16 at N = 197: at most 2 per wave.
 template <int KT, int NW = 8>
 __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__ qkv, int N, int H,
-                                                      float scale, bf16_t* __restrict__ o,
+                                                      int BH, float scale,
+                                                      bf16_t* __restrict__ o,
                                                       float* __restrict__ lse) {
   constexpr int NPAD = KT * 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NPAD * 128];
-  char* Ks = smem;
-  char* Vs = smem + NPAD * 128;
+  constexpr int IMG2 = 2 * NPAD * 128;  // K + V images of one slice
+  constexpr int QPW = 2;                // query tiles per wave and slice (QT <= 2 * NW)
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int64_t tok_stride = (int64_t)3 * H * 64;
-  const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
   const int QT = (N + 15) / 16;
-  // this wave's query fragments, one tile ahead: the first tile's load overlaps the K/V staging,
-  // each next tile's overlaps the current tile's math
-  auto load_q = [&](int qt, u32x4 (&v)[2]) {
-    const int q = qt * 16 + (lane & 15);
+  const float c = scale * LOG2E;
+  auto slice_base = [&](int bh) {
+    const int b = bh / H, h = bh - b * H;
+    return qkv + (int64_t)b * N * tok_stride + h * 64;
+  };
+  // this wave's query fragments of a slice (exactly 2 QPW loads per lane, branch-free: rows
+  // past N re-read row N - 1, unused)
+  auto load_q = [&](int bh, u32x4 (&v)[QPW][2]) {
+    const bf16_t* qbase = slice_base(bh);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      v[ks] = (u32x4){0u, 0u, 0u, 0u};
-      if (qt < QT && q < N) v[ks] = *(const u32x4*)(qbase + (int64_t)q * tok_stride + 32 * ks + 8 * g);
+    for (int j = 0; j < QPW; ++j) {
+      const int q = (wave + NW * j) * 16 + (lane & 15);
+      const int64_t qo = (int64_t)(q < N ? q : N - 1) * tok_stride + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) v[j][ks] = *(const u32x4*)(qbase + qo + 32 * ks);
     }
   };
-  u32x4 qnext[2];
-  load_q(wave, qnext);
-  stage_rows2<NPAD, 64 * NW>(Ks, qbase + H * 64, Vs, qbase + 2 * H * 64, tok_stride, N, tid);
-  __syncthreads();
-  const float c = scale * LOG2E;
-  for (int qt = wave; qt < QT; qt += NW) {
-    const int q = qt * 16 + (lane & 15);
-    bf16x8 qf[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, qnext[ks]);
-    load_q(qt + NW, qnext);
-    f32x4 s[KT];
-#pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * t, ks, lane), qf[ks], s[t], 0, 0, 0);
-    }
-    // lane holds S[q][key = 16t + 4g + r]
-    // padding keys: NPAD rounds N up to a multiple of 32, so only the last two key tiles (a
-    // compile-time set) can hold them
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      if (t >= KT - 2) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (16 * t + 4 * g + r >= N) s[t][r] = -INFINITY;
-      }
-      mx = fmaxf(mx, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    // exponent arguments and the row sum on packed pairs (v_pk_fma_f32 / v_pk_add_f32)
-    const f32x2 c2 = {c, c}, b2 = {-mx * c, -mx * c};
-    f32x2 l2 = {0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < KT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        f32x2 a = {s[t][r], s[t][r + 1]};
-        a = a * c2 + b2;
-        a[0] = fast_exp2(a[0]);
-        a[1] = fast_exp2(a[1]);
-        s[t][r] = a[0];
-        s[t][r + 1] = a[1];
-        l2 += a;
-      }
-    float l = l2[0] + l2[1];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    f32x4 acc[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < KT / 2; ++u) {
-      const bf16x8 pb = pack_frag(s[2 * u], s[2 * u + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Vs, u, 16 * dt, lane), pb, acc[dt], 0, 0, 0);
-    }
-    if (q < N) {
-      const float inv = 1.0f / l;
-      bf16_t* orow = o + ((int64_t)b * N + q) * H * 64 + h * 64 + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        *(u32x2*)(orow + 16 * dt) = (u32x2){pack2(acc[dt][0] * inv, acc[dt][1] * inv),
-                                            pack2(acc[dt][2] * inv, acc[dt][3] * inv)};
-      if (g == 0) lse[(int64_t)bh * NPAD + q] = mx * scale + logf(l);
-    }
+  u32x4 qn[QPW][2];
+  {
+    const bf16_t* qb = slice_base(blockIdx.x);
+    stage_kv_dma<KT, NW>(smem, qb + H * 64, qb + 2 * H * 64, tok_stride, N, wave, lane);
+    load_q(blockIdx.x, qn);
   }
-}
-
-// dQ (and delta = rowsum(dO * O)), query-owned.
-template <int KT>
-__global__ __launch_bounds__(256) void k_attn_bwd_dq(const bf16_t* __restrict__ qkv,
-                                                     const bf16_t* __restrict__ o,
-                                                     const bf16_t* __restrict__ dout,
-                                                     const float* __restrict__ lse, int N, int H,
-                                                     float scale, float* __restrict__ delta,
-                                                     bf16_t* __restrict__ dqkv) {
-  constexpr int NPAD = KT * 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NPAD * 128];
-  char* Ks = smem;
-  char* Vs = smem + NPAD * 128;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-  const int64_t tok_stride = (int64_t)3 * H * 64;
-  const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
-  const int64_t o_stride = (int64_t)H * 64;
-  const bf16_t* obase = o + (int64_t)b * N * o_stride + h * 64;
-  const bf16_t* dobase = dout + (int64_t)b * N * o_stride + h * 64;
-  stage_rows2<NPAD, 256>(Ks, qbase + H * 64, Vs, qbase + 2 * H * 64, tok_stride, N, tid);
-  __syncthreads();
-  const float c = scale * LOG2E;
-  const int QT = (N + 15) / 16;
-  for (int qt = wave; qt < QT; qt += 4) {
-    const int q = qt * 16 + (lane & 15);
-    const bool qv = q < N;
-    bf16x8 qf[2], df[2];
-    float dsum = 0.f;
+  int it = 0;
+  for (int bh = blockIdx.x; bh < BH; bh += gridDim.x, ++it) {
+    const char* Ks = smem + (it & 1) * IMG2;
+    const char* Vs = Ks + NPAD * 128;
+    const int b = bh / H, h = bh - b * H;
+    // this slice's images and query fragments have landed (and the previous slice's stores):
+    // one wait, pinned to the query registers so the compiler's own wait for them happens
+    // here and not in front of the first MFMA (where it would also drain the next DMA)
+    u32x4 qv[QPW][2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      u32x4 vq = {0u, 0u, 0u, 0u}, vd = {0u, 0u, 0u, 0u}, vo = {0u, 0u, 0u, 0u};
-      if (qv) {
-        vq = *(const u32x4*)(qbase + (int64_t)q * tok_stride + 32 * ks + 8 * g);
-        vd = *(const u32x4*)(dobase + (int64_t)q * o_stride + 32 * ks + 8 * g);
-        vo = *(const u32x4*)(obase + (int64_t)q * o_stride + 32 * ks + 8 * g);
+    for (int j = 0; j < QPW; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) qv[j][ks] = qn[j][ks];
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(qv[0][0]), "+v"(qv[0][1]), "+v"(qv[1][0]),
+                 "+v"(qv[1][1])::"memory");
+    // after the barrier every wave is past the previous slice, so the other buffer is free:
+    // stage the next slice into it, and prefetch the next slice's query fragments (the last
+    // slice re-stages / re-loads itself: unconditional, fixed-count issues)
+    __builtin_amdgcn_s_barrier();  // (no fence: the wait above is the one needed)
+    {
+      const int nb = bh + (int)gridDim.x < BH ? bh + (int)gridDim.x : bh;
+      const bf16_t* nq = slice_base(nb);
+      stage_kv_dma<KT, NW>(smem + ((it + 1) & 1) * IMG2, nq + H * 64, nq + 2 * H * 64,
+                           tok_stride, N, wave, lane);
+      load_q(nb, qn);
+    }
+#pragma unroll
+    for (int j = 0; j < QPW; ++j) {
+      const int qt = wave + NW * j;
+      if (qt >= QT) break;
+      const int q = qt * 16 + (lane & 15);
+      bf16x8 qf[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, qv[j][ks]);
+      f32x4 s[KT];
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * t, ks, lane), qf[ks], s[t], 0, 0, 0);
       }
-      qf[ks] = __builtin_bit_cast(bf16x8, vq);
-      df[ks] = __builtin_bit_cast(bf16x8, vd);
-      float fd[8], fo[8];
-      unpack8(vd, fd);
-      unpack8(vo, fo);
+      // lane holds S[q][key = 16t + 4g + r]; padding keys: NPAD rounds N up to a multiple of
+      // 32, so only the last two key tiles (a compile-time set) can hold them
+      float mx = -INFINITY;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) dsum += fd[e] * fo[e];
-    }
-    dsum += __shfl_xor(dsum, 16, 64);
-    dsum += __shfl_xor(dsum, 32, 64);
-    if (g == 0) delta[(int64_t)bh * NPAD + q] = qv ? dsum : 0.f;
-    const float lq = qv ? lse[(int64_t)bh * NPAD + q] * LOG2E : 0.f;
-    f32x4 s[KT];
+      for (int t = 0; t < KT; ++t) {
+        if (t >= KT - 2) {
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * t, ks, lane), qf[ks], st, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Vs, 16 * t, ks, lane), df[ks], dp, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = 16 * t + 4 * g + r;
-        const float pv = (qv && key < N) ? fast_exp2(fmaf(st[r], c, -lq)) : 0.f;
-        st[r] = pv * (dp[r] - dsum);
-      }
-      s[t] = st;
-    }
-    f32x4 acc[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < KT / 2; ++u) {
-      const bf16x8 dsb = pack_frag(s[2 * u], s[2 * u + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ks, u, 16 * dt, lane), dsb, acc[dt], 0, 0, 0);
-    }
-    if (qv) {
-      bf16_t* dst = dqkv + ((int64_t)b * N + q) * tok_stride + h * 64 + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        *(u32x2*)(dst + 16 * dt) = (u32x2){pack2(acc[dt][0] * scale, acc[dt][1] * scale),
-                                           pack2(acc[dt][2] * scale, acc[dt][3] * scale)};
-    }
-  }
-}
-
-// dK, dV, key-owned.
-template <int KT>
-__global__ __launch_bounds__(256) void k_attn_bwd_dkv(const bf16_t* __restrict__ qkv,
-                                                      const bf16_t* __restrict__ dout,
-                                                      const float* __restrict__ lse,
-                                                      const float* __restrict__ delta, int N,
-                                                      int H, float scale,
-                                                      bf16_t* __restrict__ dqkv) {
-  constexpr int NPAD = KT * 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NPAD * 128 + 2 * NPAD * 4];
-  char* Qs = smem;
-  char* Ds = smem + NPAD * 128;
-  float* Ls = (float*)(smem + 2 * NPAD * 128);
-  float* Es = Ls + NPAD;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-  const int64_t tok_stride = (int64_t)3 * H * 64;
-  const bf16_t* qbase = qkv + (int64_t)b * N * tok_stride + h * 64;
-  const int64_t o_stride = (int64_t)H * 64;
-  stage_rows(Qs, qbase, tok_stride, N, NPAD, tid);
-  stage_rows(Ds, dout + (int64_t)b * N * o_stride + h * 64, o_stride, N, NPAD, tid);
-  for (int i = tid; i < NPAD; i += 256) {
-    Ls[i] = i < N ? lse[(int64_t)bh * NPAD + i] * LOG2E : 0.f;
-    Es[i] = i < N ? delta[(int64_t)bh * NPAD + i] : 0.f;
-  }
-  __syncthreads();
-  const float c = scale * LOG2E;
-  const int KTc = (N + 15) / 16;
-  for (int kt = wave; kt < KTc; kt += 4) {
-    const int key = kt * 16 + (lane & 15);
-    const bool kv = key < N;
-    bf16x8 kf[2], vf[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      u32x4 a = {0u, 0u, 0u, 0u}, v = {0u, 0u, 0u, 0u};
-      if (kv) {
-        a = *(const u32x4*)(qbase + (int64_t)key * tok_stride + H * 64 + 32 * ks + 8 * g);
-        v = *(const u32x4*)(qbase + (int64_t)key * tok_stride + 2 * H * 64 + 32 * ks + 8 * g);
-      }
-      kf[ks] = __builtin_bit_cast(bf16x8, a);
-      vf[ks] = __builtin_bit_cast(bf16x8, v);
-    }
-    f32x4 dv[4], dk[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll 1
-    for (int u = 0; u < KT / 2; ++u) {
-      f32x4 ph[2], dsh[2];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int qt = 2 * u + hh;
-        f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * qt, ks, lane), kf[ks], st, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * qt, ks, lane), vf[ks], dp, 0, 0, 0);
+          for (int r = 0; r < 4; ++r)
+            if (16 * t + 4 * g + r >= N) s[t][r] = -INFINITY;
         }
-        // lane holds S[q = 16qt + 4g + r][key]
+        mx = fmaxf(mx, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      // exponent arguments and the row sum on packed pairs (v_pk_fma_f32 / v_pk_add_f32)
+      const f32x2 c2 = {c, c}, b2 = {-mx * c, -mx * c};
+      f32x2 l2 = {0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = 16 * qt + 4 * g + r;
-          const float pv = (kv && q < N) ? fast_exp2(fmaf(st[r], c, -Ls[q])) : 0.f;
-          ph[hh][r] = pv;
-          dsh[hh][r] = pv * (dp[r] - Es[q]);
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          f32x2 a = {s[t][r], s[t][r + 1]};
+          a = a * c2 + b2;
+          a[0] = fast_exp2(a[0]);
+          a[1] = fast_exp2(a[1]);
+          s[t][r] = a[0];
+          s[t][r + 1] = a[1];
+          l2 += a;
         }
-      }
-      const bf16x8 pb = pack_frag(ph[0], ph[1]);
-      const bf16x8 db = pack_frag(dsh[0], dsh[1]);
+      float l = l2[0] + l2[1];
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+      f32x4 acc[4];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Ds, u, 16 * dt, lane), pb, dv[dt], 0, 0, 0);
-        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag(Qs, u, 16 * dt, lane), db, dk[dt], 0, 0, 0);
-      }
-    }
-    if (kv) {
-      bf16_t* dst = dqkv + ((int64_t)b * N + key) * tok_stride + h * 64 + 4 * g;
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      // V^T fragments one 32-token chunk ahead: chunk u+1's reads go out before chunk u's MFMAs
+      bf16x8 vf[4];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        *(u32x2*)(dst + H * 64 + 16 * dt) = (u32x2){pack2(dk[dt][0] * scale, dk[dt][1] * scale),
-                                                    pack2(dk[dt][2] * scale, dk[dt][3] * scale)};
-        *(u32x2*)(dst + 2 * H * 64 + 16 * dt) = (u32x2){pack2(dv[dt][0], dv[dt][1]),
-                                                        pack2(dv[dt][2], dv[dt][3])};
+      for (int dt = 0; dt < 4; ++dt) vf[dt] = tr_frag_asm(Vs, 0, 16 * dt, lane);
+#pragma unroll
+      for (int u = 0; u < KT / 2; ++u) {
+        const bf16x8 pb = pack_frag(s[2 * u], s[2 * u + 1]);
+        lds_reads_retired();
+        bf16x8 cur[4];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          pin(vf[dt]);
+          cur[dt] = vf[dt];
+        }
+        if (u + 1 < KT / 2) {
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) vf[dt] = tr_frag_asm(Vs, u + 1, 16 * dt, lane);
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[dt], pb, acc[dt], 0, 0, 0);
+      }
+      if (q < N) {
+        const float inv = 1.0f / l;
+        bf16_t* orow = o + ((int64_t)b * N + q) * H * 64 + h * 64 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          *(u32x2*)(orow + 16 * dt) = (u32x2){pack2(acc[dt][0] * inv, acc[dt][1] * inv),
+                                              pack2(acc[dt][2] * inv, acc[dt][3] * inv)};
+        if (g == 0) lse[(int64_t)bh * NPAD + q] = mx * scale + logf(l);
       }
     }
   }
+  // the last (redundant) DMA lands before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Fused backward: one workgroup (8 waves) per (b, h).  Q, K, V, dO are staged once into LDS
 // (4 r128 images), with LSE and delta = rowsum(dO * O); then the waves share one pool of work
-// items: QT query tiles (dQ, as k_attn_bwd_dq) and QT key tiles (dK/dV, as k_attn_bwd_dkv).
+// items: QT query tiles (dQ: recompute S and P, dP^T = V dO^T, dS = P (dP - delta),
+// dQ^T = K^T dS^T) and QT key tiles (dK/dV: S = Q K^T, dP = dO V^T; dV^T += dO^T P,
+// dK^T += Q^T dS).
 template <int KT>
 __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict__ qkv,
                                                         const bf16_t* __restrict__ o,
@@ -550,6 +474,18 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
     default: break;            \
   }
 
+int attn_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+
 }  // namespace
 
 extern "C" int dfu_attention_npad(int32_t N) { return ((N + 31) / 32) * 32; }
@@ -561,7 +497,9 @@ extern "C" int dfu_attention_fwd(const void* qkv, int32_t B, int32_t N, int32_t 
   DFU_CHECK_ARG(N > 0 && N <= 256, "dfu_attention_fwd: N=%d unsupported (<= 256)", N);
   const int KT = dfu_attention_npad(N) / 16;
   hipStream_t s = (hipStream_t)stream;
-#define CALL(K) hipLaunchKernelGGL(k_attn_fwd<K>, dim3(B * H), dim3(512), 0, s, (const bf16_t*)qkv, N, H, scale, (bf16_t*)o, lse)
+  const int BH = B * H;
+  const int grid = BH < attn_cus() ? BH : attn_cus();  // persistent: one workgroup per CU
+#define CALL(K) hipLaunchKernelGGL(k_attn_fwd<K>, dim3(grid), dim3(512), 0, s, (const bf16_t*)qkv, N, H, BH, scale, (bf16_t*)o, lse)
   DISPATCH_KT(KT, CALL)
 #undef CALL
   DFU_LAUNCH_CHECK();

@@ -49,6 +49,27 @@ DFU_DEV u32x4 pack8(const float* f) {
   return r;
 }
 
+// ds_read_b64_tr_b16 by inline asm.  The compiler's own form of this read (the builtin) carries
+// no alias information, so in a kernel that also issues LDS-DMA (global_load_lds /
+// buffer_load ... lds) the waitcnt pass puts an `s_waitcnt vmcnt(0)` in front of every such
+// read: it drains every DMA in flight, including the prefetch of the NEXT K-step, and turns a
+// multi-stage ring into load-then-compute for every MN-major operand.  The asm form is
+// invisible to that pass; its lgkmcnt wait is the caller's: lds_reads_retired() and pin() on
+// every register it filled before the first use.
+DFU_DEV bf16x4 lds_tr16_b64(const char* p) {
+  bf16x4 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+DFU_DEV void lds_reads_retired() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Orders every later use of v after the preceding lds_reads_retired() (volatile asm statements
+// keep their order; v's consumers take the value this one defines).
+template <class T>
+DFU_DEV void pin(T& v) {
+  asm volatile("" : "+v"(v));
+}
+
 DFU_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -319,8 +319,9 @@ DFU_DEV bf16x8 read_frag(const char* lds, int rb, int ks, int lane) {
     const int chunk = col >> 3, half = (col >> 2) & 1;
     const char* a0 = img + mn_off(krow, chunk) + half * 8;
     const char* a1 = img + mn_off(krow + 4, chunk) + half * 8;
-    bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
-    bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
+    // asm reads (common.h lds_tr16_b64): the caller retires them before the first use
+    bf16x4 x0 = lds_tr16_b64(a0);
+    bf16x4 x1 = lds_tr16_b64(a1);
     return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
@@ -1113,6 +1114,13 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
         for (int i = 0; i < FM; ++i) fa[i] = read_frag<AK>(la, wr * WTM + i * 16, ks, lane);
 #pragma unroll
         for (int j = 0; j < FN; ++j) fb[j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
+        if constexpr (!AK || !BKc) {  // asm (MN-major) reads: retired before the MFMAs
+          lds_reads_retired();
+#pragma unroll
+          for (int i = 0; i < FM; ++i) pin(fa[i]);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) pin(fb[j]);
+        }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1129,6 +1137,16 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
         for (int j = 0; j < FN; ++j) fb[ks][j] = read_frag<BKc>(lb, wc * WTN + j * 16, ks, lane);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them)
+      if constexpr (!AK || !BKc) {  // asm (MN-major) reads: retired before the MFMAs
+        lds_reads_retired();
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) pin(fa[ks][i]);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) pin(fb[ks][j]);
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll

@@ -202,7 +202,14 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
             fb[j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
       };
       auto mfma = [&](int ha, int hb) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_reads_retired();
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {  // (asm MN-major reads: ordered after the wait)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pin(fa[i][ks]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) pin(fb[j][ks]);
+        }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)

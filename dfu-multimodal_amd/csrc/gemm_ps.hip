@@ -319,7 +319,8 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     // k-half (ks) at a time, and the reads the NEXT group needs go out as soon as the group
     // before it has consumed the registers they overwrite, so every read has a group of 8
     // MFMAs (this wave's and its SIMD partner's) to land under instead of stalling the pipe
-    // (the compiler's lgkmcnt waits are the exact ones: each read's consumer is known).
+    // (the compiler's lgkmcnt waits are the exact ones for K-contiguous reads; MN-major ones are
+    // asm, retired by an lgkmcnt(0) in front of each group).
     // kSched bit 2: both B halves stay in registers (fbh[hb]), so phase 4 does not re-read B-left
     constexpr bool kB2 = (kSched & 4) != 0;
     bf16x8 fa[4][2], fbh[2][2][2];
@@ -344,6 +345,13 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
       if constexpr ((kAbl & 2) != 0) {
         __builtin_amdgcn_sched_barrier(0);
         return;
+      }
+      if constexpr (!AK_ || !BK_) {  // asm (MN-major) fragment reads: retired before use
+        lds_reads_retired();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pin(fa[i][ks]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) pin(fbh[kB2 ? hb : 0][j][ks]);
       }
       if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
