@@ -137,6 +137,60 @@ def side_stream(device):
     return st
 
 
+_wgrad_streams = {}
+# DFU_VIT_WGRAD_STREAM=0: the ViT weight-gradient GEMMs stay on the backward's own stream (A/B)
+_VIT_WGRAD_STREAM = os.environ.get("DFU_VIT_WGRAD_STREAM", "1") != "0"
+
+
+def wgrad_stream(device):
+    """One persistent stream per device for the ViT blocks' weight-gradient GEMMs: they depend
+    only on tensors already produced and feed only the optimizer, so they run beside the input-
+    gradient chain, whose N = 768 GEMMs fill 150 of the 256 CUs (12608 / 256 x 768 / 256 tiles)
+    and whose LayerNorm / attention kernels leave the MFMAs idle."""
+    idx = torch.device(device).index
+    if idx is None:
+        idx = torch.cuda.current_device()
+    st = _wgrad_streams.get(idx)
+    if st is None:
+        st = _wgrad_streams[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
+_concurrent_encoders = [0]
+
+
+class concurrent_encoders:
+    """Context of a forward whose encoders run on two streams (models.fusion): there the other
+    encoder's kernels already fill the CUs an N = 768 GEMM leaves idle, and a third stream of
+    ViT weight gradients measured slower (18.75 -> 19.2 ms per fusion step), so ViT blocks
+    built inside it keep their weight gradients inline (thermal-only: 13.66 -> 12.38 ms)."""
+
+    def __enter__(self):
+        _concurrent_encoders[0] += 1
+
+    def __exit__(self, *exc):
+        _concurrent_encoders[0] -= 1
+
+
+class _Beside:
+    """Runs weight-gradient work on the wgrad stream after everything already enqueued on the
+    current stream (the producers of its operands); the operands are recorded on that stream so
+    the allocator does not recycle them early.  Without a stream it runs inline."""
+
+    def __init__(self, stream):
+        self.ws = stream
+        self.cur = torch.cuda.current_stream() if stream is not None else None
+
+    def run(self, fn, *tensors):
+        if self.ws is None:
+            return fn()
+        self.ws.wait_stream(self.cur)
+        with torch.cuda.stream(self.ws):
+            for t in tensors:
+                t.record_stream(self.ws)
+            return fn()
+
+
 def grads_done(*params):
     for p in params:
         if p is not None:
@@ -857,6 +911,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
+        ctx.beside = _VIT_WGRAD_STREAM and _concurrent_encoders[0] == 0
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
@@ -904,6 +959,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
+        ctx.beside = _VIT_WGRAD_STREAM and _concurrent_encoders[0] == 0
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
@@ -933,45 +989,49 @@ class ViTBlockFn(torch.autograd.Function):
         # the block's eight "sum per-block partials into a gradient vector" reductions (bias
         # column sums, LayerNorm dgamma / dbeta) run as one launch at the end (PartialReductions)
         red = ops.PartialReductions()
+        # weight gradients (and the bias column sums of the tensors they read) on the wgrad
+        # stream, beside the input-gradient chain (wgrad_stream); their reductions batch apart
+        bw = _Beside(wgrad_stream(dev) if (ctx.beside and g.is_cuda) else None)
+        red_w = ops.PartialReductions() if bw.ws is not None else red
+
+        def wgrad(lin, dy, x, width=None):
+            def fn():
+                if _wants(lin.weight):
+                    _linear_wgrad(dy, x, lin.weight, rows)
+                if width is not None and _wants(lin.bias):
+                    red_w.add(ops.colsum_partial(dy), grad_buffer(lin.bias), width)
+                grads_done(lin.weight)
+            bw.run(fn, dy, x)
+
         # ---- MLP branch: x_out = x_mid + fc2(gelu(fc1(norm2(x_mid))))
+        wgrad(mlp.fc2, gb, h)
         dh_pre = _empty((rows, Dh), BF16, dev)
         _linear_dgrad(rows, Dh, D, gb, mlp.fc2.weight, wfc2, dh_pre, epilogue=L.EPI_BF16_DGELU,
                       aux=dgl, ldaux=Dh)
-        if _wants(mlp.fc2.weight):
-            _linear_wgrad(gb, h, mlp.fc2.weight, rows)
         if _wants(mlp.fc2.bias):
             _colsum_of_grad(gout if gout.dtype == F32 else g, grad_buffer(mlp.fc2.bias), red)
-        grads_done(mlp.fc2.weight)
+        wgrad(mlp.fc1, dh_pre, xn2, Dh)
         dxn2 = _empty((rows, D), BF16, dev)
         _linear_dgrad(rows, D, Dh, dh_pre, mlp.fc1.weight, wfc1, dxn2)
-        if _wants(mlp.fc1.weight):
-            _linear_wgrad(dh_pre, xn2, mlp.fc1.weight, rows)
-        if _wants(mlp.fc1.bias):
-            red.add(ops.colsum_partial(dh_pre), grad_buffer(mlp.fc1.bias), Dh)
-        grads_done(mlp.fc1.weight)
         gmb = _empty((rows, D), BF16, dev)
         gsp = _ln_bwd(dxn2, xm, m2, r2, blk.norm2, rows, D, g2, gmb,
                       gsum=_wants(attn.proj.bias), batch=red)  # g2 := g_mid (in place)
         # ---- attention branch: x_mid = x_in + proj(attn(norm1(x_in)))
+        wgrad(attn.proj, gmb, o)
         do = _empty((rows, D), BF16, dev)
         _linear_dgrad(rows, D, D, gmb, attn.proj.weight, wproj, do)
-        if _wants(attn.proj.weight):
-            _linear_wgrad(gmb, o, attn.proj.weight, rows)
         if _wants(attn.proj.bias):
             red.add(gsp, grad_buffer(attn.proj.bias), D)
-        grads_done(attn.proj.weight)
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, T, H, dh, attn.scale)
+        wgrad(attn.qkv, dqkv, xn1, 3 * D)
         dxn1 = _empty((rows, D), BF16, dev)
         _linear_dgrad(rows, D, 3 * D, dqkv, attn.qkv.weight, wqkv, dxn1)
-        if _wants(attn.qkv.weight):
-            _linear_wgrad(dqkv, xn1, attn.qkv.weight, rows)
-        if _wants(attn.qkv.bias):
-            red.add(ops.colsum_partial(dqkv), grad_buffer(attn.qkv.bias), 3 * D)
-        grads_done(attn.qkv.weight)
         gib = _empty((B, T, D), BF16, dev)
         gsp = _ln_bwd(dxn1, x2, m1, r1, blk.norm1, rows, D, g2, gib.view(rows, D),
                       gsum=True, batch=red)  # g2 := g_in
         red.flush()
+        if red_w is not red:
+            bw.run(red_w.flush)
         grads_done(mlp.fc2.bias, mlp.fc1.bias, blk.norm2.weight, blk.norm2.bias,
                    attn.proj.bias, attn.qkv.bias, blk.norm1.weight, blk.norm1.bias)
         gin = g.view(B, T, D)

@@ -80,10 +80,11 @@ class MultimodalFusionModel(tnn.Module):
         main = torch.cuda.current_stream()
         side = Fn.side_stream(rgb.device)
         side.wait_stream(main)
-        with torch.cuda.stream(side):
-            thermal.record_stream(side)
-            th_feat = th_net(thermal)
-        rgb_feat = rgb_net(rgb)
+        with Fn.concurrent_encoders():
+            with torch.cuda.stream(side):
+                thermal.record_stream(side)
+                th_feat = th_net(thermal)
+            rgb_feat = rgb_net(rgb)
         main.wait_stream(side)
         th_feat.record_stream(main)
         return rgb_feat, th_feat
