@@ -127,6 +127,64 @@ __global__ __launch_bounds__(VPR * 16) void k_im2col_f32(
   }
 }
 
+// The same rows staged through LDS: one block per output row (b, oh) loads the C x R input rows
+// that row's windows touch (rows outside the image as zeros) with coalesced fp32 reads, then
+// writes the Q x Kp output row segment with 16-B stores.  A thread owns one 8-tap chunk kv of
+// the row (its taps' LDS row offsets and columns decoded once, kept in registers) and walks the
+// output positions ow = lane group, + 256 / VPR, ...; no division in either loop.  The gather
+// kernel above issues 8 scattered global reads per 16-B store and ran at ~1.3 TB/s of output.
+template <bool X3>
+__global__ __launch_bounds__(256) void k_im2col_lds(
+    const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int B, int C,
+    int H, int W, int R, int S, int stride, int pad, int P, int Q, int Kp,
+    bf16_t* __restrict__ out) {
+  extern __shared__ float tile[];  // [C * R][W]
+  const int KK = C * R * S;
+  const int VPR = Kp / 8;
+  const int groups = 256 / VPR;  // output positions in flight per block
+  const int kv = threadIdx.x % VPR, og = threadIdx.x / VPR;
+  int off[8], tsx[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = kv * 8 + e;
+    const int c = k / (R * S), rs = k - c * (R * S);
+    const int r = rs / S;
+    off[e] = k < KK ? (c * R + r) * W : -1;
+    tsx[e] = rs - r * S;
+  }
+  const int CR = C * R;
+  const int64_t ldo = X3 ? 3 * Kp : Kp;
+  for (int row = blockIdx.x; row < B * P; row += gridDim.x) {
+    const int b = row / P, oh = row - b * P;
+    __syncthreads();  // the previous row's gathers are done
+    const float* xb = x + b * sn;
+    for (int cr = 0; cr < CR; ++cr) {
+      const int c = cr / R, r = cr - c * R;
+      const int ih = oh * stride - pad + r;
+      const bool in = (unsigned)ih < (unsigned)H;
+      const float* src = xb + c * sc + (int64_t)(in ? ih : 0) * sh;
+      for (int iw = threadIdx.x; iw < W; iw += 256) tile[cr * W + iw] = in ? src[iw * sw] : 0.f;
+    }
+    __syncthreads();
+    if (og >= groups) continue;
+    bf16_t* orow = out + (int64_t)row * Q * ldo + kv * 8;
+    for (int ow = og; ow < Q; ow += groups) {
+      const int iw0 = ow * stride - pad;
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int iw = iw0 + tsx[e];
+        f[e] = (off[e] >= 0 && (unsigned)iw < (unsigned)W) ? tile[off[e] + iw] : 0.f;
+      }
+      if constexpr (X3) {
+        store_triple8(orow - kv * 8 + ow * ldo, Kp, kv * 8, f);
+      } else {
+        *(u32x4*)(orow + ow * ldo) = pack8(f);
+      }
+    }
+  }
+}
+
 template <bool X3 = false>
 __global__ void k_patchify_f32(const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh,
                                int64_t sw, int B, int C, int H, int W, int ps,
@@ -159,85 +217,95 @@ __global__ void k_patchify_f32(const float* __restrict__ x, int64_t sn, int64_t 
 }
 
 // ---------------------------------------------------------------- max / avg pooling
-// 3x3 / stride 2 / pad 1 (torchvision resnet maxpool); first max in row-major window order
-// wins, as ATen's max_pool2d_with_indices.
-__global__ void k_maxpool_fwd(const bf16_t* __restrict__ x, int B, int H, int W, int C,
-                              bf16_t* __restrict__ y, uint8_t* __restrict__ am, int P, int Q) {
+// 3x3 / stride 2 / pad 1 (torchvision resnet maxpool; first max in row-major window order wins,
+// as ATen's max_pool2d_with_indices) on one output row per blockIdx.y = (b, p): 32-bit index
+// math only (a grid-stride form decoding (b, p, q, c8) with 64-bit divisions per vector ran
+// 110 us on the stem's 64 x 112 x 112 x 64 input).  BN:
+// the input is the stem conv output y and every window element is first mapped to the value
+// k_bn_apply would have stored, bf16(relu(fma(y, scale, shift) + 0)) (bn.hip), so the pooled
+// output and argmax equal maxpool(bn_apply(y)) bit for bit without the BN output in HBM.
+template <bool BN>
+__global__ __launch_bounds__(256) void k_maxpool_rows(const bf16_t* __restrict__ x,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, int H,
+                                                      int W, int C, bf16_t* __restrict__ y,
+                                                      uint8_t* __restrict__ am, int P, int Q) {
   const int cv = C / 8;
-  const int64_t n = (int64_t)B * P * Q * cv;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % cv);
-    const int64_t pix = i / cv;
-    const int q = (int)(pix % Q);
-    const int64_t t = pix / Q;
-    const int p = (int)(t % P);
-    const int b = (int)(t / P);
-    float best[8];
-    int arg[8];
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= Q * cv) return;
+  const int b = blockIdx.y / P, p = blockIdx.y - b * P;
+  const int q = t / cv, c8 = t - q * cv;
+  float sc[8], sf[8];
+  if constexpr (BN) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
-    for (int wi = 0; wi < 3; ++wi) {
-      const int ih = 2 * p - 1 + wi;
-      if ((unsigned)ih >= (unsigned)H) continue;
-      for (int wj = 0; wj < 3; ++wj) {
-        const int iw = 2 * q - 1 + wj;
-        if ((unsigned)iw >= (unsigned)W) continue;
-        const u32x4 v = *(const u32x4*)(x + (((int64_t)b * H + ih) * W + iw) * C + c8 * 8);
-        float f[8];
-        unpack8(v, f);
+    for (int e = 0; e < 8; ++e) { sc[e] = scale[c8 * 8 + e]; sf[e] = shift[c8 * 8 + e]; }
+  }
+  float best[8];
+  int arg[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (f[e] > best[e] || (f[e] != f[e] && best[e] == best[e])) {
-            best[e] = f[e];
-            arg[e] = wi * 3 + wj;
-          }
+  for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+  const bf16_t* xb = x + (int64_t)b * H * W * C + c8 * 8;
+#pragma unroll
+  for (int wi = 0; wi < 3; ++wi) {
+    const int ih = 2 * p - 1 + wi;
+    if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+    for (int wj = 0; wj < 3; ++wj) {
+      const int iw = 2 * q - 1 + wj;
+      if ((unsigned)iw >= (unsigned)W) continue;
+      const u32x4 v = *(const u32x4*)(xb + (int64_t)(ih * W + iw) * C);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (BN) f[e] = bf2f(f2bf(fmaxf(fmaf(f[e], sc[e], sf[e]) + 0.f, 0.f)));
+        if (f[e] > best[e] || (f[e] != f[e] && best[e] == best[e])) {
+          best[e] = f[e];
+          arg[e] = wi * 3 + wj;
+        }
       }
     }
-    *(u32x4*)(y + pix * C + c8 * 8) = pack8(best);
-    uint64_t packed = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) packed |= (uint64_t)arg[e] << (8 * e);
-    *(uint64_t*)(am + pix * C + c8 * 8) = packed;
   }
+  const int64_t o = ((int64_t)blockIdx.y * Q + q) * C + c8 * 8;
+  *(u32x4*)(y + o) = pack8(best);
+  uint64_t packed = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) packed |= (uint64_t)arg[e] << (8 * e);
+  *(uint64_t*)(am + o) = packed;
 }
 
-// Gather form (deterministic): every input pixel sums dy of the windows whose argmax it is.
-__global__ void k_maxpool_bwd(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ am,
-                              int B, int H, int W, int C, int P, int Q, bf16_t* __restrict__ dx) {
+// Backward, one input row per blockIdx.y = (b, h): every input pixel gathers dy of the (at most
+// 2 x 2) windows whose argmax it is (deterministic: the windows in row-major order).
+__global__ __launch_bounds__(256) void k_maxpool_bwd_rows(const bf16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ am, int H,
+                                                          int W, int C, int P, int Q,
+                                                          bf16_t* __restrict__ dx) {
   const int cv = C / 8;
-  const int64_t n = (int64_t)B * H * W * cv;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % cv);
-    const int64_t pix = i / cv;
-    const int w = (int)(pix % W);
-    const int64_t t = pix / W;
-    const int h = (int)(t % H);
-    const int b = (int)(t / H);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // windows p with 2p-1 <= h <= 2p+1
-    const int p_lo = max(0, h / 2), p_hi = min(P - 1, (h + 1) / 2);
-    const int q_lo = max(0, w / 2), q_hi = min(Q - 1, (w + 1) / 2);
-    for (int p = p_lo; p <= p_hi; ++p) {
-      const int wi = h - (2 * p - 1);
-      if (wi < 0 || wi > 2) continue;
-      for (int q = q_lo; q <= q_hi; ++q) {
-        const int wj = w - (2 * q - 1);
-        if (wj < 0 || wj > 2) continue;
-        const int64_t o = (((int64_t)b * P + p) * Q + q) * C + c8 * 8;
-        const uint64_t a = *(const uint64_t*)(am + o);
-        const u32x4 g = *(const u32x4*)(dy + o);
-        float f[8];
-        unpack8(g, f);
-        const int want = wi * 3 + wj;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= W * cv) return;
+  const int b = blockIdx.y / H, h = blockIdx.y - b * H;
+  const int w = t / cv, c8 = t - w * cv;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int p_lo = h / 2, p_hi = min(P - 1, (h + 1) / 2);
+  const int q_lo = w / 2, q_hi = min(Q - 1, (w + 1) / 2);
+  for (int p = p_lo; p <= p_hi; ++p) {
+    const int wi = h - (2 * p - 1);
+    if (wi < 0 || wi > 2) continue;
+    for (int q = q_lo; q <= q_hi; ++q) {
+      const int wj = w - (2 * q - 1);
+      if (wj < 0 || wj > 2) continue;
+      const int64_t o = (((int64_t)b * P + p) * Q + q) * C + c8 * 8;
+      const uint64_t a = *(const uint64_t*)(am + o);
+      const u32x4 g = *(const u32x4*)(dy + o);
+      float f[8];
+      unpack8(g, f);
+      const int want = wi * 3 + wj;
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if ((int)((a >> (8 * e)) & 0xff) == want) acc[e] += f[e];
-      }
+      for (int e = 0; e < 8; ++e)
+        if ((int)((a >> (8 * e)) & 0xff) == want) acc[e] += f[e];
     }
-    *(u32x4*)(dx + pix * C + c8 * 8) = pack8(acc);
   }
+  *(u32x4*)(dx + ((int64_t)blockIdx.y * W + w) * C + c8 * 8) = pack8(acc);
 }
 
 __global__ void k_avgpool_fwd(const bf16_t* __restrict__ x, int B, int HW, int C,
@@ -689,6 +757,12 @@ extern "C" int dfu_cast_rows_f32(const void* in, int64_t ld_in, float* out, int6
   return DFU_OK;
 }
 
+// The LDS-staged kernel when the C x R input rows of one output row fit (the stem: 3 x 7 x 224
+// fp32 = 18.4 KiB); the per-chunk gather otherwise.
+static bool im2col_lds_fits(int C, int R, int W, int Kp) {
+  return Kp <= 256 * 8 / 2 && (int64_t)C * R * W * 4 <= 48 * 1024;
+}
+
 extern "C" int dfu_im2col_f32(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
                               int32_t B, int32_t C, int32_t H, int32_t W, int32_t R, int32_t S,
                               int32_t stride, int32_t pad, int32_t P, int32_t Q, void* out,
@@ -697,8 +771,14 @@ extern "C" int dfu_im2col_f32(const float* x, int64_t sn, int64_t sc, int64_t sh
   DFU_CHECK_ARG(((uintptr_t)out & 15) == 0, "dfu_im2col_f32: out must be 16-B aligned");
   const int64_t rows = (int64_t)B * P * Q;
   DFU_CHECK_ARG(rows < (1ll << 31), "dfu_im2col_f32: too many rows");
-  const int blocks = (int)((rows + 15) / 16 < 8192 ? (rows + 15) / 16 : 8192);
   hipStream_t st = (hipStream_t)stream;
+  if (im2col_lds_fits(C, R, W, Kp)) {
+    hipLaunchKernelGGL(k_im2col_lds<false>, dim3(B * P), dim3(256), (size_t)C * R * W * 4, st, x,
+                       sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q, Kp, (bf16_t*)out);
+    DFU_LAUNCH_CHECK();
+    return DFU_OK;
+  }
+  const int blocks = (int)((rows + 15) / 16 < 8192 ? (rows + 15) / 16 : 8192);
   switch (Kp) {
     case 160:
       hipLaunchKernelGGL(k_im2col_f32<20>, dim3(blocks), dim3(320), 0, st, x, sn, sc, sh, sw, B,
@@ -730,6 +810,13 @@ extern "C" int dfu_im2col_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t
   DFU_CHECK_ARG(((uintptr_t)out & 15) == 0, "dfu_im2col_f32_x3: out must be 16-B aligned");
   const int64_t rows = (int64_t)B * P * Q;
   DFU_CHECK_ARG(rows < (1ll << 31), "dfu_im2col_f32_x3: too many rows");
+  if (im2col_lds_fits(C, R, W, Kp)) {
+    hipLaunchKernelGGL(k_im2col_lds<true>, dim3(B * P), dim3(256), (size_t)C * R * W * 4,
+                       (hipStream_t)stream, x, sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q,
+                       Kp, (bf16_t*)out);
+    DFU_LAUNCH_CHECK();
+    return DFU_OK;
+  }
   const int blocks = (int)((rows + 15) / 16 < 8192 ? (rows + 15) / 16 : 8192);
   hipLaunchKernelGGL((k_im2col_f32<20, true>), dim3(blocks), dim3(320), 0, (hipStream_t)stream,
                      x, sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q, (bf16_t*)out);
@@ -749,10 +836,21 @@ extern "C" int dfu_patchify_f32_x3(const float* x, int64_t sn, int64_t sc, int64
 
 extern "C" int dfu_maxpool_fwd(const void* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y,
                                uint8_t* argmax, int32_t P, int32_t Q, void* stream) {
+  return dfu_maxpool_bn_fwd(x, nullptr, nullptr, B, H, W, C, y, argmax, P, Q, stream);
+}
+
+extern "C" int dfu_maxpool_bn_fwd(const void* x, const float* scale, const float* shift, int32_t B,
+                                  int32_t H, int32_t W, int32_t C, void* y, uint8_t* argmax,
+                                  int32_t P, int32_t Q, void* stream) {
   DFU_CHECK_ARG(x && y && argmax && C % 8 == 0, "dfu_maxpool_fwd: C %% 8 != 0");
   DFU_CHECK_ARG(P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1, "dfu_maxpool_fwd: bad P/Q");
-  LAUNCH(k_maxpool_fwd, (int64_t)B * P * Q * (C / 8), stream, (const bf16_t*)x, B, H, W, C,
-         (bf16_t*)y, argmax, P, Q);
+  DFU_CHECK_ARG((scale == nullptr) == (shift == nullptr), "dfu_maxpool_bn_fwd: scale and shift");
+  DFU_CHECK_ARG((int64_t)B * P < 65536 && Q * (C / 8) < (1 << 24), "dfu_maxpool_fwd: size");
+  const dim3 grid((Q * (C / 8) + 255) / 256, B * P);
+  hipLaunchKernelGGL(scale ? k_maxpool_rows<true> : k_maxpool_rows<false>, grid, dim3(256), 0,
+                     (hipStream_t)stream, (const bf16_t*)x, scale, shift, H, W, C, (bf16_t*)y,
+                     argmax, P, Q);
+  DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
 
@@ -760,8 +858,11 @@ extern "C" int dfu_maxpool_bwd(const void* dy, const uint8_t* argmax, int32_t B,
                                int32_t W, int32_t C, int32_t P, int32_t Q, void* dx,
                                void* stream) {
   DFU_CHECK_ARG(dy && dx && argmax && C % 8 == 0, "dfu_maxpool_bwd: C %% 8 != 0");
-  LAUNCH(k_maxpool_bwd, (int64_t)B * H * W * (C / 8), stream, (const bf16_t*)dy, argmax, B, H, W,
-         C, P, Q, (bf16_t*)dx);
+  DFU_CHECK_ARG((int64_t)B * H < 65536 && W * (C / 8) < (1 << 24), "dfu_maxpool_bwd: size");
+  const dim3 grid((W * (C / 8) + 255) / 256, B * H);
+  hipLaunchKernelGGL(k_maxpool_bwd_rows, grid, dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, argmax, H, W, C, P, Q, (bf16_t*)dx);
+  DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
 

@@ -469,9 +469,9 @@ class StemFn(torch.autograd.Function):
         M = B * P * Q
         y = _empty((M, Cout), BF16, x.device)
         stats = _empty((ops.stats_tiles(M), 2, Cout), F32, x.device)
-        a = _empty((M, Cout), BF16, x.device)
         bns = _BN(bn, M, Cout, x.device)
         if x3:
+            a = _empty((M, Cout), BF16, x.device)
             yf = _empty((M, Cout), F32, x.device)
             ops.gemm(M, Cout, 3 * Kp, col, 3 * Kp, weight_x3_rows(w, seg=Kp), 3 * Kp, yf, Cout,
                      epilogue=L.EPI_F32_STATS, stats=stats)
@@ -484,8 +484,11 @@ class StemFn(torch.autograd.Function):
             ops.gemm(M, Cout, Kp, col, Kp, wb, Kp, y, Cout, epilogue=L.EPI_BF16_STATS,
                      stats=stats)
             bns.forward_coeffs(stats)
-            ops.bn_apply(y, bns.scale, bns.shift, None, True, a, M, Cout)
-            out, am, P2, Q2 = ops.maxpool_fwd(a, B, P, Q, Cout)
+            # bn1 + relu applied inside the pool (the backward recomputes the ReLU mask from
+            # y, so the BN output itself is never stored)
+            a = None
+            out, am, P2, Q2 = ops.maxpool_fwd(y, B, P, Q, Cout, scale=bns.scale,
+                                              shift=bns.shift)
         ctx.mod = mod
         ctx.bns = bns
         ctx.x3 = x3

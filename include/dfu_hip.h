@@ -244,6 +244,16 @@ int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t M, int32_t
                         int32_t ncounters, void* stream);
 /* Workspace of dfu_bn_bwd_finalize's sliced form (as dfu_bn_finalize's). */
 int64_t dfu_bn_bwd_finalize_ws_bytes(int32_t blocks, int32_t C);
+/* reduce + finalize in one launch: dfu_bn_bwd_reduce's partial sums, combined by last-arriving
+ * workgroups in a fixed order (no second launch); same outputs as dfu_bn_bwd_finalize.  ws:
+ * dfu_bn_bwd_reduce_fin_ws_bytes(M, C) bytes, 8-B aligned; counters: zeroed int32 (returned
+ * zeroed), at least (C/8/min(C/8,64)) * (slices+1), checked. */
+int64_t dfu_bn_bwd_reduce_fin_ws_bytes(int64_t M, int32_t C);
+int dfu_bn_bwd_reduce_fin(const void* dout, const void* y, const void* out, int32_t relu,
+                          const float* scale, const float* shift, const float* mean,
+                          const float* invstd, int64_t M, int32_t C, const float* gamma,
+                          int32_t batch_stats, float* dgamma, float* dbeta, float* coef, void* ws,
+                          int32_t* counters, int32_t ncounters, void* stream);
 /* dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); optionally dres = g (bf16). */
 int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t relu,
                      const float* scale, const float* shift, const float* mean,
@@ -254,6 +264,13 @@ int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t r
 /* resnet maxpool 3x3/s2/p1 on NHWC bf16; argmax (0..8 window index) saved as uint8. */
 int dfu_maxpool_fwd(const void* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y,
                     uint8_t* argmax, int32_t P, int32_t Q, void* stream);
+/* The stem's bn1 + relu + maxpool in one pass (resnet.py: maxpool(relu(bn1(conv1 x))))): x is
+ * the conv output y, each window element is bf16(relu(y * scale + shift)) exactly as
+ * dfu_bn_apply(relu=1) stores it, so y/argmax equal dfu_bn_apply followed by dfu_maxpool_fwd
+ * bit for bit.  scale = shift = NULL is dfu_maxpool_fwd. */
+int dfu_maxpool_bn_fwd(const void* x, const float* scale, const float* shift, int32_t B,
+                       int32_t H, int32_t W, int32_t C, void* y, uint8_t* argmax, int32_t P,
+                       int32_t Q, void* stream);
 int dfu_maxpool_bwd(const void* dy, const uint8_t* argmax, int32_t B, int32_t H, int32_t W,
                     int32_t C, int32_t P, int32_t Q, void* dx, void* stream);
 /* resnet AdaptiveAvgPool2d(1) + flatten: NHWC bf16 [B][HW][C] -> fp32 [B][C]. */

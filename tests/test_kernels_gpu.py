@@ -347,6 +347,41 @@ def test_batchnorm_bwd_mask_from_y_is_bitwise(M, C):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("M,C,relu", [(5000, 128, 1), (3136, 2048, 1), (12544, 1024, 0),
+                                      (200704, 64, 2), (37, 256, 2), (50176, 512, 1)])
+def test_batchnorm_bwd_fused_finalize_matches_three_launches(M, C, relu, monkeypatch):
+    """dfu_bn_bwd_reduce_fin (finalize by last-arriving workgroups inside the reduce launch)
+    against reduce -> finalize -> apply: dy and dres bitwise, dgamma/dbeta and the coefficients
+    to fp64-summation-order rounding; twice in a row (the counters come back zeroed)."""
+    Y = rnd(M, C, seed=54, scale=2.0)
+    gamma = rnd(C, dtype=torch.float32, seed=55) * 0.5 + 1
+    mean = Y.float().mean(0)
+    invstd = torch.rsqrt(Y.float().var(0, unbiased=False) + 1e-5)
+    scale, shift = gamma * invstd, -mean * gamma * invstd
+    out = torch.relu(Y.float() * scale + shift).to(torch.bfloat16) if relu == 1 else None
+    dout = rnd(M, C, seed=56)
+    res = []
+    for fused in (False, True, True):
+        monkeypatch.setattr(ops, "BN_BWD_FUSED_FINALIZE", fused)
+        dy = torch.empty_like(Y)
+        dres = torch.empty_like(Y) if relu == 1 else None
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        ops.bn_bwd(dout, Y, out, relu, mean, invstd, gamma, M, C, dy, dres, dg, db,
+                   scale=scale, shift=shift)
+        res.append((dy, dres, dg, db))
+    assert int(ops.tile_counters(torch.device(DEV)).abs().sum().item()) == 0, "counters not zeroed"
+    ref = res[0]
+    for got in res[1:]:
+        # the coefficients differ at most in their last bits (fp64 sums in another order), so
+        # dy to one bf16 ulp; the masked gradient dres is exact
+        close(got[0], ref[0], atol=1e-2, rtol=8e-3, what="bn dy fused finalize")
+        if relu == 1:
+            assert torch.equal(got[1], ref[1])
+        close(got[2], ref[2], atol=1e-3, rtol=1e-5, what="dgamma fused finalize")
+        close(got[3], ref[3], atol=1e-3, rtol=1e-5, what="dbeta fused finalize")
+    assert torch.equal(res[1][0], res[2][0]) and torch.equal(res[1][2], res[2][2]), "deterministic"
+
+
 def test_layernorm_fwd_bwd():
     rows, D = 1000, 768
     x = (torch.randn(rows, D, device=DEV) * 3 + 1).float()
@@ -392,6 +427,24 @@ def test_pooling_and_layout():
     ref.backward(dy.float())
     dx = ops.maxpool_bwd(_nhwc(dy), am, B, H, W, C, P, Q)
     close(dx, _nhwc(xr.grad), atol=2e-2, rtol=1e-2, what="maxpool bwd")
+    # the stem's fused bn1 + relu + maxpool == bn_apply(relu) then maxpool, bit for bit (odd
+    # sizes too: windows clipped at both borders)
+    for (Bb, Hh, Ww) in ((2, 112, 112), (3, 57, 61)):
+        yb = rnd(Bb * Hh * Ww, C, seed=63)
+        sc = torch.randn(C, device=DEV)
+        sh = torch.randn(C, device=DEV)
+        ab = torch.empty_like(yb)
+        ops.bn_apply(yb, sc, sh, None, True, ab, Bb * Hh * Ww, C)
+        y0, am0, P0, Q0 = ops.maxpool_fwd(ab, Bb, Hh, Ww, C)
+        y1, am1, _, _ = ops.maxpool_fwd(yb, Bb, Hh, Ww, C, scale=sc, shift=sh)
+        assert torch.equal(y0, y1) and torch.equal(am0, am1), "maxpool_bn_fwd"
+        ref = F.max_pool2d(ab.view(Bb, Hh, Ww, C).permute(0, 3, 1, 2).float(), 3, 2, 1)
+        close(y1, _nhwc(ref), atol=0, what="maxpool_bn_fwd vs torch")
+        g = rnd(Bb, C, P0, Q0, seed=64)
+        ar = ab.view(Bb, Hh, Ww, C).permute(0, 3, 1, 2).float().requires_grad_(True)
+        F.max_pool2d(ar, 3, 2, 1).backward(g.float())
+        dxo = ops.maxpool_bwd(_nhwc(g), am1, Bb, Hh, Ww, C, P0, Q0)
+        close(dxo, _nhwc(ar.grad), atol=2e-2, rtol=1e-2, what="maxpool bwd (odd)")
     # avgpool
     x4 = rnd(B, 7, 7, 2048, seed=62)
     yf = ops.avgpool_fwd(x4, B, 49, 2048)
@@ -407,6 +460,11 @@ def test_pooling_and_layout():
         ref = F.unfold(xin, 7, padding=3, stride=2).transpose(1, 2).reshape(-1, 147)
         assert torch.equal(col[:, :147].float(), ref.to(torch.bfloat16).float()), "im2col"
         assert col[:, 147:].abs().max().item() == 0
+        # the bf16x3 triple [hi | lo | hi]: hi == the bf16 col, hi + lo == the fp32 unfold
+        c3, _, _ = ops.im2col_f32_x3(xin, 7, 7, 2, 3, 160)
+        assert torch.equal(c3[:, :160], col) and torch.equal(c3[:, 320:], col), "im2col x3 hi"
+        rec = c3[:, :147].float() + c3[:, 160:307].float()
+        close(rec, ref, atol=1e-6, rtol=1e-5, what="im2col x3 hi + lo")
     pt = ops.patchify_f32(xi, 16)
     ref = F.unfold(xi, 16, stride=16).transpose(1, 2).reshape(-1, 768)
     close(pt, ref, atol=2e-2, rtol=1e-2, what="patchify")
