@@ -271,161 +271,6 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
   }
 }
 
-// dfu_bn_bwd_reduce_fin: k_bn_bwd_reduce's row-block partials, then the finalize inside the same
-// launch by last arrivers (no separate k_bn_bwd_finalize launch): the row-blocks of a channel
-// group form slices of SL; the last block of a slice to arrive (agent-scope acq_rel counter:
-// last_arrive below) sums its slice's partials in
-// row-block order in fp64 and publishes the slice record; the last slice of the group sums the
-// records in slice order and writes dgamma/dbeta and the apply coefficients.  The sums do not
-// depend on the arrival order; every counter is returned to zero.
-// Release/acquire hand-off (MI355X_MICROARCH.md correctness table: stores drained, workgroup
-// barrier, agent-scope release on the counter; the last arriver's agent-scope acquire, barrier,
-// then plain loads): the records are written and read with ordinary vector accesses, so the
-// last arriver's loads go out back to back instead of one write-through load at a time.
-DFU_DEV bool last_arrive(int* counter, int n, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == n - 1;
-    if (last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-DFU_DEV void bwd_coef_out(int c, double sg, double sgx, int64_t M, const float* gamma,
-                          const float* invstd, int batch_stats, float* dgamma, float* dbeta,
-                          float* coef) {
-  if (dbeta) dbeta[c] += (float)sg;
-  if (dgamma) dgamma[c] += (float)sgx;
-  const float g = gamma ? gamma[c] : 1.f;
-  coef[3 * c + 0] = g * invstd[c];
-  coef[3 * c + 1] = batch_stats ? (float)(sg / (double)M) : 0.f;
-  coef[3 * c + 2] = batch_stats ? (float)(sgx / (double)M) : 0.f;
-}
-
-template <int RELU>
-__global__ __launch_bounds__(256) void k_bn_bwd_reduce_fin(
-    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ y, const bf16_t* __restrict__ out,
-    const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ mean, const float* __restrict__ invstd, int64_t M, int C,
-    int rows_per_block, int SL, float* __restrict__ partial, double* __restrict__ ws,
-    int* __restrict__ counters, const float* __restrict__ gamma, int batch_stats,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef) {
-  __shared__ float red[2][256][8];
-  __shared__ int flag;
-  const int cv = C / 8;
-  const int ct_n = min(cv, 64);
-  const int rl_n = 256 / ct_n;
-  const int ct = threadIdx.x % ct_n, rl = threadIdx.x / ct_n;
-  const int c0 = (blockIdx.x * ct_n + ct) * 8;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
-  const int64_t r1 = min(M, r0 + rows_per_block);
-  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float mu[8], is[8], sc[8] = {}, sf[8] = {};
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e]; }
-  if constexpr (RELU == 2) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; }
-  }
-  for (int64_t rb = r0 + rl; rb < r1; rb += (int64_t)rl_n * RED_U) {
-    u32x4 gv[RED_U], yv[RED_U], ov[RED_U];
-#pragma unroll
-    for (int u = 0; u < RED_U; ++u) {
-      const int64_t r = rb + (int64_t)u * rl_n;
-      const int64_t o = (r < r1 ? r : r0) * C + c0;
-      gv[u] = *(const u32x4*)(dout + o);
-      yv[u] = *(const u32x4*)(y + o);
-      ov[u] = (u32x4){0u, 0u, 0u, 0u};
-      if constexpr (RELU == 1) ov[u] = *(const u32x4*)(out + o);
-    }
-#pragma unroll
-    for (int u = 0; u < RED_U; ++u) {
-      if (rb + (int64_t)u * rl_n >= r1) continue;
-      float g[8], yy[8], oo[8];
-      unpack8(gv[u], g);
-      unpack8(yv[u], yy);
-      unpack8(ov[u], oo);
-      relu_mask8<RELU>(oo, yy, sc, sf, g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sg[e] += g[e];
-        sgx[e] += g[e] * (yy[e] - mu[e]) * is[e];
-      }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { red[0][threadIdx.x][e] = sg[e]; red[1][threadIdx.x][e] = sgx[e]; }
-  __syncthreads();
-  if (rl == 0) {
-    for (int l = 1; l < rl_n; ++l) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sg[e] += red[0][l * ct_n + ct][e];
-        sgx[e] += red[1][l * ct_n + ct][e];
-      }
-    }
-    float* p0 = partial + ((int64_t)blockIdx.y * 2 + 0) * C + c0;
-    float* p1 = partial + ((int64_t)blockIdx.y * 2 + 1) * C + c0;
-    *(f32x4*)p0 = (f32x4){sg[0], sg[1], sg[2], sg[3]};
-    *(f32x4*)(p0 + 4) = (f32x4){sg[4], sg[5], sg[6], sg[7]};
-    *(f32x4*)p1 = (f32x4){sgx[0], sgx[1], sgx[2], sgx[3]};
-    *(f32x4*)(p1 + 4) = (f32x4){sgx[4], sgx[5], sgx[6], sgx[7]};
-  }
-  // ---- slice level: the last row-block of slice s sums the slice's partials
-  const int RB = gridDim.y;
-  const int NS = (RB + SL - 1) / SL;
-  const int s = blockIdx.y / SL;
-  const int b0 = s * SL, b1 = min(RB, b0 + SL);
-  int* cnt = counters + blockIdx.x * (NS + 1);
-  if (!last_arrive(cnt + s, b1 - b0, &flag)) return;
-  const int CW = ct_n * 8;  // channels of this group
-  const int cg0 = blockIdx.x * CW;
-  double a0[2] = {0.0, 0.0}, a1[2] = {0.0, 0.0};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int cw = threadIdx.x + 256 * h;
-    if (cw >= CW) continue;
-    const int c = cg0 + cw;
-#pragma unroll 8
-    for (int b = b0; b < b1; ++b) {
-      a0[h] += (double)partial[((int64_t)b * 2 + 0) * C + c];
-      a1[h] += (double)partial[((int64_t)b * 2 + 1) * C + c];
-    }
-  }
-  if (NS > 1) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cw = threadIdx.x + 256 * h;
-      if (cw >= CW) continue;
-      ws[((int64_t)s * 2 + 0) * C + cg0 + cw] = a0[h];
-      ws[((int64_t)s * 2 + 1) * C + cg0 + cw] = a1[h];
-    }
-    // ---- group level: the last slice sums the slice records in slice order
-    if (!last_arrive(cnt + NS, NS, &flag)) return;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cw = threadIdx.x + 256 * h;
-      if (cw >= CW) continue;
-      a0[h] = a1[h] = 0.0;
-#pragma unroll 8
-      for (int t = 0; t < NS; ++t) {
-        a0[h] += ws[((int64_t)t * 2 + 0) * C + cg0 + cw];
-        a1[h] += ws[((int64_t)t * 2 + 1) * C + cg0 + cw];
-      }
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int cw = threadIdx.x + 256 * h;
-    if (cw < CW)
-      bwd_coef_out(cg0 + cw, a0[h], a1[h], M, gamma, invstd, batch_stats, dgamma, dbeta, coef);
-  }
-}
-
 // 16 waves x 64 channel-lanes per workgroup (coalesced 256-B row segments of the partials, the
 // waves stride the row-blocks); fp64 sums, 16-way LDS reduction.
 // Slices over the row-blocks as k_bn_finalize (blockIdx.y, last arriver sums in slice order).
@@ -609,58 +454,6 @@ extern "C" int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* ou
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dout,
                      (const bf16_t*)y, (const bf16_t*)out, scale, shift, mean, invstd, M, C, rpb,
                      partial);
-  DFU_LAUNCH_CHECK();
-  return DFU_OK;
-}
-
-namespace {
-// slice length of dfu_bn_bwd_reduce_fin: ~sqrt(row-blocks), so both last-arriver levels read a
-// similar number of records
-inline int bwd_fin_slice(int blocks) {
-  int sl = 1;
-  while (sl * sl < blocks) ++sl;
-  return sl;
-}
-}  // namespace
-
-extern "C" int64_t dfu_bn_bwd_reduce_fin_ws_bytes(int64_t M, int32_t C) {
-  const int blocks = dfu_bn_bwd_blocks(M, C);
-  const int sl = bwd_fin_slice(blocks);
-  const int ns = (blocks + sl - 1) / sl;
-  return (int64_t)blocks * 2 * C * 4 + (ns > 1 ? (int64_t)ns * 2 * C * 8 : 0);
-}
-
-extern "C" int dfu_bn_bwd_reduce_fin(const void* dout, const void* y, const void* out, int32_t relu,
-                                     const float* scale, const float* shift, const float* mean,
-                                     const float* invstd, int64_t M, int32_t C,
-                                     const float* gamma, int32_t batch_stats, float* dgamma,
-                                     float* dbeta, float* coef, void* ws, int32_t* counters,
-                                     int32_t ncounters, void* stream) {
-  DFU_CHECK_ARG(dout && y && mean && invstd && coef && ws && counters && C % 8 == 0 && M > 0 &&
-                    relu >= 0 && relu <= 2,
-                "dfu_bn_bwd_reduce_fin: bad args");
-  DFU_CHECK_ARG(relu != 1 || out, "dfu_bn_bwd_reduce_fin: relu=1 needs out");
-  DFU_CHECK_ARG(relu != 2 || (scale && shift), "dfu_bn_bwd_reduce_fin: relu=2 needs scale/shift");
-  DFU_CHECK_ARG(((uintptr_t)ws & 7) == 0, "dfu_bn_bwd_reduce_fin: ws must be 8-B aligned");
-  const int cv = C / 8;
-  const int ct_n = cv < 64 ? cv : 64;
-  DFU_CHECK_ARG(256 % ct_n == 0 && cv % ct_n == 0, "dfu_bn_bwd_reduce_fin: C=%d unsupported", C);
-  const int rpb = bwd_rows_per_block(M, C);
-  const int blocks = dfu_bn_bwd_blocks(M, C);
-  const int sl = bwd_fin_slice(blocks);
-  const int ns = (blocks + sl - 1) / sl;
-  const int groups = cv / ct_n;
-  DFU_CHECK_ARG(groups * (ns + 1) <= ncounters, "dfu_bn_bwd_reduce_fin: %d counters needed",
-                groups * (ns + 1));
-  float* partial = (float*)ws;
-  double* recs = (double*)((char*)ws + (int64_t)blocks * 2 * C * 4);
-  auto kern = relu == 1   ? k_bn_bwd_reduce_fin<1>
-              : relu == 2 ? k_bn_bwd_reduce_fin<2>
-                          : k_bn_bwd_reduce_fin<0>;
-  hipLaunchKernelGGL(kern, dim3(groups, blocks), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, scale, shift, mean,
-                     invstd, M, C, rpb, sl, partial, recs, counters, gamma, batch_stats, dgamma,
-                     dbeta, coef);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

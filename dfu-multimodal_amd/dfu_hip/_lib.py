@@ -80,6 +80,7 @@ PROTOTYPES = {
     "dfu_gemm_set_persistent": [I32],
     "dfu_gemm_set_inkernel_reduce": [I32],
     "dfu_gemm_set_tail_split": [I32],
+    "dfu_gemm_set_stream_k": [I32],
     "dfu_gemm_f32": [I32, I32, I32, P, I64, I64, P, I64, I64, P, I64, P, I32, I32, P, I64, P],
     "dfu_gemm_f32_workspace_bytes": [I32, I32, I32],
     "dfu_pack_conv_weight": [P, P, I32, I32, I32, I32, P],
@@ -100,8 +101,6 @@ PROTOTYPES = {
     "dfu_bn_apply": [P, P, P, P, I32, P, I64, I32, P],
     "dfu_bn_bwd_blocks": [I64, I32],
     "dfu_bn_bwd_reduce": [P, P, P, I32, P, P, P, P, I64, I32, P, P],
-    "dfu_bn_bwd_reduce_fin_ws_bytes": [I64, I32],
-    "dfu_bn_bwd_reduce_fin": [P, P, P, I32, P, P, P, P, I64, I32, P, I32, P, P, P, P, P, I32, P],
     "dfu_bn_bwd_finalize": [P, I32, I64, I32, P, P, I32, P, P, P, P, P, I32, P],
     "dfu_bn_bwd_apply": [P, P, P, I32, P, P, P, P, P, I64, I32, P, P, P],
     "dfu_maxpool_fwd": [P, I32, I32, I32, I32, P, P, I32, I32, P],
@@ -153,7 +152,7 @@ PROTOTYPES = {
 }
 _RESTYPE = {"dfu_last_error_string": c_char_p, "dfu_gemm_workspace_bytes": c_int64,
             "dfu_gemm_f32_workspace_bytes": c_int64, "dfu_bn_finalize_ws_bytes": c_int64,
-            "dfu_bn_bwd_finalize_ws_bytes": c_int64, "dfu_bn_bwd_reduce_fin_ws_bytes": c_int64}
+            "dfu_bn_bwd_finalize_ws_bytes": c_int64}
 
 
 def header_symbols(path=HEADER_PATH):

@@ -5,7 +5,6 @@ current HIP stream, and raises DfuError on any non-zero return code.  Nothing he
 except where an output is documented as returned; nothing synchronises.
 """
 import ctypes
-import os
 
 import torch
 
@@ -149,6 +148,11 @@ def tile_counters(device):
 def gemm_set_tail_split(enable):
     """Tail split of the last partial round of tiles along K (dfu_gemm_set_tail_split)."""
     return int(lib().dfu_gemm_set_tail_split(int(bool(enable))))
+
+
+def gemm_set_stream_k(enable):
+    """Stream-K tail of the persistent phased 256x256 tile (dfu_gemm_set_stream_k)."""
+    return int(lib().dfu_gemm_set_stream_k(int(bool(enable))))
 
 
 def gemm_set_inkernel_reduce(enable):
@@ -394,11 +398,6 @@ def bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C
           "dfu_bn_bwd_apply")
 
 
-# BN backward reduce with its finalize folded in (dfu_bn_bwd_reduce_fin: one launch fewer per
-# BN layer); DFU_BN_BWD_FUSED_FINALIZE=0 restores reduce -> finalize -> apply.
-BN_BWD_FUSED_FINALIZE = os.environ.get("DFU_BN_BWD_FUSED_FINALIZE", "1") != "0"
-
-
 def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta,
            batch_stats=True, scale=None, shift=None):
     """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply.  relu: False/0 none;
@@ -407,28 +406,13 @@ def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbet
     relu = int(relu)
     if relu == 2 and (scale is None or shift is None):
         raise ValueError("bn_bwd: relu=2 needs the forward scale/shift")
-    if not BN_BWD_FUSED_FINALIZE:
-        blocks = lib().dfu_bn_bwd_blocks(M, C)
-        partial = torch.empty((blocks, 2, C), dtype=F32, device=y.device)
-        check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
-                                      ptr(mean), ptr(invstd), M, C, ptr(partial), stream_ptr()),
-              "dfu_bn_bwd_reduce")
-        bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres,
-                      dgamma, dbeta, batch_stats, scale, shift)
-        return
-    # reduce + finalize in one launch (last-arriver finalize), then apply
-    s = stream_ptr()
-    coef = torch.empty((C, 3), dtype=F32, device=y.device)
-    ws = torch.empty(lib().dfu_bn_bwd_reduce_fin_ws_bytes(M, C) // 8, dtype=torch.float64,
-                     device=y.device)
-    cnt = tile_counters(y.device)
-    check(lib().dfu_bn_bwd_reduce_fin(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
-                                      ptr(mean), ptr(invstd), M, C, ptr(gamma), int(batch_stats),
-                                      ptr(dgamma), ptr(dbeta), ptr(coef), ptr(ws), ptr(cnt),
-                                      cnt.numel(), s), "dfu_bn_bwd_reduce_fin")
-    check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
-                                 ptr(mean), ptr(invstd), ptr(coef), M, C, ptr(dy), ptr(dres), s),
-          "dfu_bn_bwd_apply")
+    blocks = lib().dfu_bn_bwd_blocks(M, C)
+    partial = torch.empty((blocks, 2, C), dtype=F32, device=y.device)
+    check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
+                                  ptr(mean), ptr(invstd), M, C, ptr(partial), stream_ptr()),
+          "dfu_bn_bwd_reduce")
+    bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres,
+                  dgamma, dbeta, batch_stats, scale, shift)
 
 
 # ------------------------------------------------------------------------------- pooling

@@ -128,6 +128,12 @@ int dfu_gemm_set_persistent(int32_t enable);
  * counters, 0 (default: measured faster) = the separate reduce kernel.  Bitwise-identical; returns the
  * previous setting. */
 int dfu_gemm_set_inkernel_reduce(int32_t enable);
+/* Stream-K tail of the persistent phased 256x256 (tile 8, non-accumulating epilogues): 1
+ * (default) = the tiles left over after the complete rounds are cut into an even K-step range
+ * per workgroup, split tiles finished by their last segment (needs the workspace and tile
+ * counters dfu_gemm_workspace_bytes asks for); 0 = a last round of whole tiles.  Returns the
+ * previous setting. */
+int dfu_gemm_set_stream_k(int32_t enable);
 /* Tail-split switch: 1 (default) = when the tiles of an unsplit launch leave a last, partial
  * round of workgroups, split each of those tiles along K over the idle workgroups (fp32 slabs
  * in the descriptor's workspace, dfu_gemm_workspace_bytes; the tile's last split to finish sums
@@ -244,16 +250,6 @@ int dfu_bn_bwd_finalize(const float* partial, int32_t blocks, int64_t M, int32_t
                         int32_t ncounters, void* stream);
 /* Workspace of dfu_bn_bwd_finalize's sliced form (as dfu_bn_finalize's). */
 int64_t dfu_bn_bwd_finalize_ws_bytes(int32_t blocks, int32_t C);
-/* reduce + finalize in one launch: dfu_bn_bwd_reduce's partial sums, combined by last-arriving
- * workgroups in a fixed order (no second launch); same outputs as dfu_bn_bwd_finalize.  ws:
- * dfu_bn_bwd_reduce_fin_ws_bytes(M, C) bytes, 8-B aligned; counters: zeroed int32 (returned
- * zeroed), at least (C/8/min(C/8,64)) * (slices+1), checked. */
-int64_t dfu_bn_bwd_reduce_fin_ws_bytes(int64_t M, int32_t C);
-int dfu_bn_bwd_reduce_fin(const void* dout, const void* y, const void* out, int32_t relu,
-                          const float* scale, const float* shift, const float* mean,
-                          const float* invstd, int64_t M, int32_t C, const float* gamma,
-                          int32_t batch_stats, float* dgamma, float* dbeta, float* coef, void* ws,
-                          int32_t* counters, int32_t ncounters, void* stream);
 /* dy = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)); optionally dres = g (bf16). */
 int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t relu,
                      const float* scale, const float* shift, const float* mean,
