@@ -247,31 +247,6 @@ Tail tail_plan(int tiles, int slots, int ktiles, int tm, int tn, double step_us)
   return best;
 }
 
-// Stream-K tail of the persistent phased 256x256 (GemmArgs::sk_tiles): the R = tiles mod
-// slots tiles left after the complete rounds become one range of R x ktiles K-steps cut evenly
-// over every slot, instead of a last round of R whole tiles with slots - R workgroups idle.
-// Each split tile costs a 256 KiB fp32 slab store per segment and their read-back by the last
-// one (~2.5 K-steps, as the tail split's hand-off); taken when it saves >= 5% of the K-steps.
-int g_stream_k = getenv("DFU_GEMM_STREAM_K") ? atoi(getenv("DFU_GEMM_STREAM_K")) : 1;
-constexpr double kSkFixupSteps = 2.5;
-constexpr int64_t kSkSlotBytes = 256 * 256 * 4;  // one workgroup's fp32 accumulators
-
-int sk_plan(int tiles, int slots, int ktiles) {
-  if (!g_stream_k || !g_persistent) return 0;
-  const int R = tiles % slots;
-  if (R == 0 || (int64_t)R * ktiles < slots) return 0;
-  const int full = tiles / slots;
-  const double old_steps = (double)(full + 1) * ktiles;
-  const double new_steps = (double)full * ktiles + cdiv(R * ktiles, slots) + kSkFixupSteps;
-  return new_steps < 0.95 * old_steps ? R : 0;
-}
-
-int64_t sk_bytes(const dfu_gemm_desc* d, const Plan& pl) {
-  if (!pl.entry || pl.tile != T256x256ps || d->epilogue == DFU_EPI_F32_ACC) return 0;
-  const int tiles = cdiv(d->M, 256) * cdiv(d->N, 256);
-  return sk_plan(tiles, kCUs, cdiv(d->K, BK)) ? 2 * kCUs * kSkSlotBytes : 0;
-}
-
 Tail tail_for(const dfu_gemm_desc* d, const Plan& pl) {
   if (!pl.entry || d->epilogue == DFU_EPI_F32_ACC || !kTailOK[pl.tile]) return Tail();
   const int tiles = cdiv(d->M, kTM[pl.tile]) * cdiv(d->N, kTN[pl.tile]);
@@ -299,8 +274,7 @@ extern "C" int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* d) {
       }
       return b;
     }
-    const int64_t skb = sk_bytes(d, pl);
-    return skb ? skb : tail_for(d, pl).bytes;
+    return tail_for(d, pl).bytes;
   }
   return pl.split > 1 ? (int64_t)pl.split * d->M * d->N * 4 : 0;
 }
@@ -320,12 +294,6 @@ extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* spl
 extern "C" int dfu_gemm_set_persistent(int32_t enable) {
   const int old = g_persistent;
   g_persistent = enable != 0;
-  return old;
-}
-
-extern "C" int dfu_gemm_set_stream_k(int32_t enable) {
-  const int old = g_stream_k;
-  g_stream_k = enable != 0;
   return old;
 }
 
@@ -599,20 +567,9 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
       a.counters = d->tile_counters;
     }
   }
-  a.sk_tiles = 0;
-  if (pl.tile == T256x256ps && !acc_epi && splits == 1) {
-    const int R = sk_plan(a.tiles_m * a.tiles_n, slots, a.ktiles);
-    if (R > 0 && d->workspace != nullptr && d->workspace_bytes >= 2 * slots * kSkSlotBytes &&
-        d->tile_counters != nullptr && d->tile_counters_len >= R) {
-      a.sk_tiles = R;
-      a.tslab = (float*)d->workspace;
-      a.counters = d->tile_counters;
-    }
-  }
   const int units = a.tail_r ? a.tail_full + a.tail_r * a.tail_s : a.tiles_m * a.tiles_n * splits;
   const bool atomics = acc_epi && splits > 1 && a.slab == nullptr;
-  // stream-K: exactly one workgroup per slot (the range is cut over gridDim.x)
-  const int nwg = a.sk_tiles ? slots : (g_persistent && !atomics && units > slots) ? slots : units;
+  const int nwg = (g_persistent && !atomics && units > slots) ? slots : units;
   hipLaunchKernelGGL(pl.entry->fn, dim3(nwg), dim3(pl.entry->threads), 0, s, a);
   DFU_LAUNCH_CHECK();
   if (a.slab != nullptr && a.counters == nullptr) {

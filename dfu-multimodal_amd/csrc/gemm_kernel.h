@@ -98,11 +98,6 @@ struct GemmArgs {
   int n_ld_bound;
   int dbg;  // timing experiments only (DFU_GEMM_DEBUG): 1 no epilogue, 2 no MFMA, 4 no DMA
   int a_bytes, b_bytes;  // operand extents in bytes (buffer-resource DMA of gemm_ps.hip)
-  // Stream-K tail (gemm_ps.hip, split == 1): the last sk_tiles tiles of the raster are not
-  // dealt out whole but as one range of sk_tiles * ktiles K-steps cut evenly over the grid;
-  // a tile whose K-steps span several workgroups is finished by the last of them to arrive
-  // (tslab: [2 * grid][32][512] f32x4 partials; counters: one per stream-K tile).
-  int sk_tiles;
 };
 
 // ------------------------------------------------------------------------------ LDS maps

@@ -205,78 +205,15 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
   }
 }
 
-// Stream-K hand-off (GemmArgs::sk_tiles): a workgroup's first segment of its K-step range
-// stores to slot 2w, its last to 2w + 1 (a range inside one tile: slot 2w).  Every segment of a
-// split tile stores its fp32 accumulators (write-through, lane-linear), counts the tile's
-// arrivals, and the last to arrive replaces acc by the sum of all the tile's segments in
-// workgroup order (its own re-read: the same values), so the result does not depend on the
-// arrival order; it then runs the epilogue.  Publish protocol of gemm_kernel.h tail_reduce
-// (own stores drained -> barrier -> one agent-scope atomic; no workgroup waits for another).
-struct SkRange {
-  int64_t T;  // K-steps of the stream-K region
-  int G;      // workgroups
-  DFU_DEV int64_t lo(int w) const { return (int64_t)w * T / G; }
-  // the workgroup whose range holds K-step g: largest w with lo(w) <= g
-  DFU_DEV int owner(int64_t g) const { return (int)(((g + 1) * G - 1) / T); }
-};
-
-DFU_DEV bool ps_sk_fixup(const GemmArgs& p, f32x4 (&acc)[8][4], const SkRange& R, int ts,
-                         int wg, int* flag, int tid) {
-  const int kt = p.ktiles;
-  const int64_t t0 = (int64_t)ts * kt;
-  auto slot_of = [&](int w) { return R.lo(w) >= t0 ? 2 * w : 2 * w + 1; };
-  const rsrc_t rs = make_rsrc(p.tslab);
-  auto off = [&](int slot, int f) { return (int)((((int64_t)slot * 32 + f) * 512 + tid) * 16); };
-  const int mine = slot_of(wg);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
-                                             off(mine, i * 4 + j), 0, 16);
-  const int w0 = R.owner(t0), w1 = R.owner(t0 + kt - 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(p.counters + ts, 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == w1 - w0;
-    if (last) __hip_atomic_store(p.counters + ts, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (!*flag) return false;
-  for (int w = w0; w <= w1; ++w) {
-    const int sl = slot_of(w);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {  // 8 fragments' loads in flight per round trip
-      f32x4 x[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        x[q] = __builtin_bit_cast(f32x4,
-                                  __builtin_amdgcn_raw_buffer_load_b128(rs, off(sl, c * 8 + q), 0, 16));
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int i = (c * 8 + q) >> 2, j = (c * 8 + q) & 3;
-        acc[i][j] = w == w0 ? x[q] : acc[i][j] + x[q];
-      }
-    }
-  }
-  return true;
-}
-
 template <int AMODE, int BMODE, int EPI>
 __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   constexpr bool AK_ = AMODE == DFU_OPND_KMAJOR;  // A K-contiguous (else MN-major: wgrad)
   constexpr bool BK_ = BMODE == DFU_OPND_KMAJOR;  // B K-contiguous (else MN-major)
-  __shared__ __attribute__((aligned(16))) char smem[PS_LDS + 16];  // + the stream-K flag
+  __shared__ __attribute__((aligned(16))) char smem[PS_LDS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles = p.tiles_m * p.tiles_n;
-  // stream-K tail: whole tiles [0, tiles - sk) in complete rounds, then the K-step range
-  const int sk = p.sk_tiles;
-  const int units = sk ? tiles - sk : tiles * p.split;
+  const int units = tiles * p.split;
   const int nwg = gridDim.x, bid = blockIdx.x;
   int wg = bid;
   if (nwg >= 16) {  // bijective XCD-aware remap: blocks b and b+8 share an XCD
@@ -299,16 +236,6 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
       tail_slot = r0 + j;
     }
   }
-  const SkRange skr{(int64_t)sk * p.ktiles, nwg};
-  int64_t sk_lo = 0, sk_hi = 0;
-  int sk_t0 = 0;
-  if (sk) {
-    sk_lo = skr.lo(wg);
-    sk_hi = skr.lo(wg + 1);
-    sk_t0 = (int)(sk_lo / p.ktiles);
-    if (sk_hi > sk_lo) rounds += (int)((sk_hi - 1) / p.ktiles) - sk_t0 + 1;
-  }
-  const int dp_rounds = sk ? full : rounds;  // rounds of whole units before the range
   if (rounds == 0) return;
   auto unit_at = [&](int i) { return i * nwg + (i < full ? wg : tail_slot); };
   auto unit_geom = [&](int u, int& m0, int& n0, int& kb, int& nk) {
@@ -323,24 +250,10 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     kb = s * p.kt_per_split;
     nk = min(p.ktiles, kb + p.kt_per_split) - kb;
   };
-  // segment i of this workgroup: a whole unit, or (stream-K) its part of tile sk_t0 + i - dp
-  auto seg_geom = [&](int i, int& m0, int& n0, int& kb, int& nk) {
-    if (i < dp_rounds) {
-      unit_geom(unit_at(i), m0, n0, kb, nk);
-      return;
-    }
-    const int ts = sk_t0 + i - dp_rounds;
-    const int64_t b = (int64_t)ts * p.ktiles;
-    const int64_t g0 = sk_lo > b ? sk_lo : b;
-    const int64_t g1 = sk_hi < b + p.ktiles ? sk_hi : b + p.ktiles;
-    unit_geom(tiles - sk + ts, m0, n0, kb, nk);
-    kb = (int)(g0 - b);
-    nk = (int)(g1 - g0);
-  };
   int total = 0;
   for (int i = 0; i < rounds; ++i) {
     int a_, b_, c_, nk_;
-    seg_geom(i, a_, b_, c_, nk_);
+    unit_geom(unit_at(i), a_, b_, c_, nk_);
     total += nk_;
   }
   PsSrc<AK_> sa;
@@ -363,16 +276,16 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
 
   // issue cursor (the K-step whose DMA goes out next) and compute cursor
   int iu = 0, ik = 0, im0, in0, ikb, ink;
-  seg_geom(0, im0, in0, ikb, ink);
+  unit_geom(unit_at(0), im0, in0, ikb, ink);
   src_init(im0, in0);
   int ci = 0, ck = 0, cm0, cn0, ckb, cnk;
-  int cu = dp_rounds > 0 ? unit_at(0) : 0;
-  seg_geom(0, cm0, cn0, ckb, cnk);
+  int cu = unit_at(0);
+  unit_geom(cu, cm0, cn0, ckb, cnk);
   auto advance_issue = [&]() {
     if (++ik == ink) {
       ik = 0;
       if (++iu < rounds) {
-        seg_geom(iu, im0, in0, ikb, ink);
+        unit_geom(unit_at(iu), im0, in0, ikb, ink);
         src_init(im0, in0);
       }
     }
@@ -504,12 +417,8 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     mf(1, 0, 1);
     epi_last = false;
     if (++ck == cnk) {
-      // a stream-K segment that is not its whole tile: hand off, the tile's last runs on
-      bool epi = true;
-      if (sk && ci >= dp_rounds && cnk != p.ktiles)
-        epi = ps_sk_fixup(p, acc, skr, sk_t0 + ci - dp_rounds, wg, (int*)(smem + PS_LDS), tid);
       if constexpr (!(kAbl & 1)) {
-        if (epi) ps_epilogue<EPI>(p, acc, cm0, cn0, wr, wc, lane, ci < dp_rounds ? cu / tiles : 0);
+        ps_epilogue<EPI>(p, acc, cm0, cn0, wr, wc, lane, cu / tiles);
       } else {  // keep the accumulators (and so every MFMA) alive without storing them
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -520,11 +429,11 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      epi_last = epi;
+      epi_last = true;
       ck = 0;
       if (++ci < rounds) {
-        if (ci < dp_rounds) cu = unit_at(ci);
-        seg_geom(ci, cm0, cn0, ckb, cnk);
+        cu = unit_at(ci);
+        unit_geom(cu, cm0, cn0, ckb, cnk);
       }
     }
   }
@@ -532,7 +441,7 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
 
 }  // namespace
 
-#define PS(A, B, E) {A, B, E, T256x256ps, &gemm_ps<A, B, E>, PS_LDS + 16, 512}
+#define PS(A, B, E) {A, B, E, T256x256ps, &gemm_ps<A, B, E>, PS_LDS, 512}
 const Entry kTable256x256ps[] = {
     PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
     PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_GELU),

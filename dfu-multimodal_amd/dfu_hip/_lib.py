@@ -80,7 +80,6 @@ PROTOTYPES = {
     "dfu_gemm_set_persistent": [I32],
     "dfu_gemm_set_inkernel_reduce": [I32],
     "dfu_gemm_set_tail_split": [I32],
-    "dfu_gemm_set_stream_k": [I32],
     "dfu_gemm_f32": [I32, I32, I32, P, I64, I64, P, I64, I64, P, I64, P, I32, I32, P, I64, P],
     "dfu_gemm_f32_workspace_bytes": [I32, I32, I32],
     "dfu_pack_conv_weight": [P, P, I32, I32, I32, I32, P],

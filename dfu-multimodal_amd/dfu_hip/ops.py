@@ -150,11 +150,6 @@ def gemm_set_tail_split(enable):
     return int(lib().dfu_gemm_set_tail_split(int(bool(enable))))
 
 
-def gemm_set_stream_k(enable):
-    """Stream-K tail of the persistent phased 256x256 tile (dfu_gemm_set_stream_k)."""
-    return int(lib().dfu_gemm_set_stream_k(int(bool(enable))))
-
-
 def gemm_set_inkernel_reduce(enable):
     """Split-K reduction inside the GEMM (1) or by the separate reduce kernel (0)."""
     return int(lib().dfu_gemm_set_inkernel_reduce(int(bool(enable))))

@@ -128,12 +128,6 @@ int dfu_gemm_set_persistent(int32_t enable);
  * counters, 0 (default: measured faster) = the separate reduce kernel.  Bitwise-identical; returns the
  * previous setting. */
 int dfu_gemm_set_inkernel_reduce(int32_t enable);
-/* Stream-K tail of the persistent phased 256x256 (tile 8, non-accumulating epilogues): 1
- * (default) = the tiles left over after the complete rounds are cut into an even K-step range
- * per workgroup, split tiles finished by their last segment (needs the workspace and tile
- * counters dfu_gemm_workspace_bytes asks for); 0 = a last round of whole tiles.  Returns the
- * previous setting. */
-int dfu_gemm_set_stream_k(int32_t enable);
 /* Tail-split switch: 1 (default) = when the tiles of an unsplit launch leave a last, partial
  * round of workgroups, split each of those tiles along K over the idle workgroups (fp32 slabs
  * in the descriptor's workspace, dfu_gemm_workspace_bytes; the tile's last split to finish sums
