@@ -124,6 +124,13 @@ def join_grad_streams(stream=None, clear=True):
 
 
 _side_streams = {}
+# HIP stream priorities of the side streams (torch: lower = higher priority).  The concurrent
+# ViT branch (the step's MFMA-bound critical path) runs at high priority, so the ResNet stream's
+# memory-bound kernels fill the CUs it leaves idle rather than delay it (same-box A/B, fusion
+# step, two runs each: 18.57-18.61 vs 18.64-18.66 ms); DFU_SIDE_STREAM_PRIORITY=0 restores the
+# default.  DFU_WGRAD_STREAM_PRIORITY: the ViT weight-gradient stream (default 0).
+_SIDE_PRIO = int(os.environ.get("DFU_SIDE_STREAM_PRIORITY", "-1"))
+_WGRAD_PRIO = int(os.environ.get("DFU_WGRAD_STREAM_PRIORITY", "0"))
 
 
 def side_stream(device):
@@ -133,7 +140,7 @@ def side_stream(device):
         idx = torch.cuda.current_device()
     st = _side_streams.get(idx)
     if st is None:
-        st = _side_streams[idx] = torch.cuda.Stream(device=idx)
+        st = _side_streams[idx] = torch.cuda.Stream(device=idx, priority=_SIDE_PRIO)
     return st
 
 
@@ -152,7 +159,7 @@ def wgrad_stream(device):
         idx = torch.cuda.current_device()
     st = _wgrad_streams.get(idx)
     if st is None:
-        st = _wgrad_streams[idx] = torch.cuda.Stream(device=idx)
+        st = _wgrad_streams[idx] = torch.cuda.Stream(device=idx, priority=_WGRAD_PRIO)
     return st
 
 
