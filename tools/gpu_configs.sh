@@ -14,6 +14,6 @@ done
 timeout -k 10 300 python tools/gemm_step_profile.py > $OUT/gemm_step_$TAG.log 2>&1 || { echo "profile rc=$?"; tail -20 $OUT/gemm_step_$TAG.log; exit 1; }
 timeout -k 10 300 python tools/gemm_step_profile.py --config rgb > $OUT/gemm_step_${TAG}_rgb.log 2>&1 || { echo "profile rgb rc=$?"; tail -20 $OUT/gemm_step_${TAG}_rgb.log; exit 1; }
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o bench -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt-precision > $OUT/prof_${TAG}_bench.json 2> $OUT/prof_${TAG}_bench.err || { echo "rocprof trace rc=$?"; tail -5 $OUT/prof_${TAG}_bench.err; exit 1; }
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_rgb -o bench -- python3 $R/bench.py --config rgb --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_${TAG}_rgb_bench.json 2> $OUT/prof_${TAG}_rgb_bench.err || { echo "rocprof rgb rc=$?"; tail -5 $OUT/prof_${TAG}_rgb_bench.err; exit 1; }
+
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_rgb -o bench -- python3 $R/bench.py --config rgb --steps 10 --warmup 3 --no-cpu-baseline --no-alt-precision > $OUT/prof_${TAG}_rgb_bench.json 2> $OUT/prof_${TAG}_rgb_bench.err || { echo "rocprof rgb rc=$?"; tail -5 $OUT/prof_${TAG}_rgb_bench.err; exit 1; }
 echo configs-done
