@@ -157,14 +157,22 @@ __global__ __launch_bounds__(256) void k_im2col_lds(
   for (int row = blockIdx.x; row < B * P; row += gridDim.x) {
     const int b = row / P, oh = row - b * P;
     __syncthreads();  // the previous row's gathers are done
+    // every input row's load issued before any is stored (W <= 256, C * R <= 24: host-checked)
     const float* xb = x + b * sn;
-    for (int cr = 0; cr < CR; ++cr) {
-      const int c = cr / R, r = cr - c * R;
-      const int ih = oh * stride - pad + r;
-      const bool in = (unsigned)ih < (unsigned)H;
-      const float* src = xb + c * sc + (int64_t)(in ? ih : 0) * sh;
-      for (int iw = threadIdx.x; iw < W; iw += 256) tile[cr * W + iw] = in ? src[iw * sw] : 0.f;
+    const int iw = threadIdx.x;
+    float v[24];
+#pragma unroll
+    for (int cr = 0; cr < 24; ++cr) {
+      v[cr] = 0.f;
+      if (cr < CR) {
+        const int c = cr / R, r = cr - c * R;
+        const int ih = oh * stride - pad + r;
+        if ((unsigned)ih < (unsigned)H && iw < W) v[cr] = xb[c * sc + (int64_t)ih * sh + iw * sw];
+      }
     }
+#pragma unroll
+    for (int cr = 0; cr < 24; ++cr)
+      if (cr < CR && iw < W) tile[cr * W + iw] = v[cr];
     __syncthreads();
     if (og >= groups) continue;
     bf16_t* orow = out + (int64_t)row * Q * ldo + kv * 8;
@@ -245,6 +253,17 @@ __global__ __launch_bounds__(256) void k_maxpool_rows(const bf16_t* __restrict__
 #pragma unroll
   for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
   const bf16_t* xb = x + (int64_t)b * H * W * C + c8 * 8;
+  // all nine window loads issued first (out-of-image taps read a clamped in-image address and
+  // are skipped below), so they are in flight together
+  u32x4 win[9];
+#pragma unroll
+  for (int wi = 0; wi < 3; ++wi)
+#pragma unroll
+    for (int wj = 0; wj < 3; ++wj) {
+      const int ih = min(max(2 * p - 1 + wi, 0), H - 1);
+      const int iw = min(max(2 * q - 1 + wj, 0), W - 1);
+      win[wi * 3 + wj] = *(const u32x4*)(xb + (int64_t)(ih * W + iw) * C);
+    }
 #pragma unroll
   for (int wi = 0; wi < 3; ++wi) {
     const int ih = 2 * p - 1 + wi;
@@ -253,9 +272,8 @@ __global__ __launch_bounds__(256) void k_maxpool_rows(const bf16_t* __restrict__
     for (int wj = 0; wj < 3; ++wj) {
       const int iw = 2 * q - 1 + wj;
       if ((unsigned)iw >= (unsigned)W) continue;
-      const u32x4 v = *(const u32x4*)(xb + (int64_t)(ih * W + iw) * C);
       float f[8];
-      unpack8(v, f);
+      unpack8(win[wi * 3 + wj], f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         if constexpr (BN) f[e] = bf2f(f2bf(fmaxf(fmaf(f[e], sc[e], sf[e]) + 0.f, 0.f)));
@@ -286,24 +304,30 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_rows(const bf16_t* __restri
   const int b = blockIdx.y / H, h = blockIdx.y - b * H;
   const int w = t / cv, c8 = t - w * cv;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int p_lo = h / 2, p_hi = min(P - 1, (h + 1) / 2);
-  const int q_lo = w / 2, q_hi = min(Q - 1, (w + 1) / 2);
-  for (int p = p_lo; p <= p_hi; ++p) {
-    const int wi = h - (2 * p - 1);
-    if (wi < 0 || wi > 2) continue;
-    for (int q = q_lo; q <= q_hi; ++q) {
-      const int wj = w - (2 * q - 1);
-      if (wj < 0 || wj > 2) continue;
-      const int64_t o = (((int64_t)b * P + p) * Q + q) * C + c8 * 8;
-      const uint64_t a = *(const uint64_t*)(am + o);
-      const u32x4 g = *(const u32x4*)(dy + o);
-      float f[8];
-      unpack8(g, f);
-      const int want = wi * 3 + wj;
+  // windows p = h/2 + dp (dp = 0, 1) and q = w/2 + dq cover every window holding (h, w); the
+  // four candidates' loads go out together (clamped addresses), invalid ones are skipped, and
+  // the valid ones are summed in row-major window order
+  const int p0 = h / 2, q0 = w / 2;
+  uint64_t a4[4];
+  u32x4 g4[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if ((int)((a >> (8 * e)) & 0xff) == want) acc[e] += f[e];
-    }
+  for (int k = 0; k < 4; ++k) {
+    const int p = min(p0 + (k >> 1), P - 1), q = min(q0 + (k & 1), Q - 1);
+    const int64_t o = (((int64_t)b * P + p) * Q + q) * C + c8 * 8;
+    a4[k] = *(const uint64_t*)(am + o);
+    g4[k] = *(const u32x4*)(dy + o);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = p0 + (k >> 1), q = q0 + (k & 1);
+    const int wi = h - (2 * p - 1), wj = w - (2 * q - 1);
+    if (p >= P || q >= Q || wi < 0 || wi > 2 || wj < 0 || wj > 2) continue;
+    float f[8];
+    unpack8(g4[k], f);
+    const int want = wi * 3 + wj;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if ((int)((a4[k] >> (8 * e)) & 0xff) == want) acc[e] += f[e];
   }
   *(u32x4*)(dx + ((int64_t)blockIdx.y * W + w) * C + c8 * 8) = pack8(acc);
 }
@@ -760,7 +784,7 @@ extern "C" int dfu_cast_rows_f32(const void* in, int64_t ld_in, float* out, int6
 // The LDS-staged kernel when the C x R input rows of one output row fit (the stem: 3 x 7 x 224
 // fp32 = 18.4 KiB); the per-chunk gather otherwise.
 static bool im2col_lds_fits(int C, int R, int W, int Kp) {
-  return Kp <= 256 * 8 / 2 && (int64_t)C * R * W * 4 <= 48 * 1024;
+  return Kp <= 256 * 8 / 2 && C * R <= 24 && W <= 256 && (int64_t)C * R * W * 4 <= 48 * 1024;
 }
 
 extern "C" int dfu_im2col_f32(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
