@@ -135,10 +135,25 @@ __global__ void k_bn_eval_coeffs(const float* gamma, const float* beta, const fl
 // blocks and C/8 a power of two <= 256 (every ResNet-50 width) the stride is a multiple of C/8,
 // so a thread's channel group never changes: FIXED kernels decode it once and keep the
 // per-channel constants in registers (no per-vector 64-bit modulo, no per-element loads).
+// mask (optional): bit e of byte i = (stored output element 8i + e > 0), the ReLU mask the
+// backward needs (dfu_bn_bwd_* relu = 3) at 1/16 of the bytes of re-reading the output.
+DFU_DEV unsigned positive_bits8(const u32x4 pk) {
+  unsigned m = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const unsigned lo = pk[w] & 0xffffu, hi = pk[w] >> 16;
+    // bf16 bits of a value > 0: +denormal .. +inf (0x0001 .. 0x7f80); not +-0, negatives, NaN
+    m |= (unsigned)(lo - 1u < 0x7f80u) << (2 * w);
+    m |= (unsigned)(hi - 1u < 0x7f80u) << (2 * w + 1);
+  }
+  return m;
+}
+
 template <bool FIXED>
 __global__ void k_bn_apply(const bf16_t* __restrict__ y, const float* __restrict__ scale,
                            const float* __restrict__ shift, const bf16_t* __restrict__ res,
-                           int relu, bf16_t* __restrict__ out, int64_t M, int C) {
+                           int relu, bf16_t* __restrict__ out, uint8_t* __restrict__ mask,
+                           int64_t M, int C) {
   const int cv = C / 8;
   const int64_t n = M * cv;
   float sc[8], sf[8];
@@ -163,7 +178,9 @@ __global__ void k_bn_apply(const bf16_t* __restrict__ y, const float* __restrict
       float v = fmaf(f[e], sc[e], sf[e]) + r[e];
       f[e] = relu ? fmaxf(v, 0.f) : v;
     }
-    *(u32x4*)(out + i * 8) = pack8(f);
+    const u32x4 pk = pack8(f);
+    *(u32x4*)(out + i * 8) = pk;
+    if (mask) mask[i] = (uint8_t)positive_bits8(pk);
   }
 }
 
@@ -194,10 +211,11 @@ inline int bwd_rows_per_block(int64_t M, int C) {
 // A compile-time mode: every load of an iteration is issued before any of them is used.
 template <int RELU>
 DFU_DEV void relu_mask8(const float* oo, const float* yy, const float* sc, const float* sf,
-                        float* g) {
+                        float* g, unsigned mb = 0) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     if constexpr (RELU == 1) g[e] = oo[e] > 0.f ? g[e] : 0.f;
+    if constexpr (RELU == 3) g[e] = ((mb >> e) & 1u) ? g[e] : 0.f;
     if constexpr (RELU == 2) g[e] = (fmaf(yy[e], sc[e], sf[e]) + 0.f) > 0.f ? g[e] : 0.f;
   }
 }
@@ -237,6 +255,7 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
       yv[u] = *(const u32x4*)(y + o);
       ov[u] = (u32x4){0u, 0u, 0u, 0u};
       if constexpr (RELU == 1) ov[u] = *(const u32x4*)(out + o);
+      if constexpr (RELU == 3) ov[u][0] = ((const uint8_t*)out)[o / 8];
     }
 #pragma unroll
     for (int u = 0; u < RED_U; ++u) {
@@ -245,7 +264,7 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
       unpack8(gv[u], g);
       unpack8(yv[u], yy);
       unpack8(ov[u], oo);
-      relu_mask8<RELU>(oo, yy, sc, sf, g);
+      relu_mask8<RELU>(oo, yy, sc, sf, g, ov[u][0]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         sg[e] += g[e];
@@ -354,10 +373,11 @@ __global__ void k_bn_bwd_apply(const bf16_t* __restrict__ dout, const bf16_t* __
     const u32x4 gv = *(const u32x4*)(dout + i * 8), yv = *(const u32x4*)(y + i * 8);
     u32x4 ov = {};
     if constexpr (RELU == 1) ov = *(const u32x4*)(out + i * 8);
+    if constexpr (RELU == 3) ov[0] = ((const uint8_t*)out)[i];
     unpack8(gv, g);
     unpack8(yv, yy);
     unpack8(ov, oo);
-    relu_mask8<RELU>(oo, yy, sc, sf, g);
+    relu_mask8<RELU>(oo, yy, sc, sf, g, ov[0]);
     if (dres) *(u32x4*)(dres + i * 8) = pack8(g);
     float d[8];
 #pragma unroll
@@ -419,16 +439,22 @@ extern "C" int dfu_bn_eval_coeffs(const float* gamma, const float* beta, const f
   return DFU_OK;
 }
 
-extern "C" int dfu_bn_apply(const void* y, const float* scale, const float* shift,
-                            const void* residual, int32_t relu, void* out, int64_t M, int32_t C,
-                            void* stream) {
+extern "C" int dfu_bn_apply_mask(const void* y, const float* scale, const float* shift,
+                                 const void* residual, int32_t relu, void* out, uint8_t* mask,
+                                 int64_t M, int32_t C, void* stream) {
   DFU_CHECK_ARG(y && scale && shift && out && C % 8 == 0 && M > 0, "dfu_bn_apply: bad args");
   hipLaunchKernelGGL(fixed_channels(C) ? k_bn_apply<true> : k_bn_apply<false>,
                      dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)y, scale, shift, (const bf16_t*)residual, relu, (bf16_t*)out,
-                     M, C);
+                     mask, M, C);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
+}
+
+extern "C" int dfu_bn_apply(const void* y, const float* scale, const float* shift,
+                            const void* residual, int32_t relu, void* out, int64_t M, int32_t C,
+                            void* stream) {
+  return dfu_bn_apply_mask(y, scale, shift, residual, relu, out, nullptr, M, C, stream);
 }
 
 extern "C" int dfu_bn_bwd_blocks(int64_t M, int32_t C) {
@@ -441,16 +467,19 @@ extern "C" int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* ou
                                  const float* invstd, int64_t M, int32_t C, float* partial,
                                  void* stream) {
   DFU_CHECK_ARG(dout && y && mean && invstd && partial && C % 8 == 0 && M > 0 && relu >= 0 &&
-                    relu <= 2,
+                    relu <= 3,
                 "dfu_bn_bwd_reduce: bad args");
-  DFU_CHECK_ARG(relu != 1 || out, "dfu_bn_bwd_reduce: relu=1 needs out");
+  DFU_CHECK_ARG((relu != 1 && relu != 3) || out, "dfu_bn_bwd_reduce: relu=1/3 needs out/mask");
   DFU_CHECK_ARG(relu != 2 || (scale && shift), "dfu_bn_bwd_reduce: relu=2 needs scale/shift");
   const int cv = C / 8;
   const int ct_n = cv < 64 ? cv : 64;
   DFU_CHECK_ARG(256 % ct_n == 0 && cv % ct_n == 0, "dfu_bn_bwd_reduce: C=%d unsupported", C);
   const int rpb = bwd_rows_per_block(M, C);
   dim3 grid(cv / ct_n, dfu_bn_bwd_blocks(M, C));
-  auto kern = relu == 1 ? k_bn_bwd_reduce<1> : relu == 2 ? k_bn_bwd_reduce<2> : k_bn_bwd_reduce<0>;
+  auto kern = relu == 1   ? k_bn_bwd_reduce<1>
+              : relu == 2 ? k_bn_bwd_reduce<2>
+              : relu == 3 ? k_bn_bwd_reduce<3>
+                          : k_bn_bwd_reduce<0>;
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dout,
                      (const bf16_t*)y, (const bf16_t*)out, scale, shift, mean, invstd, M, C, rpb,
                      partial);
@@ -484,13 +513,14 @@ extern "C" int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out
                                 const float* invstd, const float* coef, int64_t M, int32_t C,
                                 void* dy, void* dres, void* stream) {
   DFU_CHECK_ARG(dout && y && mean && invstd && coef && dy && C % 8 == 0 && M > 0 && relu >= 0 &&
-                    relu <= 2,
+                    relu <= 3,
                 "dfu_bn_bwd_apply: bad args");
-  DFU_CHECK_ARG(relu != 1 || out, "dfu_bn_bwd_apply: relu=1 needs out");
+  DFU_CHECK_ARG((relu != 1 && relu != 3) || out, "dfu_bn_bwd_apply: relu=1/3 needs out/mask");
   DFU_CHECK_ARG(relu != 2 || (scale && shift), "dfu_bn_bwd_apply: relu=2 needs scale/shift");
   const bool fx = fixed_channels(C);
   auto kern = relu == 1   ? (fx ? k_bn_bwd_apply<1, true> : k_bn_bwd_apply<1, false>)
               : relu == 2 ? (fx ? k_bn_bwd_apply<2, true> : k_bn_bwd_apply<2, false>)
+              : relu == 3 ? (fx ? k_bn_bwd_apply<3, true> : k_bn_bwd_apply<3, false>)
                           : (fx ? k_bn_bwd_apply<0, true> : k_bn_bwd_apply<0, false>);
   hipLaunchKernelGGL(kern, dim3(grid_for(M * C / 8)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)dout, (const bf16_t*)y, (const bf16_t*)out, scale, shift, mean,

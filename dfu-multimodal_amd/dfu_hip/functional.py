@@ -347,9 +347,9 @@ class _BN:
                                self.invstd, _empty((self.C,), F32, self.mean.device))
 
     def backward(self, dout, y, out, relu, dy, dres):
-        """relu: False; True (mask from `out`, the BN + residual + ReLU case); or 2 (BN + ReLU
+        """relu: False; True (mask from `out`, the BN + residual + ReLU case); 2 (BN + ReLU
         with no residual: the mask is recomputed from y with the forward's scale/shift, so
-        `out` is not read)."""
+        `out` is not read); or 3 (`out` is the forward's ReLU bitmask, ops.bn_apply(mask=))."""
         bn = self.bn
         dgamma = grad_buffer(bn.weight) if _wants(bn.weight) else None
         dbeta = grad_buffer(bn.bias) if _wants(bn.bias) else None
@@ -582,7 +582,7 @@ class BottleneckFn(torch.autograd.Function):
         M2 = B * g2.p * g2.q
         planes, outc = g1.k, g3.k
 
-        def conv_bn(xrows, geom, w, bnmod, relu, residual=None):
+        def conv_bn(xrows, geom, w, bnmod, relu, residual=None, mask=None):
             M = geom.n * geom.p * geom.q
             y = _empty((M, geom.k), BF16, dev)
             stats = _empty((ops.stats_tiles(M), 2, geom.k), F32, dev)
@@ -590,7 +590,7 @@ class BottleneckFn(torch.autograd.Function):
             st = _BN(bnmod, M, geom.k, dev)
             st.forward_coeffs(stats)
             out = _empty((M, geom.k), BF16, dev)
-            ops.bn_apply(y, st.scale, st.shift, residual, relu, out, M, geom.k)
+            ops.bn_apply(y, st.scale, st.shift, residual, relu, out, M, geom.k, mask=mask)
             return y, out, st
 
         def conv_bn_x3(x3rows, geom, w3x, bnmod, relu, res=None, res_mode=0, want3=True,
@@ -639,8 +639,12 @@ class BottleneckFn(torch.autograd.Function):
             y3, out, out3, _, s3 = conv_bn_x3(a2_3, g3, conv_weight_x3(mod.conv3.weight),
                                               mod.bn3, True, res=res, res_mode=res_mode)
             del a2_3, res, xin3
+            mask3 = None
         else:
-            y3, out, s3 = conv_bn(a2, g3, w3, mod.bn3, True, residual=idn)
+            # bn3 + residual + ReLU also writes its ReLU bitmask: the backward reads M*C/8 bytes
+            # instead of the block output twice (reduce and apply)
+            mask3 = _empty((M2 * outc // 8,), torch.uint8, dev)
+            y3, out, s3 = conv_bn(a2, g3, w3, mod.bn3, True, residual=idn, mask=mask3)
         ctx.x3 = x3mode
         ctx.mod = mod
         ctx.geo = (g1, g2, g3, gd)
@@ -655,8 +659,8 @@ class BottleneckFn(torch.autograd.Function):
             ctx.probes = (from_rows(a1, B, g1.p, g1.q, planes).detach().requires_grad_(True),
                           from_rows(a2, B, g2.p, g2.q, planes).detach().requires_grad_(True))
             mod._probes = ctx.probes
-        ctx.save_for_backward(xr, y1, a1, y2, a2, y3, out, w1, w2, w3,
-                              *( (yd, wd) if yd is not None else ()))
+        ctx.save_for_backward(xr, y1, a1, y2, a2, y3, out if mask3 is None else mask3, w1, w2,
+                              w3, *( (yd, wd) if yd is not None else ()))
         res = from_rows(out, B, g3.p, g3.q, outc)
         if out3 is not None:
             res._dfu_x3 = out3
@@ -674,10 +678,10 @@ class BottleneckFn(torch.autograd.Function):
         dev = xr.device
         g = rows_view(nhwc_bf16(gout))
         M1, M2 = y1.shape[0], y3.shape[0]
-        # bn3 (+ residual) + relu
+        # bn3 (+ residual) + relu: the mask from the forward's bitmask (bf16) or its output (x3)
         dy3 = torch.empty_like(y3)
         dres = torch.empty_like(y3)
-        s3.backward(g, y3, out, True, dy3, dres)
+        s3.backward(g, y3, out, 3 if out.dtype == torch.uint8 else True, dy3, dres)
         # downsample branch (its dgrad is added in place after conv1's, below)
         dyd = None
         if yd is not None:

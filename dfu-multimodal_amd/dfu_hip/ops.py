@@ -371,9 +371,16 @@ def bn_eval_coeffs(gamma, beta, rm, rv, eps, scale_out, shift_out):
           "dfu_bn_eval_coeffs")
 
 
-def bn_apply(y, scale, shift, residual, relu, out, M, C):
-    check(lib().dfu_bn_apply(ptr(y), ptr(scale), ptr(shift), ptr(residual), int(relu), ptr(out),
-                             M, C, stream_ptr()), "dfu_bn_apply")
+def bn_apply(y, scale, shift, residual, relu, out, M, C, mask=None):
+    """out = act(y * scale + shift (+ residual)); with `mask` (uint8 [M * C / 8]) also the bitmask
+    of out > 0 that bn_bwd(relu=3) reads in place of out."""
+    if mask is None:
+        check(lib().dfu_bn_apply(ptr(y), ptr(scale), ptr(shift), ptr(residual), int(relu),
+                                 ptr(out), M, C, stream_ptr()), "dfu_bn_apply")
+    else:
+        check(lib().dfu_bn_apply_mask(ptr(y), ptr(scale), ptr(shift), ptr(residual), int(relu),
+                                      ptr(out), ptr(mask), M, C, stream_ptr()),
+              "dfu_bn_apply_mask")
 
 
 def bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres,
@@ -397,7 +404,8 @@ def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbet
            batch_stats=True, scale=None, shift=None):
     """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply.  relu: False/0 none;
     True/1 mask from the stored output `out`; 2 mask recomputed from y with the forward's
-    scale/shift (BN + ReLU without residual; `out` is not read)."""
+    scale/shift (BN + ReLU without residual; `out` is not read); 3 mask from the bitmask
+    bn_apply(mask=) wrote, passed as `out`."""
     relu = int(relu)
     if relu == 2 and (scale is None or shift is None):
         raise ValueError("bn_bwd: relu=2 needs the forward scale/shift")

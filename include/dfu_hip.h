@@ -227,10 +227,16 @@ int dfu_bn_eval_coeffs(const float* gamma, const float* beta, const float* runni
 /* out = act(y*scale[c] + shift[c] (+ residual)), bf16 NHWC; act = relu if relu != 0. */
 int dfu_bn_apply(const void* y, const float* scale, const float* shift, const void* residual,
                  int32_t relu, void* out, int64_t M, int32_t C, void* stream);
+/* dfu_bn_apply that also writes the ReLU mask of its output: bit e of mask[i] = (out element
+ * 8i + e > 0), M*C/8 bytes (the backward's relu = 3 input; mask may be NULL). */
+int dfu_bn_apply_mask(const void* y, const float* scale, const float* shift,
+                      const void* residual, int32_t relu, void* out, uint8_t* mask, int64_t M,
+                      int32_t C, void* stream);
 /* Backward of out = act(bn(y) (+res)).  reduce: per-channel partial sums of g and g*xhat,
  * g = dout * mask; written as [blocks][2][C] (dfu_bn_bwd_blocks(M, C)).  relu: 0 no mask;
  * 1 mask = out > 0 (BN + residual + ReLU: reads out); 2 mask = y*scale + shift > 0 with the
- * forward's scale/shift (BN + ReLU, no residual: recomputed from y, out not read). */
+ * forward's scale/shift (BN + ReLU, no residual: recomputed from y, out not read); 3 the same
+ * mask as 1 from the bitmask dfu_bn_apply_mask wrote, passed as `out` (1/16 of the bytes). */
 int dfu_bn_bwd_blocks(int64_t M, int32_t C);
 int dfu_bn_bwd_reduce(const void* dout, const void* y, const void* out, int32_t relu,
                       const float* scale, const float* shift, const float* mean,

@@ -321,8 +321,9 @@ def test_batchnorm_train_fwd_bwd():
 
 @pytest.mark.parametrize("M,C", [(5000, 128), (3136, 2048), (200704, 64)])
 def test_batchnorm_bwd_mask_from_y_is_bitwise(M, C):
-    """relu=2 (mask recomputed from y with the forward scale/shift, `out` not read) equals relu=1
-    (mask from the stored BN+ReLU output) bit for bit."""
+    """relu=2 (mask recomputed from y with the forward scale/shift, `out` not read) and relu=3
+    (the bitmask bn_apply wrote beside its output) equal relu=1 (mask from the stored BN+ReLU
+    output) bit for bit."""
     y = rnd(M, C, seed=50, scale=2.0)
     stats = torch.empty(ops.stats_tiles(M), 2, C, dtype=torch.float32, device=DEV)
     Y = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
@@ -334,17 +335,21 @@ def test_batchnorm_bwd_mask_from_y_is_bitwise(M, C):
     ops.bn_finalize(stats, M, C, gamma, beta, 1e-5, 0.1, None, None, None, mean, invstd, scale,
                     shift)
     out = torch.empty_like(Y)
-    ops.bn_apply(Y, scale, shift, None, True, out, M, C)
+    mask = torch.empty(M * C // 8, dtype=torch.uint8, device=DEV)
+    ops.bn_apply(Y, scale, shift, None, True, out, M, C, mask=mask)
+    bits = ((mask.view(-1, 1) >> torch.arange(8, device=DEV, dtype=torch.uint8)) & 1).view(M, C)
+    assert torch.equal(bits.bool(), out.float() > 0), "bitmask != (out > 0)"
     dout = rnd(M, C, seed=53)
     res = []
-    for mode, o in ((1, out), (2, None)):
+    for mode, o in ((1, out), (2, None), (3, mask)):
         dy = torch.empty_like(Y)
         dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
         ops.bn_bwd(dout, Y, o, mode, mean, invstd, gamma, M, C, dy, None, dg, db,
                    scale=scale, shift=shift)
         res.append((dy, dg, db))
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            assert torch.equal(a, b)
 
 
 def test_layernorm_fwd_bwd():
