@@ -18,14 +18,20 @@ from . import functional as Fn
 
 
 def init_from_env(backend=None):
-    """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/MASTER_*)."""
+    """Initialise the default process group from torchrun's env (RANK/WORLD_SIZE/MASTER_*).
+    Rehearsal knobs (a one-GPU box running the N-rank path): DFU_DIST_BACKEND picks the backend
+    (default nccl = RCCL with a GPU, else gloo) and DFU_SHARE_DEVICE=1 puts every rank on device
+    0 (gloo then all-reduces the CUDA gradient buckets through host memory)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return 0, 1, 0
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    if os.environ.get("DFU_SHARE_DEVICE", "0") == "1":
+        local = 0
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("DFU_DIST_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     if not dist.is_initialized():
