@@ -727,12 +727,13 @@ __global__ __launch_bounds__(256) void k_transpose_bf16(const dfu_transpose_job*
   const int r0 = (lt / tn) * 64, c0 = (lt % tn) * 64;
   const uint16_t* src = (const uint16_t*)jb.src;
   uint16_t* dst = (uint16_t*)jb.dst;
+  const int64_t lds = jb.ld_src ? jb.ld_src : jb.cols, ldd = jb.ld_dst ? jb.ld_dst : jb.rows;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {  // 64 rows x 8 chunks of 8 columns
     const int q = threadIdx.x + 256 * h;
     const int r = q >> 3, cc = (q & 7) * 8;
     if (r0 + r < jb.rows && c0 + cc < jb.cols) {
-      const u32x4 v = *(const u32x4*)(src + (int64_t)(r0 + r) * jb.cols + c0 + cc);
+      const u32x4 v = *(const u32x4*)(src + (int64_t)(r0 + r) * lds + c0 + cc);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         t[r][cc + 2 * e] = (uint16_t)(v[e] & 0xffffu);
@@ -750,7 +751,7 @@ __global__ __launch_bounds__(256) void k_transpose_bf16(const dfu_transpose_job*
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         v[e] = (uint32_t)t[rr + 2 * e][c] | ((uint32_t)t[rr + 2 * e + 1][c] << 16);
-      *(u32x4*)(dst + (int64_t)(c0 + c) * jb.rows + r0 + rr) = v;
+      *(u32x4*)(dst + (int64_t)(c0 + c) * ldd + r0 + rr) = v;
     }
   }
 }

@@ -281,6 +281,32 @@ def weight_bf16_T(w):
     return w._dfu_shadow_T
 
 
+# Stride-1 spatial conv input gradients as forward convolutions of dY with the flipped,
+# channel-transposed weight (optim.FlatParams.add_flipped): K-contiguous weight operand and the
+# forward's gather loader instead of the dgrad's MN-major weight view.  DFU_DGRAD_FLIP=0: the
+# dgrad loaders (A/B timing).
+_DGRAD_FLIP = os.environ.get("DFU_DGRAD_FLIP", "1") != "0"
+
+
+def conv_weight_flipped(w):
+    """W'[C][R][S][K] = W[K][R-1-r][S-1-s][C] (bf16, [C][R*S*K]) of a FusedAdamW-managed
+    channels-last conv weight, or None.  Re-derived (one launch, on the current stream) on the
+    first use after the optimizer rewrote the shadows or the weight was edited outside it."""
+    if not _DGRAD_FLIP or not _krsc_strided(w):
+        return None
+    sh = weight_bf16_rows(w)
+    flat = getattr(w, "_dfu_flat", None)
+    if flat is None or sh is not getattr(w, "_dfu_shadow", None):
+        return None
+    if getattr(w, "_dfu_shadow_F", None) is None:
+        flat.add_flipped(w)
+    key = (flat.gen, getattr(w, "_dfu_shadow_version", None))
+    if w._dfu_fkey != key:
+        w._dfu_flip_jobs.launch()
+        w._dfu_fkey = key
+    return w._dfu_shadow_F
+
+
 def conv_weight_bf16(w):
     """fp32 OIHW conv weight -> bf16 KRSC GEMM operand: the shadow view for a 1x1 conv (OIHW ==
     KRSC) and for a FusedAdamW-managed weight stored channels-last; else a packing kernel."""
@@ -399,13 +425,21 @@ def conv_fwd_x3(x3_rows, geom, w3, y, stats):
                  epilogue=L.EPI_F32_STATS, stats=stats, conv=g3)
 
 
-def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, bn=None, y=None):
+def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, bn=None, y=None, w_flip=None):
     """dx[N*H*W, C] = dgrad(dy) (+ add, bf16).  With bn (a _BN whose input y is this conv's
     input, BN + ReLU without residual; stride 1): the epilogue also reduces that BN's
     backward sums over dx (DFU_EPI_BF16_DSTATS); returns the [tiles][2][C] records for
-    _BN.backward_from_dstats."""
+    _BN.backward_from_dstats.  With w_flip (conv_weight_flipped; stride 1, no add, no bn): dx
+    is the forward convolution of dy (K input channels, pad R-1-pad) with the flipped weight."""
     g = geom
     Mx = g.n * g.h * g.w
+    if w_flip is not None and add is None and bn is None and g.stride == 1:
+        gd = ops.ConvGeom(g.n, g.p, g.q, g.k, g.c, g.r, g.s, 1, g.r - 1 - g.pad)
+        if (gd.p, gd.q) == (g.h, g.w) and g.r - 1 - g.pad >= 0:
+            K = g.r * g.s * g.k
+            ops.gemm(Mx, g.c, K, dy_rows, 0, w_flip, K, dx, g.c, a_mode=L.OPND_CONV_FWD,
+                     epilogue=L.EPI_BF16, conv=gd)
+            return None
     epi = L.EPI_BF16_ADD if add is not None else L.EPI_BF16
     aux, ld_aux, stats = add, (g.c if add is not None else 0), None
     if bn is not None:
@@ -709,7 +743,10 @@ class BottleneckFn(torch.autograd.Function):
         else:
             s2.backward(da2, y2, a2 if ctx.x3 else None, 1 if ctx.x3 else 2, dy2, None)
         da1 = torch.empty_like(a1)
-        st1 = conv_dgrad(dy2, g2, w2, da1, bn=s1 if fuse and g2.stride == 1 else None, y=y1)
+        fuse1 = fuse and g2.stride == 1
+        st1 = conv_dgrad(dy2, g2, w2, da1, bn=s1 if fuse1 else None, y=y1,
+                         w_flip=None if fuse1 or g2.stride != 1 else
+                         conv_weight_flipped(mod.conv2.weight))
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[0], from_rows(da1, B, g1.p, g1.q, g1.k))
         if _wants(mod.conv2.weight):

@@ -229,7 +229,9 @@ def cast_rows_bf16(x, ld_out=None, out=None):
 
 class TransposeJobs:
     """A device table of bf16 transposes (dfu_transpose_bf16: dst[c][r] = src[r][c]) built once
-    and launched as ONE kernel each time (the transposed weight shadows, optim.FlatParams)."""
+    and launched as ONE kernel each time (the transposed / flipped weight shadows,
+    optim.FlatParams).  src and dst are 2-D views with unit column stride (row strides and
+    sizes multiples of 8, 16-B aligned)."""
 
     def __init__(self, pairs):
         import struct
@@ -238,10 +240,14 @@ class TransposeJobs:
             _req(src, BF16, "transpose_bf16")
             _req(dst, BF16, "transpose_bf16")
             r, c = src.shape
-            if dst.shape != (c, r) or r % 8 or c % 8 or not (src.is_contiguous() and
-                                                            dst.is_contiguous()):
-                raise ValueError(f"transpose_bf16: [{r}, {c}] -> {tuple(dst.shape)} unsupported")
-            raw += struct.pack("<QQiiii", src.data_ptr(), dst.data_ptr(), r, c, tile0, 0)
+            ok = (dst.shape == (c, r) and r % 8 == 0 and c % 8 == 0 and src.stride(1) == 1 and
+                  dst.stride(1) == 1 and src.stride(0) % 8 == 0 and dst.stride(0) % 8 == 0 and
+                  src.data_ptr() % 16 == 0 and dst.data_ptr() % 16 == 0)
+            if not ok:
+                raise ValueError(f"transpose_bf16: [{r}, {c}] stride {src.stride()} -> "
+                                 f"{tuple(dst.shape)} stride {dst.stride()} unsupported")
+            raw += struct.pack("<QQiiiiii", src.data_ptr(), dst.data_ptr(), r, c, tile0,
+                               src.stride(0), dst.stride(0), 0)
             tile0 += ((r + 63) // 64) * ((c + 63) // 64)
         self.pairs = list(pairs)  # keep the buffers alive as long as the table
         self.njobs, self.ntiles = len(self.pairs), tile0

@@ -72,7 +72,8 @@ class FlatParams:
         self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=dev) if dev.type == "cuda" \
             else None
         self.gen = 0         # bumped whenever every shadow is rewritten (step, refresh)
-        self.t_params = []   # parameters with a transposed shadow (p._dfu_shadow_T)
+        self.t_params = []   # parameters with a transposed (p._dfu_shadow_T) or flipped
+        self.t_pairs = []    # (p._dfu_shadow_F) shadow, and their (src, dst) transpose jobs
         self.t_jobs = None
         with torch.no_grad():
             for p, o, kr in zip(self.params, self.offsets, self.krsc):
@@ -100,11 +101,33 @@ class FlatParams:
         sh = p._dfu_shadow
         p._dfu_shadow_T = torch.empty((sh.shape[1], sh.shape[0]), dtype=sh.dtype,
                                       device=sh.device)
+        self._add_jobs(p, [(sh, p._dfu_shadow_T)])
+
+    def add_flipped(self, p):
+        """Give spatial conv weight p (KRSC shadow [K][R*S*C]) a flipped, channel-transposed bf16
+        copy W'[C][R][S][K] = W[K][R-1-r][S-1-s][C] -- the weight of its stride-1 input gradient
+        run as a forward convolution (functional.conv_dgrad) -- and its launch table (one
+        transpose job per filter tap).  Derived on first use after each shadow rewrite
+        (functional.conv_weight_flipped), i.e. on the ResNet's own stream in backward, not in
+        the optimizer's tail: a batched refresh after AdamW measured slower in the two-stream
+        step (it lengthens the step's serial end)."""
+        K, C, R, S = p.shape
+        sh = p._dfu_shadow.view(K, R * S, C)
+        f = torch.empty((C, R * S * K), dtype=sh.dtype, device=sh.device)
+        fv = f.view(C, R * S, K)
+        p._dfu_shadow_F = f
+        p._dfu_flip_jobs = ops.TransposeJobs([(sh[:, t, :], fv[:, R * S - 1 - t, :])
+                                              for t in range(R * S)])
+        p._dfu_fkey = None
+
+    def _add_jobs(self, p, pairs):
         self.t_params.append(p)
-        self.t_jobs = ops.TransposeJobs([(q._dfu_shadow, q._dfu_shadow_T) for q in self.t_params])
+        self.t_pairs += pairs
+        self.t_jobs = ops.TransposeJobs(self.t_pairs)
 
     def shadows_rewritten(self):
-        """Every shadow was just rewritten (AdamW, refresh): re-derive the transposed ones."""
+        """Every shadow was just rewritten (AdamW, refresh): re-derive the transposed ones (the
+        flipped conv copies follow on their next use: gen changed)."""
         self.gen += 1
         if self.t_jobs is not None:
             self.t_jobs.launch()

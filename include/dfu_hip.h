@@ -156,10 +156,13 @@ int dfu_conv_grad_krsc_to_oihw(const float* krsc, float* oihw, int32_t K, int32_
 /* fp32 [rows][cols] -> bf16 [rows][ld_out] (cols..ld_out-1 zero-filled). */
 int dfu_cast_rows_bf16(const float* in, int64_t ld_in, void* out, int64_t ld_out, int32_t rows,
                        int32_t cols, void* stream);
-/* Batched bf16 transpose: for each job, dst[c][r] = src[r][c] (src [rows][cols], dst
- * [cols][rows], both dense; rows and cols multiples of 8).  Keeps a transposed copy of the
- * ViT Linear weights' bf16 shadow so the input-gradient GEMMs read their weight operand
- * K-contiguous (dX = dY W: B = W^T [in][out]) instead of MN-major.  `jobs` lives in DEVICE
+/* Batched bf16 transpose: for each job, dst[c][r] = src[r][c] (src [rows][cols] with row
+ * stride ld_src, dst [cols][rows] with row stride ld_dst, in elements, 0 = dense; rows, cols
+ * and the strides multiples of 8, both 16-B aligned).  Keeps a transposed copy of the ViT
+ * Linear weights' bf16 shadow so the input-gradient GEMMs read their weight operand
+ * K-contiguous (dX = dY W: B = W^T [in][out]) instead of MN-major, and, one job per filter tap,
+ * the flipped channel-transposed copy of the 3x3 conv weights the stride-1 conv dgrads run as
+ * forward convolutions on (W'[c][R-1-r][S-1-s][k] = W[k][r][s][c]).  `jobs` lives in DEVICE
  * memory; job j covers the launch's 64x64 tiles [tile0_j, tile0_j + ceil(rows/64) *
  * ceil(cols/64)), in job order; `ntiles` is the total. */
 typedef struct dfu_transpose_job {
@@ -167,6 +170,7 @@ typedef struct dfu_transpose_job {
   void* dst;
   int32_t rows, cols;
   int32_t tile0;
+  int32_t ld_src, ld_dst;
   int32_t pad_;
 } dfu_transpose_job;
 int dfu_transpose_bf16(const dfu_transpose_job* jobs, int32_t njobs, int32_t ntiles,

@@ -205,14 +205,17 @@ def test_vit_dgrad_on_transposed_shadow_is_bitwise_equal():
         assert torch.equal(w._dfu_shadow_T, w._dfu_shadow.t())
 
 
-def test_resnet_stage_with_channels_last_conv_weights_is_bitwise_equal():
+def test_resnet_stage_with_channels_last_conv_weights_is_bitwise_equal(monkeypatch):
     """FusedAdamW stores the 3x3 conv weights channels-last (KRSC, optim.FlatParams): the
     forward reads the bf16 shadow as the GEMM operand and the weight-gradient GEMM accumulates
     straight into p.grad.  Against unmanaged weights (per-call OIHW -> KRSC packing, gradient
     permute-added from a scratch buffer) every gradient and output is bitwise equal, before and
-    after an optimizer step."""
+    after an optimizer step (the stride-1 dgrads on their dgrad loaders here, as unmanaged
+    weights run them: test_stride1_dgrad_on_flipped_weights covers the forward-conv form)."""
     from models.resnet import resnet50
+    from dfu_hip import functional as Fn
     from dfu_hip.optim import FusedAdamW
+    monkeypatch.setattr(Fn, "_DGRAD_FLIP", False)
     torch.manual_seed(0)
     a = resnet50(num_classes=0).to(DEV).train()
     b = resnet50(num_classes=0).to(DEV).train()
@@ -246,3 +249,49 @@ def test_resnet_stage_with_channels_last_conv_weights_is_bitwise_equal():
             if isinstance(bn_a, torch.nn.BatchNorm2d):
                 bn_b.running_mean.copy_(bn_a.running_mean)
                 bn_b.running_var.copy_(bn_a.running_var)
+
+
+def test_stride1_dgrad_on_flipped_weights(monkeypatch):
+    """The stride-1 3x3 conv input gradients of FusedAdamW-managed weights run as forward
+    convolutions of dY with the flipped channel-transposed bf16 copy W'[c][r][s][k] =
+    W[k][2-r][2-s][c] (optim.FlatParams.add_flipped, refreshed in the optimizer's batched
+    transpose launch): the copy equals the flip of the shadow after each step; outputs are
+    unchanged and every gradient matches the dgrad-loader form to fp32 summation-order rounding
+    of the bf16 input gradients (relative L2 < 1e-2) and a torch fp32 conv2d_input (< 2e-2)."""
+    from models.resnet import resnet50
+    from dfu_hip import functional as Fn
+    from dfu_hip.optim import FusedAdamW
+    torch.manual_seed(0)
+    net = resnet50(num_classes=0).to(DEV).train()
+    stage = net.layer3  # 5 stride-1 3x3 convs, 14x14, 256 channels
+    opt = FusedAdamW(stage.parameters(), lr=1e-3, weight_decay=1e-4)
+    x0 = torch.randn(4, 512, 28, 28, device=DEV).contiguous(memory_format=torch.channels_last)
+    for step in range(2):
+        res = []
+        for flip in (False, True):
+            monkeypatch.setattr(Fn, "_DGRAD_FLIP", flip)
+            opt.zero_grad()
+            y = stage(x0)
+            Rg = torch.randn(y.shape, device=DEV,
+                             generator=torch.Generator(device=DEV).manual_seed(step))
+            (y.float() * Rg).sum().backward()
+            res.append((y.detach().float(), [p.grad.clone() for p in stage.parameters()]))
+        torch.cuda.synchronize()
+        assert torch.equal(res[0][0], res[1][0]), "forward changed"
+        for (n, _), g0, g1 in zip(stage.named_parameters(), res[0][1], res[1][1]):
+            assert rel(g1, g0) < 1e-2, (step, n, rel(g1, g0))
+        w = stage[1].conv2.weight
+        f = w._dfu_shadow_F.view(256, 3, 3, 256)
+        kr = w._dfu_shadow.view(256, 3, 3, 256)  # [k][r][s][c]
+        assert torch.equal(f, kr.flip(1, 2).permute(3, 1, 2, 0)), step
+        opt.step()
+    # the forward-conv form against torch on one conv
+    w = stage[1].conv2.weight
+    dy = torch.randn(4, 256, 14, 14, device=DEV).to(torch.bfloat16)
+    g = Fn._geom(stage[1].conv2, 4, 14, 14)
+    dx = torch.empty(4 * 14 * 14, 256, dtype=torch.bfloat16, device=DEV)
+    Fn.conv_dgrad(Fn.rows_view(Fn.nhwc_bf16(dy)), g, None, dx,
+                  w_flip=Fn.conv_weight_flipped(w))
+    wb = Fn.weight_bf16_rows(w).view(256, 3, 3, 256).permute(0, 3, 1, 2).float()
+    ref = torch.nn.grad.conv2d_input((4, 256, 14, 14), wb, dy.float(), padding=1)
+    assert rel(dx.view(4, 14, 14, 256).permute(0, 3, 1, 2), ref) < 2e-2
