@@ -164,6 +164,9 @@ def wgrad_stream(device):
 
 
 _concurrent_encoders = [0]
+# DFU_VIT_WGRAD_BESIDE_FUSED=1: the ViT weight gradients run on the wgrad stream also while the
+# ResNet branch runs concurrently (A/B; default: inline on the ViT's own stream there)
+_WGRAD_BESIDE_FUSED = os.environ.get("DFU_VIT_WGRAD_BESIDE_FUSED", "0") != "0"
 
 
 class concurrent_encoders:
@@ -962,7 +965,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
-        ctx.beside = _VIT_WGRAD_STREAM and _concurrent_encoders[0] == 0
+        ctx.beside = _VIT_WGRAD_STREAM and (_concurrent_encoders[0] == 0 or _WGRAD_BESIDE_FUSED)
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
@@ -1010,7 +1013,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
-        ctx.beside = _VIT_WGRAD_STREAM and _concurrent_encoders[0] == 0
+        ctx.beside = _VIT_WGRAD_STREAM and (_concurrent_encoders[0] == 0 or _WGRAD_BESIDE_FUSED)
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
