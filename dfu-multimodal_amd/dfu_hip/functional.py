@@ -105,9 +105,31 @@ def grad_buffer(p):
         ops.zero_(g)
         p.grad = g
     if g.is_cuda:
-        st = torch.cuda.current_stream(g.device)
-        _grad_streams[(st.device_index, st.stream_id)] = st
+        st = _current_stream_obj(g)
+        _grad_streams[id(st)] = st
+        # this step's producer stream of p's gradient (False: more than one), for FusedAdamW's
+        # early update of parameters whose gradients are final on a side stream
+        prev = getattr(p, "_dfu_grad_stream", None)
+        p._dfu_grad_stream = st if prev is None or prev is st else False
     return g
+
+
+_stream_objs = {}
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _current_stream_obj(t):
+    """The current stream of t's device as one cached torch Stream per raw HIP stream (the
+    per-call torch.cuda.current_stream() object costs ~8 us of host time; this is called for
+    every parameter gradient of the step)."""
+    if _raw_stream is None:
+        return torch.cuda.current_stream(t.device)
+    idx = t.get_device()
+    raw = _raw_stream(idx)
+    st = _stream_objs.get(raw)
+    if st is None:
+        st = _stream_objs[raw] = torch.cuda.current_stream(t.device)
+    return st
 
 
 def join_grad_streams(stream=None, clear=True):

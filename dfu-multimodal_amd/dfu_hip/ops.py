@@ -19,7 +19,15 @@ def lib():
     return L.load()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream_ptr():
+    """The current HIP stream of the current device (the raw-pointer query: torch.cuda.
+    current_stream() builds a Stream object per call, ~8 us of host time x ~260 calls a step)."""
+    if _raw_stream is not None and _cur_device is not None:
+        return ctypes.c_void_p(_raw_stream(_cur_device()))
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 

@@ -23,12 +23,20 @@ view) and ``p.grad`` into a matching flat gradient buffer, so:
     (functional.weight_bf16_rows); edits through ``p.data`` bypass that counter — call
     ``FlatParams.refresh_shadow()`` after those.
 """
+import os
+
 import torch
+import torch.distributed as dist
 
 from . import functional as Fn
 from . import ops
 
 _ALIGN = 4  # elements (16 B) so every tensor view starts 16-byte aligned
+
+
+def _dp_world():
+    """Whether this process is one rank of a multi-rank process group."""
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
 def _aligned(n):
@@ -142,6 +150,15 @@ class FlatParams:
     def grad_view(self, i):
         return self.view(self.grad, i)
 
+    def needs_rebind(self):
+        """Host-side check: has user code replaced or cleared any p.grad?"""
+        base = self.grad.data_ptr()
+        for p, o in zip(self.params, self.offsets):
+            g = p.grad
+            if g is None or g.data_ptr() != base + 4 * o:
+                return True
+        return False
+
     def rebind_grads(self):
         """Re-attach p.grad to the flat buffer if user code replaced or cleared it (eager)."""
         for i, p in enumerate(self.params):
@@ -171,23 +188,75 @@ class FusedAdamW(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
         self.step_dev = torch.zeros((), dtype=torch.int64, device=dev)
         self.check_grads = True  # set False inside captured graphs (pointers are static)
+        # update a side stream's parameter block on that stream (step); DFU_EARLY_ADAMW=0: off
+        self.early_update = os.environ.get("DFU_EARLY_ADAMW", "1") != "0"
 
     def zero_grad(self, set_to_none=True):
         # gradients stay bound to the flat buffer (stable addresses); one memset clears them
         ops.zero_(self.flat.grad)
 
-    @torch.no_grad()
-    def step(self, closure=None):
-        loss = closure() if closure is not None else None
-        Fn.join_grad_streams()
-        if self.check_grads:
-            self.flat.rebind_grads()
+    def _early_range(self, cur):
+        """(lo, hi, stream): the largest run of parameters, contiguous in the flat buffers, whose
+        gradients this step were all produced on one stream other than `cur` (the concurrent ViT
+        branch's side stream in the fusion step), or None."""
+        best, run = None, None
+        fp = self.flat
+        for i, p in enumerate(fp.params):
+            st = getattr(p, "_dfu_grad_stream", None)
+            st = st if st is not None and st is not False and st != cur else None
+            lo, hi = fp.offsets[i], fp.offsets[i] + _aligned(p.numel())
+            if st is not None and run is not None and run[2] == st and run[1] == lo:
+                run = (run[0], hi, st)
+            else:
+                run = (lo, hi, st) if st is not None else None
+            if run is not None and (best is None or run[1] - run[0] > best[1] - best[0]):
+                best = run
+        return best if best is not None and best[1] - best[0] >= (1 << 20) else None
+
+    def _adamw(self, lo, hi):
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        ops.step_increment(self.step_dev)
-        ops.adamw_flat(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, g["lr"], b1,
-                       b2, g["eps"], g["weight_decay"], self.step_dev, shadow=self.flat.shadow)
-        self.flat.shadows_rewritten()
+        fp = self.flat
+        ops.adamw_flat(fp.data[lo:hi], fp.grad[lo:hi], self.exp_avg[lo:hi],
+                       self.exp_avg_sq[lo:hi], g["lr"], b1, b2, g["eps"], g["weight_decay"],
+                       self.step_dev, shadow=None if fp.shadow is None else fp.shadow[lo:hi])
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        """One AdamW update of every parameter.  Where a contiguous block of parameters got its
+        gradients on a side stream (the fusion step's ViT branch), that block is updated on that
+        stream as soon as its backward is done -- beside the other branch's backward tail --
+        and the rest after every gradient stream is joined (single process only: under data
+        parallelism the gradients are final only after the all-reduce)."""
+        loss = closure() if closure is not None else None
+        fp = self.flat
+        early = None
+        # host-side check first: the rebinding copies (and their per-parameter views) only when
+        # user code replaced a gradient
+        rebind = self.check_grads and fp.needs_rebind()
+        if self.early_update and fp.data.is_cuda and not _dp_world() and not rebind:
+            early = self._early_range(torch.cuda.current_stream(fp.data.device))
+        if early is not None:
+            lo, hi, st = early
+            cur = torch.cuda.current_stream(fp.data.device)
+            with torch.cuda.stream(st):
+                ops.step_increment(self.step_dev)  # the rest runs after the join: sees it
+                self._adamw(lo, hi)
+            cur.wait_stream(st)  # the rest, the step counter and the shadow transposes after it
+        Fn.join_grad_streams()
+        if rebind:
+            fp.rebind_grads()
+        if early is None:
+            ops.step_increment(self.step_dev)
+            self._adamw(0, fp.numel)
+        else:
+            for a, b in ((0, early[0]), (early[1], fp.numel)):
+                if b > a:
+                    self._adamw(a, b)
+        for p in fp.params:
+            p._dfu_grad_stream = None
+        self.last_early = None if early is None else early[:2]
+        fp.shadows_rewritten()
         return loss
 
     def state_dict(self):

@@ -54,3 +54,42 @@ def test_adamw_matches_torch_and_shadow_tracks():
     err = (y.float() - ref_y).norm() / ref_y.norm()
     assert err < 2e-2, err.item()
     assert torch.equal(m[0].weight._dfu_shadow, sd["0.weight"].to(torch.bfloat16))
+
+
+def test_early_adamw_on_side_stream_is_bitwise_equal():
+    """In the two-stream fusion step the ViT branch's parameters get their AdamW update on the
+    ViT side stream as soon as its backward is done (FusedAdamW.step early block), the rest
+    after the join: parameters, moments, bf16 shadows and the ViT transposed shadows after two
+    steps equal the single-launch update bit for bit, and the early block is the ViT's."""
+    import bench
+    from dfu_hip import nn as hnn
+    from dfu_hip.optim import FusedAdamW
+    dev = torch.device("cuda", 0)
+    res = []
+    from models.fusion import MultimodalFusionModel
+    for early in (False, True):
+        torch.manual_seed(0)
+        model = MultimodalFusionModel(num_classes=2, dropout=0.0).to(dev).train()
+        fwd = lambda m, r, t: m(r, t)  # noqa: E731
+        opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
+        opt.early_update = early
+        crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
+        rgb, th, y = bench.synthetic(4, dev, seed=3)
+        for _ in range(2):
+            opt.zero_grad()
+            crit(fwd(model, rgb, th), y).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        if early:
+            lo, hi = opt.last_early
+            vit = [i for i, p in enumerate(opt.flat.params)
+                   if any(p is q for q in model.vit.parameters())]
+            assert opt.flat.offsets[vit[0]] == lo and hi - lo >= 85_000_000
+        else:
+            assert opt.last_early is None
+        tq = model.vit.blocks[0].mlp.fc1.weight
+        res.append([opt.flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(),
+                    opt.flat.shadow.clone(), getattr(tq, "_dfu_shadow_T").clone(),
+                    opt.step_dev.clone()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
