@@ -260,7 +260,7 @@ class TransposeJobs:
         self.pairs = list(pairs)  # keep the buffers alive as long as the table
         self.njobs, self.ntiles = len(self.pairs), tile0
         dev = self.pairs[0][0].device
-        self.table = torch.frombuffer(bytes(raw), dtype=torch.uint8).to(dev)
+        self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
 
     def launch(self):
         check(lib().dfu_transpose_bf16(ptr(self.table), self.njobs, self.ntiles, stream_ptr()),
