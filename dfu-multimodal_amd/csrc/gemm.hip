@@ -375,6 +375,13 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
                   d->a_mode, d->b_mode, d->epilogue, d->tile);
     return DFU_E_UNSUPPORTED;
   }
+  if (d->epilogue == DFU_EPI_BF16_DGELU && d->stats != nullptr && pl.tile != T256x256ps) {
+    // the dGELU column sums exist in the persistent phased 256x256 epilogue only; the caller
+    // then sums the columns itself
+    dfu_set_error("dfu_gemm: dGELU column sums need the persistent 256x256 tile (plan: %d)",
+                  pl.tile + 1);
+    return DFU_E_UNSUPPORTED;
+  }
   DFU_CHECK_ARG(((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0,
                 "dfu_gemm: A and B must be 16-byte aligned");
   if (d->a_mode == DFU_OPND_KMAJOR || d->a_mode == DFU_OPND_MNMAJOR)

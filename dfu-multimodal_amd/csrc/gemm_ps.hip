@@ -110,7 +110,9 @@ DFU_DEV int ps_epi_stores(const GemmArgs& p) {
   constexpr bool bf16_out = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_GELU ||
                             EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD;
   const int per = bf16_out && p.n8 ? 16 : 32 * (p.n4 ? 1 : 4);
-  return EPI == DFU_EPI_BF16_GELU ? 2 * per : per;
+  // dGELU with column sums (p.stats): four more 16-B stores per wave (scalar: sixteen)
+  const int cs = EPI == DFU_EPI_BF16_DGELU && p.stats ? (p.n4 ? 4 : 16) : 0;
+  return (EPI == DFU_EPI_BF16_GELU ? 2 * per : per) + cs;
 }
 
 // lane holds C[m0 + (i>>2)*128 + wr*64 + (i&3)*16 + (lane&15)]
@@ -123,6 +125,15 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
   const rsrc_t rc = make_rsrc(p.C);
   const rsrc_t ra = make_rsrc(p.aux);
   const rsrc_t ro = make_rsrc(p.aux_out);
+  // dGELU + p.stats: per-column sums of the stored (bf16) values over this wave's 128 rows,
+  // the bias gradient of the Linear whose output gradient this is (timm Mlp fc1.bias)
+  float cs[2][2][4];
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[hb][jj][r] = 0.f;
   float bias[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -175,6 +186,12 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
           for (int r = 0; r < 4; ++r)
             v[jj][r] = EPI == DFU_EPI_BF16_DGELU ? v[jj][r] * x[r] : v[jj][r] + x[r];
         }
+        if constexpr (EPI == DFU_EPI_BF16_DGELU) {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[hb][jj][r] += okm ? bf2f(f2bf(v[jj][r])) : 0.f;
+        }
         st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
       } else if constexpr (EPI == DFU_EPI_F32_ACC) {  // split-K slab, or C += acc unsplit
 #pragma unroll
@@ -201,6 +218,23 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
           st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
         }
       }
+    }
+  }
+  if constexpr (EPI == DFU_EPI_BF16_DGELU) {
+    if (p.stats) {  // row (m0 / 256) * 2 + wr of the [2 * tiles_m][N] partial slab
+      const rsrc_t rs = make_rsrc(p.stats);
+      const int64_t prow = (int64_t)(m0 / 256) * 2 + wr;
+      const bool lead = (lane & 15) == 0;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          float t[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[r] = row16_sum(cs[hb][jj][r]);
+          const int n = n0 + hb * 128 + wc * 32 + jj * 16 + 4 * (lane >> 4);
+          st4_f32(rs, prow * N + n, lead, n, N, n4, t);
+        }
     }
   }
 }

@@ -941,6 +941,10 @@ def _linear_dgrad(rows, N, K, g, weight, w_rows, out, epilogue=L.EPI_BF16, **kw)
                  **kw)
 
 
+# fc1.bias gradient from the dGELU epilogue's column sums (DFU_DGELU_COLSUM=0: a colsum pass)
+_DGELU_COLSUM = os.environ.get("DFU_DGELU_COLSUM", "1") != "0"
+
+
 class ViTBlockFn(torch.autograd.Function):
     """timm Block (pre-norm, qkv_bias, SDPA, exact GELU, no LayerScale, drop_path 0)."""
 
@@ -1070,23 +1074,40 @@ class ViTBlockFn(torch.autograd.Function):
         bw = _Beside(wgrad_stream(dev) if (ctx.beside and g.is_cuda) else None)
         red_w = ops.PartialReductions() if bw.ws is not None else red
 
-        def wgrad(lin, dy, x, width=None):
+        def wgrad(lin, dy, x, width=None, partial=None):
             def fn():
                 if _wants(lin.weight):
                     _linear_wgrad(dy, x, lin.weight, rows)
                 if width is not None and _wants(lin.bias):
-                    red_w.add(ops.colsum_partial(dy), grad_buffer(lin.bias), width)
+                    red_w.add(ops.colsum_partial(dy) if partial is None else partial,
+                              grad_buffer(lin.bias), width)
                 grads_done(lin.weight)
-            bw.run(fn, dy, x)
+            bw.run(fn, dy, x, *(() if partial is None else (partial,)))
 
         # ---- MLP branch: x_out = x_mid + fc2(gelu(fc1(norm2(x_mid))))
         wgrad(mlp.fc2, gb, h)
         dh_pre = _empty((rows, Dh), BF16, dev)
-        _linear_dgrad(rows, Dh, D, gb, mlp.fc2.weight, wfc2, dh_pre, epilogue=L.EPI_BF16_DGELU,
-                      aux=dgl, ldaux=Dh)
+        # fc1.bias's gradient = column sums of dh_pre: reduced in the dGELU epilogue (per 128-row
+        # half of each 256-row tile) where the plan is the persistent 256x256 tile, else a pass
+        # (when the ViT runs alone: inside the two-stream fusion step the longer dGELU GEMM on
+        # the ViT's critical stream measured 0.07 ms slower per step than the separate pass,
+        # thermal-only 0.13 ms faster)
+        cs1 = None
+        if _DGELU_COLSUM and ctx.beside and _wants(mlp.fc1.bias) and g.is_cuda:
+            cs1 = _empty((2 * ((rows + 255) // 256), Dh), F32, dev)
+            try:
+                _linear_dgrad(rows, Dh, D, gb, mlp.fc2.weight, wfc2, dh_pre,
+                              epilogue=L.EPI_BF16_DGELU, aux=dgl, ldaux=Dh, stats=cs1)
+            except L.DfuError as e:
+                if e.code != L.DFU_E_UNSUPPORTED:
+                    raise
+                cs1 = None
+        if cs1 is None:
+            _linear_dgrad(rows, Dh, D, gb, mlp.fc2.weight, wfc2, dh_pre,
+                          epilogue=L.EPI_BF16_DGELU, aux=dgl, ldaux=Dh)
         if _wants(mlp.fc2.bias):
             _colsum_of_grad(gout if gout.dtype == F32 else g, grad_buffer(mlp.fc2.bias), red)
-        wgrad(mlp.fc1, dh_pre, xn2, Dh)
+        wgrad(mlp.fc1, dh_pre, xn2, Dh, partial=cs1)
         dxn2 = _empty((rows, D), BF16, dev)
         _linear_dgrad(rows, D, Dh, dh_pre, mlp.fc1.weight, wfc1, dxn2)
         gmb = _empty((rows, D), BF16, dev)

@@ -55,7 +55,11 @@ enum dfu_epilogue {
   DFU_EPI_BF16_GELU = 2,     /* pre = acc + bias: C bf16 = gelu(pre), aux_out bf16 = gelu'(pre) */
   DFU_EPI_F32 = 3,           /* C f32 = alpha*acc + bias                                    */
   DFU_EPI_F32_RESID = 4,     /* C f32 = aux f32 + alpha*acc + bias  (residual stream)       */
-  DFU_EPI_BF16_DGELU = 5,    /* C bf16 = acc * aux bf16 (aux = the GELU epilogue's gelu')   */
+  DFU_EPI_BF16_DGELU = 5,    /* C bf16 = acc * aux bf16 (aux = the GELU epilogue's gelu');
+                                with `stats`: also the column sums of the stored C over each
+                                128-row half of every 256-row tile, fp32 [2*ceil(M/256)][N]
+                                (the bias gradient's partials; persistent 256x256 tile only,
+                                DFU_E_UNSUPPORTED otherwise)                                 */
   DFU_EPI_BF16_ADD = 6,      /* C bf16 = acc + aux bf16                                     */
   DFU_EPI_F32_ACC = 7,       /* C f32 += acc   (split-K: fp32 slabs + reduce, or atomics)   */
   DFU_EPI_F32_ACC_CONVW = 8, /* retired: conv wgrad accumulates KRSC + dfu_conv_grad_krsc... */

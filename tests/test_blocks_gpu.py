@@ -168,11 +168,15 @@ def test_transpose_bf16(shape):
     assert torch.equal(outs[0], x.t()) and torch.equal(outs[1], y.t())
 
 
-def test_vit_dgrad_on_transposed_shadow_is_bitwise_equal():
+def test_vit_dgrad_on_transposed_shadow_is_bitwise_equal(monkeypatch):
     """The ViT input-gradient GEMMs read the weight K-contiguous from the transposed bf16 shadow
     (FusedAdamW-managed weights, functional.weight_bf16_T) or MN-major from the shadow itself:
     the same products in the same K order, so every gradient is bitwise equal; after an
     optimizer step the batched transpose keeps the copy current."""
+    from dfu_hip import functional as Fn
+    # fc1.bias by the colsum pass on both sides (the dGELU epilogue sums exist on one tile only,
+    # and the two operand layouts may be planned on different tiles)
+    monkeypatch.setattr(Fn, "_DGELU_COLSUM", False)
     from models.vit import vit_base_patch16_224
     from dfu_hip.optim import FusedAdamW
     torch.manual_seed(0)

@@ -303,3 +303,33 @@ def test_conv_tail_split(case):
         a, b = a.float(), b.float()
         assert ((a - b).abs() <= 2e-2 * (1 + b.abs())).all(), (a - b).abs().max().item()
     assert int(ops.tile_counters(x.device).abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(12608, 3072, 768), (1000, 768, 256)])
+def test_dgelu_column_sums(M, N, K):
+    """dGELU epilogue with `stats` on the persistent 256x256 tile: besides C = bf16(acc * aux),
+    fp32 column sums of the stored C over each 128-row half of every 256-row tile (the fc1 bias
+    gradient's partials, ViTBlockFn.backward); other tiles refuse the request."""
+    A = drnd(M, K, seed=70)
+    B = drnd(N, K, seed=71)
+    aux = drnd(M, N, seed=72)
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    parts = torch.full((2 * ((M + 255) // 256), N), float("nan"), device=DEV)
+    ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_DGELU, aux=aux, ldaux=N,
+             stats=parts, tile=8)
+    ref = torch.empty_like(C)
+    ops.gemm(M, N, K, A, K, B, K, ref, N, epilogue=L.EPI_BF16_DGELU, aux=aux, ldaux=N, tile=8)
+    assert torch.equal(C, ref), "the column sums changed the stored output"
+    # the halves: rows [256 t + 128 h + 64 w .. ] -- wave row w of tile t covers rows
+    # 256 t + {0..63, 128..191} (w = 0) and {64..127, 192..255} (w = 1)
+    Cf = torch.zeros(parts.shape[0] // 2 * 256, N, device=DEV)
+    Cf[:M] = C.float()
+    blk = Cf.view(-1, 2, 2, 64, N)  # [tile][h][w][64 rows][N]
+    want = blk.sum(dim=(1, 3)).reshape(-1, N)  # [tile * 2 + w][N]
+    torch.cuda.synchronize()
+    assert not torch.isnan(parts).any()
+    assert torch.allclose(parts, want, rtol=1e-5, atol=1e-3 * (1 + want.abs().max().item()) * 1e-2)
+    assert torch.allclose(parts.sum(0), C.float().sum(0), rtol=1e-4, atol=1e-2)
+    with pytest.raises(L.DfuError):
+        ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16_DGELU, aux=aux, ldaux=N,
+                 stats=parts, tile=1)
