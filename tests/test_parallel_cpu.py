@@ -52,7 +52,9 @@ def _worker(rank, port, overlap, q):
         red.close()
         data = torch.cat([p.detach().reshape(-1) for p in flat.params])
         grads = torch.cat([p.grad.reshape(-1) for p in flat.params])
-        q.put((rank, data, grads, None))
+        # numpy arrays travel pickled by value (a tensor would pass a shared-memory handle that
+        # dies with this process if it exits before the parent has read it)
+        q.put((rank, data.numpy(), grads.numpy(), None))
     except Exception as e:  # report to the parent instead of hanging it
         q.put((rank, None, None, repr(e)))
     finally:
@@ -72,7 +74,7 @@ def test_grad_allreduce_world2(overlap):
     for _ in range(WORLD):
         rank, data, grads, err = q.get(timeout=120)
         assert err is None, f"rank {rank}: {err}"
-        res[rank] = (data, grads)
+        res[rank] = (torch.from_numpy(data), torch.from_numpy(grads))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
