@@ -26,6 +26,7 @@ sum_b output[b, 0]; in eval mode the images are independent, so each map equals 
 """
 import torch
 
+from dfu_hip import functional as Fn
 from dfu_hip import ops
 
 
@@ -77,6 +78,9 @@ class GradCAM:
             out = self.model(x)
             self.model.zero_grad()
             out[:, 0].sum().backward()
+        # the ViT blocks' weight gradients may run on the wgrad stream: join it (a graph capture
+        # rejects unjoined work, and the next forward's weight reads must follow it)
+        Fn.join_grad_streams()
         name = self.target_name()
         if name is None:
             return None
