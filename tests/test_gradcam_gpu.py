@@ -155,3 +155,42 @@ def test_gradcam_maps_match_reference_restatement(B):
     # the reference signature: (1, C, H, W) -> numpy map
     one = cam_rgb.generate_cam(rgb[:1].to(DEV))
     assert one.shape == (7, 7) and math.isclose(float(one.max()), 1.0, rel_tol=1e-6)
+
+
+def test_gradcam_step_replays_from_a_hip_graph():
+    """The C5 step (bench.py --config gradcam) captured into one HIP graph: the capture must
+    succeed (every side / weight-gradient stream joined before it ends) and a replay must
+    reproduce the eager maps."""
+    from models.fusion import MultimodalFusionModel
+    from models.gradcam import GradCAM
+    torch.manual_seed(5)
+    model = MultimodalFusionModel(num_classes=2, dropout=0.7).to(DEV).eval()
+    rgb, th, _ = R.synthetic_batch(4, seed=41)
+    rgb, th = rgb.to(DEV), th.to(DEV)
+    cam_rgb, cam_th = GradCAM(model.resnet, ["layer4"]), GradCAM(model.vit, ["blocks"])
+    outs = {}
+
+    def step():
+        with torch.no_grad():
+            outs["pred"] = torch.softmax(model(rgb, th), dim=1).argmax(1)
+        outs["cam"] = cam_rgb.generate_cams(rgb)
+        outs["sal"] = cam_th.generate_cams(th)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    ref = {k: v.clone() for k, v in outs.items()}
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    for k in outs:
+        outs[k].zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(outs["pred"], ref["pred"])
+    assert torch.allclose(outs["cam"], ref["cam"], atol=1e-5)
+    assert torch.allclose(outs["sal"], ref["sal"], atol=1e-5)
