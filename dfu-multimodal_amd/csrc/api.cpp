@@ -26,3 +26,56 @@ extern "C" int dfu_zero(void* ptr, int64_t bytes, void* stream) {
   }
   return DFU_OK;
 }
+
+// Recovery after a failed HIP-graph capture (dfu_hip.graphs): when the origin stream's
+// hipStreamEndCapture fails on unjoined work, the capture is NOT ended -- the origin and every
+// stream forked into it stay in capture mode, and the next eager call that touches the legacy
+// stream (an allocation, an event) fails.  Join every capturing stream into every other one
+// (events recorded inside the capture), then end the capture on each (only the origin's end
+// succeeds; the others return hipErrorStreamCaptureUnmatched) and drop the partial graphs.
+extern "C" int dfu_streams_abort_capture(void* const* streams, int32_t n,
+                                         int32_t* still_capturing) {
+  if (still_capturing) *still_capturing = 0;
+  if (n <= 0 || streams == nullptr) return DFU_OK;
+  if (n > 64) {
+    dfu_set_error("dfu_streams_abort_capture: at most 64 streams");
+    return DFU_E_INVALID;
+  }
+  hipStream_t cap[64];
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)streams[i], &st) == hipSuccess &&
+        st != hipStreamCaptureStatusNone)
+      cap[m++] = (hipStream_t)streams[i];
+  }
+  hipEvent_t ev[64];
+  for (int i = 0; i < m; ++i) {
+    ev[i] = nullptr;
+    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess)
+      (void)hipEventRecord(ev[i], cap[i]);
+  }
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j)
+      if (i != j && ev[j] != nullptr) (void)hipStreamWaitEvent(cap[i], ev[j], 0);
+  for (int pass = 0; pass < 2; ++pass)
+    for (int i = 0; i < m; ++i) {
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(cap[i], &st) != hipSuccess || st == hipStreamCaptureStatusNone)
+        continue;
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(cap[i], &g);
+      if (g != nullptr) (void)hipGraphDestroy(g);
+    }
+  for (int i = 0; i < m; ++i)
+    if (ev[i] != nullptr) (void)hipEventDestroy(ev[i]);
+  int left = 0;
+  for (int i = 0; i < m; ++i) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(cap[i], &st) == hipSuccess && st != hipStreamCaptureStatusNone)
+      ++left;
+  }
+  (void)hipGetLastError();  // the failed ends above are the expected outcome
+  if (still_capturing) *still_capturing = left;
+  return DFU_OK;
+}

@@ -461,6 +461,181 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
   }
 }
 
+// ------------------------------------------------------------------ bf16x3 forward
+// fp32-accurate attention for the "bf16x3" precision mode (include/dfu_hip.h): the same MFMA
+// dataflow as k_attn_fwd on split operands x = hi + lo (hi = bf16(x), lo = bf16(x - hi)):
+//   S^T = Khi Qhi^T + Khi Qlo^T + Klo Qhi^T,   O^T = Vhi^T Phi^T + Vhi^T Plo^T + Vlo^T Phi^T
+// with the softmax in fp32 between them, i.e. every product keeps 16 mantissa bits (the
+// dropped lo*lo term and the split remainders are ~2^-17 relative per product, against
+// bf16's 2^-9).  One 8-wave workgroup per (b, h): K and V are read from the fp32 qkv GEMM
+// output and split into four r128 LDS images while staging; each wave owns query tiles
+// wave, wave + 8.  The kernel also writes the plain bf16 copy of qkv (hi: the bf16 backward's
+// operand; every element is read exactly once here), o as the A-operand triple
+// [hi | lo | hi] of the proj GEMM, o bf16 and the LSE, exactly as k_attn_fwd's.
+DFU_DEV void split_f4(const f32x4 v, u32x2& hi, u32x2& lo) {
+  hi = (u32x2){pack2(v[0], v[1]), pack2(v[2], v[3])};
+  const f32x4 r = {v[0] - lo_bf(hi[0]), v[1] - hi_bf(hi[0]), v[2] - lo_bf(hi[1]),
+                   v[3] - hi_bf(hi[1])};
+  lo = (u32x2){pack2(r[0], r[1]), pack2(r[2], r[3])};
+}
+
+template <int KT>
+__global__ __launch_bounds__(512) void k_attn_fwd_x3(const float* __restrict__ qkv, int N, int H,
+                                                     float scale, int npad,
+                                                     bf16_t* __restrict__ qkv_bf,
+                                                     bf16_t* __restrict__ o3,
+                                                     bf16_t* __restrict__ o_bf,
+                                                     float* __restrict__ lse) {
+  constexpr int NPAD = KT * 16;
+  constexpr int IMG = NPAD * 128;
+  constexpr int NTH = 512, NW = 8;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // K hi, K lo, V hi, V lo
+  char* Kh = smem;
+  char* Kl = smem + IMG;
+  char* Vh = smem + 2 * IMG;
+  char* Vl = smem + 3 * IMG;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * 64;
+  const int64_t tok = (int64_t)3 * D;
+  const float* base = qkv + (int64_t)b * N * tok + h * 64;
+  bf16_t* bbase = qkv_bf ? qkv_bf + (int64_t)b * N * tok + h * 64 : nullptr;
+  // staging, one tensor at a time (K, then V): 16 float4 per row; every load of the tensor
+  // issued before any conversion
+  constexpr int IT = (NPAD * 16 + NTH - 1) / NTH;
+#pragma unroll
+  for (int which = 1; which <= 2; ++which) {
+    char* dh = which == 1 ? Kh : Vh;
+    char* dl = which == 1 ? Kl : Vl;
+    f32x4 v[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int idx = tid + i * NTH, row = idx >> 4, c4 = idx & 15;
+      const int64_t o = (int64_t)(row < N ? row : N - 1) * tok + 4 * c4;
+      v[i] = *(const f32x4*)(base + which * D + o);
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int idx = tid + i * NTH, row = idx >> 4, c4 = idx & 15;
+      if (idx < NPAD * 16) {
+        const bool in = row < N;
+        const int off = r128_off(row, c4 >> 1) + (c4 & 1) * 8;
+        u32x2 hi, lo;
+        split_f4(v[i], hi, lo);
+        const u32x2 z = {0u, 0u};
+        *(u32x2*)(dh + off) = in ? hi : z;
+        *(u32x2*)(dl + off) = in ? lo : z;
+        if (bbase && in) *(u32x2*)(bbase + (int64_t)row * tok + which * D + 4 * c4) = hi;
+      }
+    }
+  }
+  __syncthreads();
+  const float c = scale * LOG2E;
+  const int QT = (N + 15) / 16;
+  for (int qt = wave; qt < QT; qt += NW) {
+    const int q = qt * 16 + (lane & 15);
+    const bool qvalid = q < N;
+    bf16x8 qh[2], ql[2];
+    {
+      const int64_t qo = (int64_t)(qvalid ? q : N - 1) * tok + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const f32x4 a = *(const f32x4*)(base + qo + 32 * ks);
+        const f32x4 bq = *(const f32x4*)(base + qo + 32 * ks + 4);
+        u32x2 ha, la, hb, lb;
+        split_f4(a, ha, la);
+        split_f4(bq, hb, lb);
+        qh[ks] = __builtin_bit_cast(bf16x8, (u32x4){ha[0], ha[1], hb[0], hb[1]});
+        ql[ks] = __builtin_bit_cast(bf16x8, (u32x4){la[0], la[1], lb[0], lb[1]});
+        if (bbase && qvalid)
+          *(u32x4*)(bbase + (int64_t)q * tok + 8 * g + 32 * ks) = (u32x4){ha[0], ha[1], hb[0], hb[1]};
+      }
+    }
+    f32x4 s[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 khf = row_frag(Kh, 16 * t, ks, lane);
+        const bf16x8 klf = row_frag(Kl, 16 * t, ks, lane);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(klf, qh[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(khf, ql[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(khf, qh[ks], acc, 0, 0, 0);
+      }
+      s[t] = acc;
+      // bound the scheduler's hoisting of later tiles' LDS reads (each is 8 VGPRs: hoisting
+      // them all spilled)
+      if (t % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      if (t >= KT - 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * t + 4 * g + r >= N) s[t][r] = -INFINITY;
+      }
+      mx = fmaxf(mx, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = fast_exp2(fmaf(s[t][r], c, -mx * c));
+        s[t][r] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 acc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < KT / 2; ++u) {
+      f32x4 r0, r1;
+      const bf16x8 ph = pack_frag(s[2 * u], s[2 * u + 1]);
+      {
+        const u32x4 w = __builtin_bit_cast(u32x4, ph);
+        r0 = (f32x4){s[2 * u][0] - lo_bf(w[0]), s[2 * u][1] - hi_bf(w[0]),
+                     s[2 * u][2] - lo_bf(w[1]), s[2 * u][3] - hi_bf(w[1])};
+        r1 = (f32x4){s[2 * u + 1][0] - lo_bf(w[2]), s[2 * u + 1][1] - hi_bf(w[2]),
+                     s[2 * u + 1][2] - lo_bf(w[3]), s[2 * u + 1][3] - hi_bf(w[3])};
+      }
+      const bf16x8 pl = pack_frag(r0, r1);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 vhf = tr_frag(Vh, u, 16 * dt, lane);
+        const bf16x8 vlf = tr_frag(Vl, u, 16 * dt, lane);
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vlf, ph, acc[dt], 0, 0, 0);
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vhf, pl, acc[dt], 0, 0, 0);
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vhf, ph, acc[dt], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (qvalid) {
+      const float inv = 1.0f / l;
+      const int64_t row = (int64_t)b * N + q;
+      const int col = h * 64 + 4 * g;
+      bf16_t* r3 = o3 + row * 3 * D + col;
+      bf16_t* rb = o_bf + row * D + col;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        u32x2 hi, lo;
+        split_f4(acc[dt] * inv, hi, lo);
+        *(u32x2*)(rb + 16 * dt) = hi;
+        *(u32x2*)(r3 + 16 * dt) = hi;
+        *(u32x2*)(r3 + D + 16 * dt) = lo;
+        *(u32x2*)(r3 + 2 * D + 16 * dt) = hi;
+      }
+      if (g == 0) lse[(int64_t)bh * npad + q] = mx * scale + logf(l);
+    }
+  }
+}
+
 #define DISPATCH_KT(KTV, CALL) \
   switch (KTV) {               \
     case 2: CALL(2); break;    \
@@ -501,6 +676,33 @@ extern "C" int dfu_attention_fwd(const void* qkv, int32_t B, int32_t N, int32_t 
   const int grid = BH < attn_cus() ? BH : attn_cus();  // persistent: one workgroup per CU
 #define CALL(K) hipLaunchKernelGGL(k_attn_fwd<K>, dim3(grid), dim3(512), 0, s, (const bf16_t*)qkv, N, H, BH, scale, (bf16_t*)o, lse)
   DISPATCH_KT(KT, CALL)
+#undef CALL
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_attention_fwd_f32(const float* qkv, int32_t B, int32_t N, int32_t H,
+                                     int32_t dh, float scale, int32_t npad, void* qkv_bf16,
+                                     void* o3, void* o_bf16, float* lse, void* stream) {
+  DFU_CHECK_ARG(qkv && o3 && o_bf16 && lse && B > 0 && H > 0,
+                "dfu_attention_fwd_f32: bad args");
+  DFU_CHECK_ARG(dh == 64, "dfu_attention_fwd_f32: head dim %d unsupported (64 only)", dh);
+  DFU_CHECK_ARG(N > 0 && N <= 224 && npad >= dfu_attention_npad(N),
+                "dfu_attention_fwd_f32: N=%d unsupported (<= 224) or npad %d < %d", N, npad,
+                dfu_attention_npad(N));
+  const int KT = dfu_attention_npad(N) / 16;
+  hipStream_t s = (hipStream_t)stream;
+#define CALL(K) hipLaunchKernelGGL(k_attn_fwd_x3<K>, dim3(B * H), dim3(512), 0, s, qkv, N, H, scale, npad, (bf16_t*)qkv_bf16, (bf16_t*)o3, (bf16_t*)o_bf16, lse)
+  switch (KT) {
+    case 2: CALL(2); break;
+    case 4: CALL(4); break;
+    case 6: CALL(6); break;
+    case 8: CALL(8); break;
+    case 10: CALL(10); break;
+    case 12: CALL(12); break;
+    case 14: CALL(14); break;
+    default: break;
+  }
 #undef CALL
   DFU_LAUNCH_CHECK();
   return DFU_OK;

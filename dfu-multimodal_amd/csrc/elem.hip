@@ -621,6 +621,21 @@ __global__ void k_argmax_rows(const float* __restrict__ x, int rows, int C,
   }
 }
 
+// torch.softmax(outputs, dim=1) of the reference's test phase (train_multimodal_fusion.py:477):
+// out[r][c] = exp(x[r][c] - max_r) / sum_c' exp(x[r][c'] - max_r), fp32 with expf.
+__global__ void k_softmax_rows(const float* __restrict__ x, int rows, int C,
+                               float* __restrict__ out) {
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += gridDim.x * blockDim.x) {
+    const float* xr = x + (int64_t)r * C;
+    float mx = xr[0];
+    for (int c = 1; c < C; ++c) mx = fmaxf(mx, xr[c]);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += expf(xr[c] - mx);
+    const float inv = 1.0f / s;
+    for (int c = 0; c < C; ++c) out[(int64_t)r * C + c] = expf(xr[c] - mx) * inv;
+  }
+}
+
 inline unsigned grid_for(int64_t n) {
   int64_t b = (n + TPB - 1) / TPB;
   if (b > 65536) b = 65536;
@@ -1022,6 +1037,13 @@ extern "C" int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t*
                                void* stream) {
   DFU_CHECK_ARG(x && out && rows > 0 && C > 0, "dfu_argmax_rows: bad args");
   LAUNCH(k_argmax_rows, (int64_t)rows, stream, x, rows, C, out);
+  return DFU_OK;
+}
+
+extern "C" int dfu_softmax_rows(const float* x, int32_t rows, int32_t C, float* out,
+                                void* stream) {
+  DFU_CHECK_ARG(x && out && rows > 0 && C > 0, "dfu_softmax_rows: bad args");
+  LAUNCH(k_softmax_rows, (int64_t)rows, stream, x, rows, C, out);
   return DFU_OK;
 }
 

@@ -289,130 +289,6 @@ __global__ void k_gelu_x3(const float* __restrict__ hpre, int64_t rows, int N,
   }
 }
 
-// ---------------------------------------------------------------- attention
-// fp32 softmax attention (F.scaled_dot_product_attention, timm Attention) for one (image, head)
-// and QB = 64 queries per workgroup: K and V of the head staged in LDS; wave w owns 16 queries,
-// lane = (query qi = lane & 15, key group kg = lane >> 4): the lane scores keys kg, kg+4, ...
-// against its query row held in registers, the softmax row statistics combine the 4 key groups
-// by shuffles, and each lane accumulates its keys' share of O[qi][0..63], summed over the group.
-// Exact fp32 arithmetic throughout (expf, no bf16 rounding).  Outputs: o as a triple (the proj
-// GEMM operand), o bf16 and the natural-log LSE of the scaled scores (the bf16 backward's
-// inputs, as k_attn_fwd's).
-constexpr int AQB = 64;
-constexpr int AMAXN = 208;       // tokens (ViT-B/16 at 224: 197)
-constexpr int AKPL = AMAXN / 4;  // keys per lane
-
-__global__ __launch_bounds__(256) void k_attn_fwd_f32(const float* __restrict__ qkv, int N, int H,
-                                                      float scale, int npad,
-                                                      bf16_t* __restrict__ o3,
-                                                      bf16_t* __restrict__ o_bf,
-                                                      float* __restrict__ lse) {
-  constexpr int DH = 64, KLD = DH + 4;  // padded K rows: the 4 key groups hit distinct banks
-  __shared__ __attribute__((aligned(16))) float sm[AMAXN * (KLD + DH)];  // 110.5 KiB
-  float* Ks = sm;
-  float* Vs = sm + AMAXN * KLD;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qblocks = (N + AQB - 1) / AQB;
-  const int bh = blockIdx.x / qblocks, qb = blockIdx.x - bh * qblocks;
-  const int b = bh / H, h = bh - b * H;
-  const int D = H * DH;
-  const int64_t tok = 3 * (int64_t)D;
-  const float* base = qkv + (int64_t)b * N * tok + h * DH;
-  for (int i = tid; i < N * (DH / 4); i += blockDim.x) {
-    const int j = i / (DH / 4), c = (i - j * (DH / 4)) * 4;
-    *(f32x4*)(Ks + j * KLD + c) = *(const f32x4*)(base + j * tok + D + c);
-    *(f32x4*)(Vs + j * DH + c) = *(const f32x4*)(base + j * tok + 2 * D + c);
-  }
-  const int qi = lane & 15, kg = lane >> 4;
-  const int q = qb * AQB + wave * 16 + qi;
-  const bool qv = q < N;
-  float qr[DH];
-  {
-    const float* qp = base + (int64_t)(qv ? q : 0) * tok;
-#pragma unroll
-    for (int c = 0; c < DH; c += 4) {
-      const f32x4 t = *(const f32x4*)(qp + c);
-      qr[c] = t[0]; qr[c + 1] = t[1]; qr[c + 2] = t[2]; qr[c + 3] = t[3];
-    }
-  }
-  __syncthreads();
-  float sc[AKPL];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int t = 0; t < AKPL; ++t) {
-    const int j = kg + 4 * t;
-    float s = -INFINITY;
-    if (j < N) {
-      const float* kr = Ks + j * KLD;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-      for (int c = 0; c < DH; c += 4) {
-        const f32x4 kv = *(const f32x4*)(kr + c);
-        a0 = fmaf(qr[c], kv[0], a0);
-        a1 = fmaf(qr[c + 1], kv[1], a1);
-        a2 = fmaf(qr[c + 2], kv[2], a2);
-        a3 = fmaf(qr[c + 3], kv[3], a3);
-      }
-      s = (a0 + a1) + (a2 + a3);
-    }
-    sc[t] = s;
-    mx = fmaxf(mx, s);
-  }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  float l = 0.f;
-#pragma unroll
-  for (int t = 0; t < AKPL; ++t) {
-    const float p = kg + 4 * t < N ? expf((sc[t] - mx) * scale) : 0.f;
-    sc[t] = p;
-    l += p;
-  }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  float acc[DH];
-#pragma unroll
-  for (int c = 0; c < DH; ++c) acc[c] = 0.f;
-#pragma unroll
-  for (int t = 0; t < AKPL; ++t) {
-    const int j = kg + 4 * t;
-    if (j < N) {
-      const float p = sc[t];
-      const float* vr = Vs + j * DH;
-#pragma unroll
-      for (int c = 0; c < DH; c += 4) {
-        const f32x4 vv = *(const f32x4*)(vr + c);
-        acc[c] = fmaf(p, vv[0], acc[c]);
-        acc[c + 1] = fmaf(p, vv[1], acc[c + 1]);
-        acc[c + 2] = fmaf(p, vv[2], acc[c + 2]);
-        acc[c + 3] = fmaf(p, vv[3], acc[c + 3]);
-      }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < DH; ++c) {
-    acc[c] += __shfl_xor(acc[c], 16, 64);
-    acc[c] += __shfl_xor(acc[c], 32, 64);
-  }
-  if (!qv) return;
-  const float inv = 1.0f / l;
-  // lane group kg writes columns [16 kg, 16 kg + 16) of the head's 64
-  float ov[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    float v = acc[e];
-#pragma unroll
-    for (int g = 1; g < 4; ++g) v = kg == g ? acc[16 * g + e] : v;
-    ov[e] = v * inv;
-  }
-  const int64_t row = (int64_t)b * N + q;
-  const int col = h * DH + 16 * kg;
-  st_triple8(o3 + row * 3 * D, D, col, ov, 0);
-  st_triple8(o3 + row * 3 * D, D, col + 8, ov + 8, 0);
-  *(u32x4*)(o_bf + row * D + col) = pack8(ov);
-  *(u32x4*)(o_bf + row * D + col + 8) = pack8(ov + 8);
-  if (kg == 0) lse[(int64_t)bh * npad + q] = mx * scale + logf(l);
-}
-
 }  // namespace
 
 extern "C" int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_t cols,
@@ -499,19 +375,6 @@ extern "C" int dfu_gelu_x3(const float* hpre, int64_t rows, int32_t N, void* h3,
   if (n == 0) return DFU_OK;
   hipLaunchKernelGGL(k_gelu_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, hpre, rows,
                      N, (bf16_t*)h3, (bf16_t*)h_bf16, (bf16_t*)dgelu_bf16);
-  DFU_LAUNCH_CHECK();
-  return DFU_OK;
-}
-
-extern "C" int dfu_attention_fwd_f32(const float* qkv, int32_t B, int32_t N, int32_t H,
-                                     int32_t dh, float scale, int32_t npad, void* o3,
-                                     void* o_bf16, float* lse, void* stream) {
-  DFU_CHECK_ARG(qkv && o3 && o_bf16 && lse && B > 0 && H > 0 && dh == 64 && N > 0 &&
-                    N <= AMAXN && npad >= N,
-                "dfu_attention_fwd_f32: bad args (dh == 64, N <= 208, npad >= N)");
-  const int qblocks = (N + AQB - 1) / AQB;
-  hipLaunchKernelGGL(k_attn_fwd_f32, dim3(B * H * qblocks), dim3(256), 0, (hipStream_t)stream,
-                     qkv, N, H, scale, npad, (bf16_t*)o3, (bf16_t*)o_bf16, lse);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -353,7 +353,7 @@ class GpuPairLoader:
             yield b
 
     def __len__(self):
-        n = len(self.dataset)
+        n = len(self.sampler) if self.sampler is not None else len(self.dataset)
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def _decode(self, pool, idx):

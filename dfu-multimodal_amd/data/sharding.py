@@ -1,0 +1,82 @@
+"""Per-rank sample sharding for data-parallel training (one process per GPU,
+each rank its own share of every batch).
+
+The reference trains on one device: its paired loader draws `len(pairs)` indices with
+replacement from a WeightedRandomSampler (train_multimodal_fusion.py:266-275, weights 1 / count
+of the pair's class) and walks the val / test sets in order (:279-280).  Under data
+parallelism every rank must see a disjoint share of ONE such draw, and every rank must run the
+same number of batches (the gradient all-reduce pairs collectives across ranks), so:
+
+  * ShardedWeightedSampler: every rank makes the SAME weighted draw (a generator seeded with
+    seed + epoch, so it changes per epoch as the reference's global-RNG draw does), pads it
+    by wrapping to a multiple of world_size, and keeps positions rank, rank + world, ...  The
+    union of the shards is the single-rank draw (plus the wrapped padding).
+  * ShardedSequentialSampler: the val / test order (0 .. n-1) split the same way.
+
+`set_epoch(e)` mirrors torch.utils.data.DistributedSampler.
+"""
+import math
+
+import torch
+
+
+def _shard(indices, rank, world):
+    n = len(indices)
+    per = math.ceil(n / world) if n else 0
+    padded = indices + indices[:per * world - n] if n else []
+    return padded[rank:per * world:world]
+
+
+class ShardedWeightedSampler(torch.utils.data.Sampler):
+    """WeightedRandomSampler(weights, num_samples, replacement=True) drawn identically on every
+    rank and sharded: rank r yields draws r, r + world, ... (wrap-padded to equal length)."""
+
+    def __init__(self, weights, num_samples=None, rank=0, world_size=1, seed=42):
+        self.weights = torch.as_tensor(weights, dtype=torch.double)
+        self.num_samples = len(self.weights) if num_samples is None else int(num_samples)
+        if world_size < 1 or not 0 <= rank < world_size:
+            raise ValueError(f"rank {rank} of world {world_size}")
+        self.rank, self.world = rank, world_size
+        self.seed = seed
+        self.epoch = 0
+
+    def set_epoch(self, epoch):
+        self.epoch = int(epoch)
+
+    def full_draw(self):
+        """The draw every rank shares (what a single-rank WeightedRandomSampler with this
+        generator would yield)."""
+        g = torch.Generator().manual_seed(self.seed + self.epoch)
+        return torch.multinomial(self.weights, self.num_samples, True, generator=g).tolist()
+
+    def __iter__(self):
+        return iter(_shard(self.full_draw(), self.rank, self.world))
+
+    def __len__(self):
+        return math.ceil(self.num_samples / self.world)
+
+
+class ShardedSequentialSampler(torch.utils.data.Sampler):
+    """0 .. n-1 sharded over ranks (wrap-padded to equal length): the val / test loaders."""
+
+    def __init__(self, n, rank=0, world_size=1):
+        if world_size < 1 or not 0 <= rank < world_size:
+            raise ValueError(f"rank {rank} of world {world_size}")
+        self.n, self.rank, self.world = int(n), rank, world_size
+
+    def set_epoch(self, epoch):
+        pass
+
+    def __iter__(self):
+        return iter(_shard(list(range(self.n)), self.rank, self.world))
+
+    def __len__(self):
+        return math.ceil(self.n / self.world)
+
+
+def dp_rank_world(group=None):
+    """(rank, world) of the default process group, (0, 1) without one."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1

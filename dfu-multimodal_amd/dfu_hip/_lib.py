@@ -73,6 +73,7 @@ PROTOTYPES = {
     "dfu_last_error_string": [],
     "dfu_version": [],
     "dfu_zero": [P, I64, P],
+    "dfu_streams_abort_capture": [P, I32, P],
     "dfu_gemm": [ctypes.POINTER(GemmDesc), P],
     "dfu_gemm_stats_tiles": [I32],
     "dfu_gemm_workspace_bytes": [ctypes.POINTER(GemmDesc)],
@@ -134,6 +135,7 @@ PROTOTYPES = {
     "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P],
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
+    "dfu_softmax_rows": [P, I32, I32, P, P],
     "dfu_metrics_accumulate": [P, P, I32, I32, P, P, P, P, P],
     "dfu_split_x3": [P, I64, I32, I32, I32, P, I32, P, I64, P],
     "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, P],
@@ -144,7 +146,7 @@ PROTOTYPES = {
     "dfu_avgpool_fwd_x3": [P, I32, I32, I32, P, P],
     "dfu_layernorm_fwd_x3": [P, I64, I32, I32, P, P, F, P, P, P, P, P],
     "dfu_gelu_x3": [P, I64, I32, P, P, P, P],
-    "dfu_attention_fwd_f32": [P, I32, I32, I32, I32, F, I32, P, P, P, P],
+    "dfu_attention_fwd_f32": [P, I32, I32, I32, I32, F, I32, P, P, P, P, P],
     "dfu_resize_ksize": [I32, I32],
     "dfu_resize_coeffs": [I32, I32, P, P],
     "dfu_resize_batch": [P, P, P, I32, I32, I32, P, P, P],

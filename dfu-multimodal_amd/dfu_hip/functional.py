@@ -119,16 +119,17 @@ _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def _current_stream_obj(t):
-    """The current stream of t's device as one cached torch Stream per raw HIP stream (the
-    per-call torch.cuda.current_stream() object costs ~8 us of host time; this is called for
-    every parameter gradient of the step)."""
+    """The current stream of t's device as one cached torch Stream per (device, raw HIP stream)
+    (the per-call torch.cuda.current_stream() object costs ~8 us of host time; this is called
+    for every parameter gradient of the step).  A cached object is re-validated against the
+    raw handle, so a destroyed user stream whose address is reused gets a fresh object."""
     if _raw_stream is None:
         return torch.cuda.current_stream(t.device)
     idx = t.get_device()
     raw = _raw_stream(idx)
-    st = _stream_objs.get(raw)
-    if st is None:
-        st = _stream_objs[raw] = torch.cuda.current_stream(t.device)
+    st = _stream_objs.get((idx, raw))
+    if st is None or st.cuda_stream != raw:
+        st = _stream_objs[(idx, raw)] = torch.cuda.current_stream(t.device)
     return st
 
 
@@ -145,21 +146,60 @@ def join_grad_streams(stream=None, clear=True):
         _grad_streams.clear()
 
 
+# Parameter gradients are written in place, possibly on a branch's side stream or the ViT
+# weight-gradient stream, which autograd does not synchronise (it only orders the gradients it
+# returns).  So that user code after loss.backward() -- torch.optim optimizers, clip_grad_norm_,
+# manual reductions -- may read every p.grad on the stream that called backward, the first
+# encoder-boundary backward of a graph task (arm_backward_join: the head side of TokenNormFn /
+# AvgPoolFn / ConcatFn, which run on the forward's stream) queues an engine final callback that
+# makes that stream wait for every gradient-producing stream once all backward nodes are
+# enqueued.  Optimizers joined through join_grad_streams anyway (FusedAdamW, GradAllReducer)
+# see no extra wait; any other torch.optim optimizer also joins in a step pre-hook.
+_join_armed = [False]
+
+
+def arm_backward_join():
+    if _join_armed[0] or not torch.cuda.is_available():
+        return
+    target = torch.cuda.current_stream()
+    _join_armed[0] = True
+
+    def _join():
+        _join_armed[0] = False
+        join_grad_streams(target, clear=False)
+    try:
+        torch.autograd.Variable._execution_engine.queue_callback(_join)
+    except RuntimeError:  # not inside a backward pass (a direct .backward() call of a Function)
+        _join_armed[0] = False
+
+
+def _optimizer_pre_hook(optimizer, args, kwargs):
+    if _grad_streams and not getattr(optimizer, "_dfu_joins_itself", False):
+        join_grad_streams()
+
+
+try:
+    from torch.optim.optimizer import register_optimizer_step_pre_hook
+    register_optimizer_step_pre_hook(_optimizer_pre_hook)
+except ImportError:  # torch without global optimizer hooks
+    pass
+
+
 _side_streams = {}
-# HIP stream priorities of the side streams (torch: lower = higher priority).  The concurrent
-# ViT branch (the step's MFMA-bound critical path) runs at high priority, so the ResNet stream's
-# memory-bound kernels fill the CUs it leaves idle rather than delay it (same-box A/B, fusion
-# step, two runs each: 18.57-18.61 vs 18.64-18.66 ms); DFU_SIDE_STREAM_PRIORITY=0 restores the
-# default.  DFU_WGRAD_STREAM_PRIORITY: the ViT weight-gradient stream (default 0).
-_SIDE_PRIO = int(os.environ.get("DFU_SIDE_STREAM_PRIORITY", "-1"))
+# HIP stream priorities of the side streams (torch: lower = higher priority).  Default 0 (the
+# streams' default).  DFU_SIDE_STREAM_PRIORITY=-1 runs the concurrent ViT branch at high
+# priority: in the eager fusion step that measured 18.57-18.61 vs 18.64-18.66 ms per step (within
+# 0.3%), but a C5 Grad-CAM step whose warm-up ran with the priority -1 side stream replayed from
+# a HIP graph at 49.6-54.4 ms against 22.9 ms with priority 0 everywhere -- even with the capture
+# itself on priority-0 streams -- so the default keeps one priority for every stream.
+# DFU_WGRAD_STREAM_PRIORITY: the ViT weight-gradient stream (default 0).
+_SIDE_PRIO = int(os.environ.get("DFU_SIDE_STREAM_PRIORITY", "0"))
 _WGRAD_PRIO = int(os.environ.get("DFU_WGRAD_STREAM_PRIORITY", "0"))
 
 
 def side_stream(device):
-    """One persistent side stream per device for the concurrent encoder branch.  Under HIP graph
-    capture the default-priority stream is used instead: a graph captured across streams of
-    different priorities replayed 2.4x slower than eager (C5 Grad-CAM, B = 32: 54.4 ms per
-    replay vs 22.9 ms with the side stream at priority 0)."""
+    """One persistent side stream per device for the concurrent encoder branch (at
+    DFU_SIDE_STREAM_PRIORITY; under HIP graph capture always at the default priority)."""
     idx = torch.device(device).index
     if idx is None:
         idx = torch.cuda.current_device()
@@ -820,6 +860,8 @@ class AvgPoolFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if g.is_cuda:
+            arm_backward_join()
         B, C, H, W = ctx.shape
         g = g.reshape(B, C)
         if g.dtype != F32:
@@ -1004,7 +1046,8 @@ class ViTBlockFn(torch.autograd.Function):
     @staticmethod
     def _forward_x3(ctx, blk, x2, B, T, D, H, dh, rows, wqkv, wproj, wfc1, wfc2, bias):
         """bf16x3 forward: the four Linears on split-bf16 triples (K tripled), fp32 GEMM
-        outputs, fp32 attention; saves the same bf16 tensors as the bf16 forward."""
+        outputs, fp32-accurate attention (split-bf16 MFMA); saves the same bf16 tensors as the
+        bf16 forward."""
         attn, mlp = blk.attn, blk.mlp
         dev = x2.device
         Dh = wfc1.shape[0]
@@ -1023,8 +1066,8 @@ class ViTBlockFn(torch.autograd.Function):
         ops.gemm(rows, 3 * D, 3 * D, xn1_3, 3 * D, weight_x3_rows(attn.qkv.weight), 3 * D, qkvf,
                  3 * D, epilogue=L.EPI_F32, bias=bias(attn.qkv))
         del xn1_3
-        qkv = ops.cast_rows_bf16(qkvf)
-        o3, o, lse = ops.attention_fwd_f32(qkvf, B, T, H, dh, attn.scale)
+        qkv = _empty((rows, 3 * D), BF16, dev)  # written by the attention kernel
+        o3, o, lse = ops.attention_fwd_f32(qkvf, B, T, H, dh, attn.scale, qkv_bf16=qkv)
         del qkvf
         xm = _empty((rows, D), F32, dev)
         ops.gemm(rows, D, 3 * D, o3, 3 * D, weight_x3_rows(attn.proj.weight), 3 * D, xm, D,
@@ -1168,6 +1211,7 @@ class TokenNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         if g.is_cuda:  # produced on the fusion head's stream; the ViT may run on a side stream
+            arm_backward_join()
             g.record_stream(torch.cuda.current_stream())
         x, mean, rstd = ctx.saved_tensors
         norm = ctx.norm
@@ -1312,6 +1356,8 @@ class ConcatFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if g.is_cuda:
+            arm_backward_join()
         Na, Nb = ctx.dims
         ga, gb = ops.split2_f32(g, Na, Nb)
         if ctx.dtypes[0] != F32:

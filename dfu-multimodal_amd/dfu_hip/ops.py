@@ -688,6 +688,16 @@ def argmax_rows(x):
     return out
 
 
+def softmax_rows(x):
+    """torch.softmax(x, dim=1) of fp32 [rows, C] logits (dfu_softmax_rows)."""
+    _req(x, F32, "softmax_rows")
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    check(lib().dfu_softmax_rows(ptr(x), x.shape[0], x.shape[1], ptr(out), stream_ptr()),
+          "dfu_softmax_rows")
+    return out
+
+
 # --------------------------------------------------------------- bf16x3 (split) forward
 # csrc/precise.hip: a triple is bf16 [rows][3C] = [hi | lo | hi] (pattern 0, GEMM A operand)
 # or [hi | hi | lo] (pattern 1, GEMM B operand / weights), hi = bf16(x), lo = bf16(x - hi).
@@ -784,16 +794,20 @@ def gelu_x3(hpre):
     return h3, h, hp
 
 
-def attention_fwd_f32(qkv, B, N, H, dh, scale):
-    """fp32 attention on fp32 qkv -> (o triple, o bf16, lse)."""
+def attention_fwd_f32(qkv, B, N, H, dh, scale, qkv_bf16=None):
+    """fp32-accurate attention (bf16x3 MFMA) on fp32 qkv -> (o triple, o bf16, lse); also fills
+    qkv_bf16 (the plain bf16 copy of qkv) when given."""
     _req(qkv, F32, "attention_fwd_f32")
     D = H * dh
+    if qkv_bf16 is not None:
+        _req(qkv_bf16, BF16, "attention_fwd_f32")
+        assert qkv_bf16.shape == qkv.shape and qkv_bf16.is_contiguous()
     o3 = torch.empty((B * N, 3 * D), dtype=BF16, device=qkv.device)
     o = torch.empty((B * N, D), dtype=BF16, device=qkv.device)
     npad = attention_npad(N)
     lse = torch.empty((B * H, npad), dtype=F32, device=qkv.device)
-    check(lib().dfu_attention_fwd_f32(ptr(qkv), B, N, H, dh, scale, npad, ptr(o3), ptr(o),
-                                      ptr(lse), stream_ptr()), "dfu_attention_fwd_f32")
+    check(lib().dfu_attention_fwd_f32(ptr(qkv), B, N, H, dh, scale, npad, ptr(qkv_bf16), ptr(o3),
+                                      ptr(o), ptr(lse), stream_ptr()), "dfu_attention_fwd_f32")
     return o3, o, lse
 
 

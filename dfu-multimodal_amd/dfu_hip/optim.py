@@ -190,10 +190,16 @@ class FusedAdamW(torch.optim.Optimizer):
         self.check_grads = True  # set False inside captured graphs (pointers are static)
         # update a side stream's parameter block on that stream (step); DFU_EARLY_ADAMW=0: off
         self.early_update = os.environ.get("DFU_EARLY_ADAMW", "1") != "0"
+        self._dfu_joins_itself = True  # step() joins the gradient streams (functional)
+        # the flat gradient buffer's autograd version at the last zero_grad / step: the kernels
+        # write gradients through raw pointers (no bump), so a change means user code edited
+        # p.grad in place (clip_grad_norm_, unscaling, a manual reduction) on its own stream
+        self._grad_version = self.flat.grad._version
 
     def zero_grad(self, set_to_none=True):
         # gradients stay bound to the flat buffer (stable addresses); one memset clears them
         ops.zero_(self.flat.grad)
+        self._grad_version = self.flat.grad._version
 
     def _early_range(self, cur):
         """(lo, hi, stream): the largest run of parameters, contiguous in the flat buffers, whose
@@ -234,7 +240,11 @@ class FusedAdamW(torch.optim.Optimizer):
         # host-side check first: the rebinding copies (and their per-parameter views) only when
         # user code replaced a gradient
         rebind = self.check_grads and fp.needs_rebind()
-        if self.early_update and fp.data.is_cuda and not _dp_world() and not rebind:
+        # the early update reads its block on the producing side stream, which does not wait for
+        # the current stream: only for gradients nothing touched since backward wrote them
+        touched = fp.grad._version != self._grad_version
+        if (self.early_update and fp.data.is_cuda and not _dp_world() and not rebind
+                and not touched):
             early = self._early_range(torch.cuda.current_stream(fp.data.device))
         if early is not None:
             lo, hi, st = early
@@ -257,6 +267,7 @@ class FusedAdamW(torch.optim.Optimizer):
             p._dfu_grad_stream = None
         self.last_early = None if early is None else early[:2]
         fp.shadows_rewritten()
+        self._grad_version = fp.grad._version
         return loss
 
     def state_dict(self):

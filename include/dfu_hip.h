@@ -34,6 +34,13 @@ int dfu_version(void);
 /* Fill `bytes` of device memory with zero on `stream` (grad buckets, BN slabs). */
 int dfu_zero(void* ptr, int64_t bytes, void* stream);
 
+/* End a HIP stream capture left active on any of `streams` (n <= 64) after a failed capture
+ * (e.g. unjoined work: the origin's end fails and the origin and its forked streams stay in
+ * capture mode): the capturing streams are joined to each other inside the capture, the capture
+ * is ended on its origin and the partial graph dropped, so the streams run eager work again.
+ * *still_capturing (optional) = streams still capturing afterwards (0 on success). */
+int dfu_streams_abort_capture(void* const* streams, int32_t n, int32_t* still_capturing);
+
 /* ---------------------------------------------------------------- GEMM -------------
  * C[M,N] (+)= epilogue(alpha * sum_k A[m,k] * B[n,k]) on bf16 MFMA tiles, fp32 accumulate.
  * Replaces every cuBLAS / cuDNN contraction of the hot path:
@@ -386,6 +393,9 @@ int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_a
 int dfu_step_increment(int64_t* step_dev, void* stream);
 /* argmax over C for each row (torch.max(outputs, 1), :384) -> int64. */
 int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t* out, void* stream);
+/* torch.softmax(outputs, dim=1) over fp32 rows of C logits (the test phase's ulcer
+ * probability softmax[:, 1], train_multimodal_fusion.py:477) -> fp32 [rows][C]. */
+int dfu_softmax_rows(const float* x, int32_t rows, int32_t C, float* out, void* stream);
 /* The per-step metrics of train_multimodal_fusion.py:383-388 (loss.item(), torch.max(outputs,
  * 1), .cpu()) accumulated on the device, read back once per epoch: confusion int64 [C][C]
  * (row = label, column = argmax, first maximum wins) += 1 per row; *loss_sum (fp64) += *loss
@@ -434,12 +444,14 @@ int dfu_layernorm_fwd_x3(const float* x, int64_t ldx, int32_t rows, int32_t D,
  * DFU_EPI_BF16_DGELU operand, as DFU_EPI_BF16_GELU's aux_out). */
 int dfu_gelu_x3(const float* hpre, int64_t rows, int32_t N, void* h3, void* h_bf16,
                 void* dgelu_bf16, void* stream);
-/* fp32 softmax attention (SDPA) on fp32 qkv [B*N][3][H][dh] -> o triple [B*N][3*H*dh], o bf16,
- * lse fp32 [B*H][npad] (as dfu_attention_fwd's: the bf16 backward's inputs).  dh == 64,
- * N <= 208. */
+/* fp32-accurate softmax attention (SDPA) on the fp32 qkv GEMM output [B*N][3][H][dh]: the
+ * bf16 MFMA attention on split operands (S = Qhi Khi + Qhi Klo + Qlo Khi, O = Phi Vhi + Plo Vhi +
+ * Phi Vlo, fp32 softmax; ~2^-17 relative per product) -> o triple [B*N][3*H*dh], o bf16, lse
+ * fp32 [B*H][npad] (as dfu_attention_fwd's: the bf16 backward's inputs) and, when qkv_bf16 is
+ * not NULL, the plain bf16 copy of qkv (the backward's operand).  dh == 64, N <= 224. */
 int dfu_attention_fwd_f32(const float* qkv, int32_t B, int32_t N, int32_t H, int32_t dh,
-                          float scale, int32_t npad, void* o3, void* o_bf16, float* lse,
-                          void* stream);
+                          float scale, int32_t npad, void* qkv_bf16, void* o3, void* o_bf16,
+                          float* lse, void* stream);
 
 /* ---------------------------------------------------------------- input pipeline ---- */
 /* The torchvision transforms of train_multimodal_fusion.py:172-205 on a decoded batch,

@@ -53,3 +53,58 @@ def test_concurrent_branches_bitwise_equal_to_serial(monkeypatch):
     assert not bad, f"gradients differ: {bad[:5]}"
     bad = [n for n in p0 if not torch.equal(p0[n], p1[n])]
     assert not bad, f"parameters differ after two steps: {bad[:5]}"
+
+
+@pytest.mark.parametrize("failure", ["unjoined", "host_sync"])
+def test_failed_capture_recovers_to_eager(failure):
+    """A failed HIP-graph capture (work forked onto the side stream and never joined; a host
+    synchronisation inside the step) must leave a process that runs eager steps and HIP-event
+    timing normally (bench.py crashed in elapsed_time after such a failure),
+    with the same results as before the attempt."""
+    from dfu_hip import functional as Fn
+    from dfu_hip import graphs
+    from dfu_hip import nn as hnn
+    from models.fusion import MultimodalFusionModel
+    torch.manual_seed(0)
+    m = MultimodalFusionModel(num_classes=2, dropout=0.0).to(DEV).train()
+    rgb, th, y = R.synthetic_batch(4, seed=3)
+    rgb, th, y = rgb.to(DEV), th.to(DEV), y.to(DEV)
+    crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=DEV))
+
+    def step():
+        m.zero_grad(set_to_none=False)
+        loss = crit(m(rgb, th), y)
+        loss.backward()
+        Fn.join_grad_streams()
+        return loss
+
+    ref = step().detach().clone()
+    torch.cuda.synchronize()
+    scratch = torch.zeros(1024, device=DEV)
+
+    def bad():
+        step()
+        if failure == "unjoined":
+            side = Fn.side_stream(DEV)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                scratch.add_(1.0)  # never joined back into the capture's origin stream
+        else:
+            torch.cuda.synchronize()
+
+    msgs = []
+    g = graphs.try_capture(bad, log=msgs.append)
+    assert g is None and msgs and "graph capture failed" in msgs[0]
+    assert not torch.cuda.is_current_stream_capturing()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    got = step().detach().clone()
+    e1.record()
+    torch.cuda.synchronize()
+    assert e0.elapsed_time(e1) > 0
+    assert torch.equal(got, ref)
+    # a good step still captures and replays afterwards
+    g = graphs.try_capture(step, log=msgs.append)
+    assert g is not None
+    g.replay()
+    torch.cuda.synchronize()
