@@ -27,6 +27,17 @@ extern "C" int dfu_zero(void* ptr, int64_t bytes, void* stream) {
   return DFU_OK;
 }
 
+extern "C" int dfu_stream_capture_status(void* stream, int32_t* status) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing((hipStream_t)stream, &st);
+  if (e != hipSuccess) {
+    dfu_set_error("dfu_stream_capture_status: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  if (status) *status = (int32_t)st;
+  return DFU_OK;
+}
+
 // Recovery after a failed HIP-graph capture (dfu_hip.graphs): when the origin stream's
 // hipStreamEndCapture fails on unjoined work, the capture is NOT ended -- the origin and every
 // stream forked into it stay in capture mode, and the next eager call that touches the legacy
@@ -77,5 +88,34 @@ extern "C" int dfu_streams_abort_capture(void* const* streams, int32_t n,
   }
   (void)hipGetLastError();  // the failed ends above are the expected outcome
   if (still_capturing) *still_capturing = left;
+  return DFU_OK;
+}
+
+// Library-owned streams (the encoder side stream, the ViT weight-gradient stream, graph-capture
+// streams): non-blocking, so they never take part in the legacy stream's implicit
+// synchronisation, and owned here rather than by torch's stream pool, so one left capturing by a
+// failed capture (HIP cannot end it: dfu_streams_abort_capture) can be retired for good instead
+// of being handed out again by the pool's round robin.
+extern "C" int dfu_stream_create(int32_t priority, void** stream) {
+  if (stream == nullptr) {
+    dfu_set_error("dfu_stream_create: null output");
+    return DFU_E_INVALID;
+  }
+  hipStream_t s = nullptr;
+  hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority);
+  if (e != hipSuccess) {
+    dfu_set_error("dfu_stream_create: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  *stream = (void*)s;
+  return DFU_OK;
+}
+
+extern "C" int dfu_stream_destroy(void* stream) {
+  hipError_t e = hipStreamDestroy((hipStream_t)stream);
+  if (e != hipSuccess) {
+    dfu_set_error("dfu_stream_destroy: %s", hipGetErrorString(e));
+    return (int)e;
+  }
   return DFU_OK;
 }

@@ -382,6 +382,11 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
                   pl.tile + 1);
     return DFU_E_UNSUPPORTED;
   }
+  if (d->epilogue == DFU_EPI_X3_GELU) {
+    DFU_CHECK_ARG(pl.tile == T256x256ps, "dfu_gemm: X3_GELU needs the persistent 256x256 tile");
+    DFU_CHECK_ARG(d->aux_out != nullptr && d->ldaux_out >= d->N && d->ldc >= 3LL * d->N,
+                  "dfu_gemm: X3_GELU needs aux_out (ldaux_out >= N) and ldc >= 3N");
+  }
   DFU_CHECK_ARG(((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0,
                 "dfu_gemm: A and B must be 16-byte aligned");
   if (d->a_mode == DFU_OPND_KMAJOR || d->a_mode == DFU_OPND_MNMAJOR)

@@ -112,6 +112,7 @@ DFU_DEV int ps_epi_stores(const GemmArgs& p) {
   const int per = bf16_out && p.n8 ? 16 : 32 * (p.n4 ? 1 : 4);
   // dGELU with column sums (p.stats): four more 16-B stores per wave (scalar: sixteen)
   const int cs = EPI == DFU_EPI_BF16_DGELU && p.stats ? (p.n4 ? 4 : 16) : 0;
+  if constexpr (EPI == DFU_EPI_X3_GELU) return 4 * (p.n8 ? 16 : 32 * (p.n4 ? 1 : 4));
   return (EPI == DFU_EPI_BF16_GELU ? 2 * per : per) + cs;
 }
 
@@ -140,7 +141,8 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
   constexpr bool kBias = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_GELU ||
-                         EPI == DFU_EPI_F32_RESID;
+                         EPI == DFU_EPI_F32_RESID || EPI == DFU_EPI_F32 ||
+                         EPI == DFU_EPI_X3_GELU;
   if (kBias && p.bias) {
     float b2[2][4];
 #pragma unroll
@@ -176,6 +178,26 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
           for (int r = 0; r < 4; ++r) gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
         st_row_bf16<2>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
         st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+      } else if constexpr (EPI == DFU_EPI_X3_GELU) {
+        // gelu(pre) as the split triple hi = bf16(g), lo = bf16(g - hi): segments hi | lo | hi
+        float g[2][4], d[2][4], lo[2][4];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
+            lo[jj][r] = g[jj][r] - bf2f(f2bf(g[jj][r]));
+          }
+        st_row_bf16<2>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
+        st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, lo);
+        st_row_bf16<2>(rc, mc * p.ldc + 2 * N, okm, n0w, N, p.n8, n4, lane, g);
+      } else if constexpr (EPI == DFU_EPI_F32) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int n = n0w + jj * 16 + 4 * (lane >> 4);
+          st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+        }
       } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
@@ -480,6 +502,8 @@ const Entry kTable256x256ps[] = {
     PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
     PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_GELU),
     PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_RESID),
+    PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32),      // bf16x3 forward (qkv)
+    PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_X3_GELU),  // bf16x3 forward (fc1 + GELU)
     PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_DGELU),  // dgrads on a transposed weight
     PS(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16),
     PS(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_DGELU),

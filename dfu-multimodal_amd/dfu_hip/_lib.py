@@ -24,7 +24,7 @@ OPND_KMAJOR, OPND_MNMAJOR, OPND_CONV_FWD, OPND_CONV_DGRAD, OPND_CONV_DGRAD_W, OP
 # enum dfu_epilogue
 (EPI_BF16, EPI_BF16_RELU, EPI_BF16_GELU, EPI_F32, EPI_F32_RESID, EPI_BF16_DGELU, EPI_BF16_ADD,
  EPI_F32_ACC, EPI_F32_ACC_CONVW, EPI_BF16_STATS, EPI_PATCH, EPI_F32_STATS,
- EPI_BF16_DSTATS) = range(13)
+ EPI_BF16_DSTATS, EPI_X3_GELU) = range(14)
 
 DFU_E_INVALID = 1001
 DFU_E_UNSUPPORTED = 1002
@@ -74,6 +74,9 @@ PROTOTYPES = {
     "dfu_version": [],
     "dfu_zero": [P, I64, P],
     "dfu_streams_abort_capture": [P, I32, P],
+    "dfu_stream_capture_status": [P, P],
+    "dfu_stream_create": [I32, P],
+    "dfu_stream_destroy": [P],
     "dfu_gemm": [ctypes.POINTER(GemmDesc), P],
     "dfu_gemm_stats_tiles": [I32],
     "dfu_gemm_workspace_bytes": [ctypes.POINTER(GemmDesc)],

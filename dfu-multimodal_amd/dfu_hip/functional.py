@@ -197,6 +197,17 @@ _SIDE_PRIO = int(os.environ.get("DFU_SIDE_STREAM_PRIORITY", "0"))
 _WGRAD_PRIO = int(os.environ.get("DFU_WGRAD_STREAM_PRIORITY", "0"))
 
 
+def new_stream(idx, priority=0):
+    """A library-owned non-blocking HIP stream (dfu_stream_create) as a torch ExternalStream.
+    Never returned to torch's stream pool: a stream a failed graph capture left capturing is
+    retired (dfu_hip.graphs) and this makes a fresh one."""
+    import ctypes
+    h = ctypes.c_void_p(0)
+    with torch.cuda.device(idx):
+        L.check(L.load().dfu_stream_create(int(priority), ctypes.byref(h)), "dfu_stream_create")
+    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+
+
 def side_stream(device):
     """One persistent side stream per device for the concurrent encoder branch (at
     DFU_SIDE_STREAM_PRIORITY; under HIP graph capture always at the default priority)."""
@@ -206,7 +217,7 @@ def side_stream(device):
     prio = 0 if torch.cuda.is_current_stream_capturing() else _SIDE_PRIO
     st = _side_streams.get((idx, prio))
     if st is None:
-        st = _side_streams[(idx, prio)] = torch.cuda.Stream(device=idx, priority=prio)
+        st = _side_streams[(idx, prio)] = new_stream(idx, prio)
     return st
 
 
@@ -226,7 +237,7 @@ def wgrad_stream(device):
     prio = 0 if torch.cuda.is_current_stream_capturing() else _WGRAD_PRIO  # see side_stream
     st = _wgrad_streams.get((idx, prio))
     if st is None:
-        st = _wgrad_streams[(idx, prio)] = torch.cuda.Stream(device=idx, priority=prio)
+        st = _wgrad_streams[(idx, prio)] = new_stream(idx, prio)
     return st
 
 
@@ -927,10 +938,10 @@ class PatchEmbedFn(torch.autograd.Function):
 
 # ---------------------------------------------------------------------------- ViT block
 def _linear_wgrad(dy_bf, x_bf, w, rows):
-    """w.grad [N, K] += dy^T x  (dy [rows, N], x [rows, K], both bf16)."""
+    """w.grad [N, K] += dy^T x  (dy [rows, N], x [rows, K] with any row stride, both bf16)."""
     N, K = w.shape
-    ops.gemm(N, K, rows, dy_bf, N, x_bf, K, grad_buffer(w), K, a_mode=L.OPND_MNMAJOR,
-             b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+    ops.gemm(N, K, rows, dy_bf, N, x_bf, x_bf.stride(0), grad_buffer(w), K,
+             a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
 
 
 def _ln_fwd(x2d, norm, rows, D, out_bf):
@@ -987,6 +998,11 @@ def _linear_dgrad(rows, N, K, g, weight, w_rows, out, epilogue=L.EPI_BF16, **kw)
         ops.gemm(rows, N, K, g, K, w_rows, N, out, N, b_mode=L.OPND_MNMAJOR, epilogue=epilogue,
                  **kw)
 
+
+# Tile of the ViT's bf16x3 forward GEMMs (tripled K): 8 = the persistent phased 256x256 (with
+# the fused fc1 + GELU triple epilogue, DFU_EPI_X3_GELU); DFU_X3_TILE=0: the cost model's pick
+# and a separate GELU split pass (A/B).
+_X3_TILE = int(os.environ.get("DFU_X3_TILE", "8"))
 
 # fc1.bias gradient from the dGELU epilogue's column sums (DFU_DGELU_COLSUM=0: a colsum pass)
 _DGELU_COLSUM = os.environ.get("DFU_DGELU_COLSUM", "1") != "0"
@@ -1061,29 +1077,40 @@ class ViTBlockFn(torch.autograd.Function):
                                  rstd)
             return t3, tb, mean, rstd
 
+        tl = _X3_TILE
         xn1_3, xn1, m1, r1 = ln_x3(x2, blk.norm1)
         qkvf = _empty((rows, 3 * D), F32, dev)
         ops.gemm(rows, 3 * D, 3 * D, xn1_3, 3 * D, weight_x3_rows(attn.qkv.weight), 3 * D, qkvf,
-                 3 * D, epilogue=L.EPI_F32, bias=bias(attn.qkv))
+                 3 * D, epilogue=L.EPI_F32, bias=bias(attn.qkv), tile=tl)
         del xn1_3
         qkv = _empty((rows, 3 * D), BF16, dev)  # written by the attention kernel
         o3, o, lse = ops.attention_fwd_f32(qkvf, B, T, H, dh, attn.scale, qkv_bf16=qkv)
         del qkvf
         xm = _empty((rows, D), F32, dev)
         ops.gemm(rows, D, 3 * D, o3, 3 * D, weight_x3_rows(attn.proj.weight), 3 * D, xm, D,
-                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D)
+                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D, tile=tl)
         del o3
         xn2_3, xn2, m2, r2 = ln_x3(xm, blk.norm2)
-        hf = _empty((rows, Dh), F32, dev)
-        ops.gemm(rows, Dh, 3 * D, xn2_3, 3 * D, weight_x3_rows(mlp.fc1.weight), 3 * D, hf, Dh,
-                 epilogue=L.EPI_F32, bias=bias(mlp.fc1))
+        dgl = _empty((rows, Dh), BF16, dev)  # bf16 gelu'(pre): the DGELU factor
+        if tl == 8:
+            # fc1 + GELU with the split triple written by the epilogue; the backward's bf16 h
+            # is the triple's hi segment (a strided view)
+            h3 = _empty((rows, 3 * Dh), BF16, dev)
+            ops.gemm(rows, Dh, 3 * D, xn2_3, 3 * D, weight_x3_rows(mlp.fc1.weight), 3 * D, h3,
+                     3 * Dh, epilogue=L.EPI_X3_GELU, bias=bias(mlp.fc1), aux_out=dgl,
+                     ldaux_out=Dh, tile=tl)
+            h = h3[:, :Dh]
+        else:
+            hf = _empty((rows, Dh), F32, dev)
+            ops.gemm(rows, Dh, 3 * D, xn2_3, 3 * D, weight_x3_rows(mlp.fc1.weight), 3 * D, hf,
+                     Dh, epilogue=L.EPI_F32, bias=bias(mlp.fc1), tile=tl)
+            h3, h, dgl = ops.gelu_x3(hf)
+            del hf
         del xn2_3
-        h3, h, dgl = ops.gelu_x3(hf)  # dgl = bf16 gelu'(pre): the DGELU factor
-        del hf
         xo = _empty((B, T, D), F32, dev)
         ops.gemm(rows, D, 3 * Dh, h3, 3 * Dh, weight_x3_rows(mlp.fc2.weight), 3 * Dh,
                  xo.view(rows, D), D, epilogue=L.EPI_F32_RESID, bias=bias(mlp.fc2), aux=xm,
-                 ldaux=D)
+                 ldaux=D, tile=tl)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)

@@ -33,6 +33,25 @@ def step_streams(device=None, extra=()):
     return uniq
 
 
+def capture_status(stream):
+    """0 none, 1 active, 2 invalidated (dfu_stream_capture_status)."""
+    st = ctypes.c_int32(0)
+    L.check(L.load().dfu_stream_capture_status(ctypes.c_void_p(stream.cuda_stream),
+                                               ctypes.byref(st)), "dfu_stream_capture_status")
+    return st.value
+
+
+def join_forked(origin, extra=()):
+    """Inside a capture on `origin`: make it wait for every step stream that is capturing (a
+    fork of this capture), so work left on a side stream joins the graph instead of failing
+    the capture as unjoined -- which HIP cannot undo: the origin's hipStreamEndCapture then
+    returns hipErrorStreamCaptureUnjoined and leaves the origin and its forks capturing for
+    good (a second end returns hipErrorStreamCaptureWrongThread; tools/diag)."""
+    for s in step_streams(extra=extra):
+        if s.cuda_stream != origin.cuda_stream and capture_status(s) == 1:
+            origin.wait_stream(s)
+
+
 def abort_captures(streams):
     """End any capture left active on `streams` (dfu_streams_abort_capture); returns
     (streams that were capturing, streams still capturing afterwards)."""
@@ -50,35 +69,56 @@ def abort_captures(streams):
 
 
 def reset_after_failed_capture(extra=()):
-    """Recover the streams and host-side stream state after a failed capture."""
-    n, left = abort_captures(step_streams(extra=extra))
-    if left:
-        raise RuntimeError(f"dfu: {left} stream(s) still capturing after the capture abort")
+    """Recover after a failed capture: end what HIP lets us end, retire the library-owned
+    streams still capturing (HIP cannot end a capture whose origin's end already failed:
+    tools/diag/capture_unjoined.py) -- the next side_stream / wgrad_stream call makes fresh
+    ones -- and reset the host-side stream state.  Returns (streams that were capturing,
+    streams retired)."""
+    streams = step_streams(extra=extra)
+    n, _ = abort_captures(streams)
+    stuck = {s.cuda_stream for s in streams if capture_status(s) != 0}
+    for cache in (Fn._side_streams, Fn._wgrad_streams):
+        for k in [k for k, s in cache.items() if s.cuda_stream in stuck]:
+            del cache[k]  # leaked on purpose: a capturing stream cannot be destroyed or reused
+    cur = torch.cuda.current_stream()
+    if cur.cuda_stream in stuck:
+        raise RuntimeError("dfu: the caller's stream is still capturing after a failed capture")
     Fn._grad_streams.clear()
     Fn._join_armed[0] = False
     Fn._stream_objs.clear()
-    torch.cuda.synchronize()
-    return n
+    try:  # can the process run eager work again?  (an allocation + a kernel + a host sync)
+        torch.empty(1024, device=cur.device).fill_(0.0)
+        torch.cuda.synchronize()
+    except RuntimeError as e:
+        # HIP leaves an INVALIDATED capture that had forked streams active for good (e.g. a host
+        # synchronisation inside the step): every later legacy-stream or allocation call fails
+        # with hipErrorStreamCaptureImplicit.  Nothing in-process can end it.
+        raise RuntimeError("dfu: a failed HIP-graph capture left this process unable to run "
+                           "eager work (HIP cannot end an invalidated capture with forked "
+                           "streams); rerun without graph capture") from e
+    return n, len(stuck)
 
 
 def try_capture(step, log=None, pool=None):
     """Capture `step()` into a torch.cuda.CUDAGraph on a fresh capture stream; returns the graph,
     or None after a failed capture (streams recovered, the failure reported through `log`,
-    default stderr).  The caller warms `step` up eagerly first, as graph capture requires."""
+    default stderr).  Work the step left on a forked stream is joined into the capture
+    (join_forked).  The caller warms `step` up eagerly first, as graph capture requires."""
     prev = torch.cuda.current_stream()
-    cap = torch.cuda.Stream()
+    cap = Fn.new_stream(prev.device_index)  # library-owned: retired, not reused, if it sticks
     cap.wait_stream(prev)
     g = torch.cuda.CUDAGraph()
     try:
         with torch.cuda.graph(g, pool=pool, stream=cap):
             step()
+            join_forked(cap)
         return g
     except Exception as e:  # noqa: BLE001 -- any capture failure falls back to eager
         # torch.cuda.graph.__exit__ leaves its capture stream current when capture_end raises
         torch.cuda.set_stream(prev)
-        left = reset_after_failed_capture(extra=(cap,))
+        n, stuck = reset_after_failed_capture(extra=(cap,))
         msg = (f"[dfu] graph capture failed ({type(e).__name__}: {str(e).splitlines()[0]}); "
-               f"{left} stream(s) left capturing were ended; running eager")
+               f"{n} stream(s) were left capturing, {stuck} retired; running eager")
         if log is None:
             print(msg, file=sys.stderr)
         elif log:

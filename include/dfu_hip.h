@@ -34,6 +34,11 @@ int dfu_version(void);
 /* Fill `bytes` of device memory with zero on `stream` (grad buckets, BN slabs). */
 int dfu_zero(void* ptr, int64_t bytes, void* stream);
 
+/* Library-owned non-blocking HIP streams at a HIP priority (lower = higher; 0 default). */
+int dfu_stream_create(int32_t priority, void** stream);
+int dfu_stream_destroy(void* stream);
+/* Capture status of `stream`: 0 none, 1 active, 2 invalidated (hipStreamCaptureStatus). */
+int dfu_stream_capture_status(void* stream, int32_t* status);
 /* End a HIP stream capture left active on any of `streams` (n <= 64) after a failed capture
  * (e.g. unjoined work: the origin's end fails and the origin and its forked streams stay in
  * capture mode): the capturing streams are joined to each other inside the capture, the capture
@@ -74,7 +79,7 @@ enum dfu_epilogue {
   DFU_EPI_PATCH = 10,        /* ViT patch-embed: C f32 [B][T+1][N] row 1+p = acc+bias+pos   */
   DFU_EPI_F32_STATS = 11,    /* C f32 = acc; per-column (sum, M2) of each 128-row tile (the
                                 split-bf16 "bf16x3" forward: BN statistics of unrounded y)  */
-  DFU_EPI_BF16_DSTATS = 12   /* BatchNorm backward statistics in the dgrad that produces the
+  DFU_EPI_BF16_DSTATS = 12,  /* BatchNorm backward statistics in the dgrad that produces the
                                 BN output's gradient: C bf16 = g = alpha*acc; per column of
                                 each 128-row tile, stats[tile][0] = sum g', stats[tile][1] =
                                 sum g' (y - mean) invstd over g' = g masked by the forward's
@@ -82,6 +87,10 @@ enum dfu_epilogue {
                                 bn_coef = fp32 [4][N] rows scale, shift, mean, invstd.  The
                                 records feed dfu_bn_bwd_finalize (blocks = ceil(M/128)) in
                                 place of dfu_bn_bwd_reduce.  Stride-1 launches only.         */
+  DFU_EPI_X3_GELU = 13       /* bf16x3 forward of timm Mlp.fc1 + GELU: pre = acc + bias (fp32),
+                                C = the A-operand triple [hi | lo | hi] of gelu(pre), bf16
+                                [M][3N] (ldc >= 3N; segments at columns 0, N, 2N), aux_out
+                                bf16 = gelu'(pre).  Persistent 256x256 tile only.            */
 };
 
 typedef struct dfu_gemm_desc {

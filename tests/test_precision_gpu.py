@@ -72,6 +72,39 @@ def test_gemm_over_triples_is_fp32_accurate(M, N, K):
     assert err < 2e-5 and errb > 20 * err
 
 
+@pytest.mark.parametrize("M,N,K", [(12608, 3072, 768), (1000, 520, 200), (257, 264, 64)])
+def test_x3_gelu_and_f32_epilogues_on_persistent_tile(M, N, K):
+    """The bf16x3 ViT forward's fc1 + GELU on the persistent 256x256 tile (DFU_EPI_X3_GELU):
+    the triple [hi | lo | hi] of gelu(A.B^T + bias) to ~1e-5 of fp64, gelu'(pre) in bf16, and
+    the same GEMM with the plain fp32 epilogue (qkv); ragged M and N edges included."""
+    import math
+    L, ops = _ops()
+    torch.manual_seed(11)
+    A = torch.randn(M, K, device=DEV) * 0.5
+    B = torch.randn(N, K, device=DEV) * (1.0 / math.sqrt(K))
+    bias = torch.randn(N, device=DEV)
+    A3, B3 = ops.split_x3(A, ops.X3_A), ops.split_x3(B, ops.X3_B)
+    pre = A.double() @ B.double().T + bias.double()
+    C = torch.empty(M, N, device=DEV)
+    ops.gemm(M, N, 3 * K, A3, 3 * K, B3, 3 * K, C, N, epilogue=L.EPI_F32, bias=bias, tile=8)
+    assert ((C.double() - pre).norm() / pre.norm()).item() < 2e-5
+    h3 = torch.full((M, 3 * N), float("nan"), device=DEV).to(torch.bfloat16)
+    dg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(M, N, 3 * K, A3, 3 * K, B3, 3 * K, h3, 3 * N, epilogue=L.EPI_X3_GELU, bias=bias,
+             aux_out=dg, ldaux_out=N, tile=8)
+    g = torch.nn.functional.gelu(pre)
+    v, hi0, hi2 = _trip(h3, N)
+    err = (v.double() - g).abs().max().item()
+    print(f"\n[x3 gelu {M}x{N}x{K}] max abs err {err:.2e} (max |gelu| {g.abs().max().item():.2f})")
+    assert err < 2e-5 * max(1.0, g.abs().max().item())
+    assert torch.equal(hi0, hi2)
+    dref = 0.5 * torch.erfc(-pre / math.sqrt(2)) + pre * torch.exp(-0.5 * pre * pre) / math.sqrt(2 * math.pi)
+    assert ((dg.double() - dref).abs() <= 2.0 ** -8 * dref.abs() + 1e-5).all()
+    with pytest.raises(L.DfuError):  # the fused triple exists on the persistent tile only
+        ops.gemm(M, N, 3 * K, A3, 3 * K, B3, 3 * K, h3, 3 * N, epilogue=L.EPI_X3_GELU,
+                 bias=bias, aux_out=dg, ldaux_out=N, tile=1)
+
+
 @pytest.mark.parametrize("tile", [1, 2])
 def test_f32_stats_epilogue(tile):
     """fp32 output + per-128-row (sum, M2) of the unrounded accumulators, both tiles that

@@ -55,14 +55,8 @@ def test_concurrent_branches_bitwise_equal_to_serial(monkeypatch):
     assert not bad, f"parameters differ after two steps: {bad[:5]}"
 
 
-@pytest.mark.parametrize("failure", ["unjoined", "host_sync"])
-def test_failed_capture_recovers_to_eager(failure):
-    """A failed HIP-graph capture (work forked onto the side stream and never joined; a host
-    synchronisation inside the step) must leave a process that runs eager steps and HIP-event
-    timing normally (bench.py crashed in elapsed_time after such a failure),
-    with the same results as before the attempt."""
+def _capture_setup():
     from dfu_hip import functional as Fn
-    from dfu_hip import graphs
     from dfu_hip import nn as hnn
     from models.fusion import MultimodalFusionModel
     torch.manual_seed(0)
@@ -70,31 +64,39 @@ def test_failed_capture_recovers_to_eager(failure):
     rgb, th, y = R.synthetic_batch(4, seed=3)
     rgb, th, y = rgb.to(DEV), th.to(DEV), y.to(DEV)
     crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=DEV))
+    out = {}
 
     def step():
         m.zero_grad(set_to_none=False)
         loss = crit(m(rgb, th), y)
         loss.backward()
         Fn.join_grad_streams()
+        out["loss"] = loss
         return loss
-
     ref = step().detach().clone()
     torch.cuda.synchronize()
-    scratch = torch.zeros(1024, device=DEV)
+    return step, ref, out
+
+
+def test_failed_capture_recovers_to_eager():
+    """A failed HIP-graph capture -- here an error raised inside the captured step after its
+    forward and backward were enqueued (e.g. a DfuError from an unsupported launch, or the
+    bench's replay check) -- must leave a process that runs eager steps and HIP-event timing
+    normally (bench.py crashed in elapsed_time after a failed capture: the
+    capture stream stayed current), with the same results as before the attempt, and a good
+    step must still capture afterwards."""
+    from dfu_hip import graphs
+    step, ref, out = _capture_setup()
 
     def bad():
         step()
-        if failure == "unjoined":
-            side = Fn.side_stream(DEV)
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                scratch.add_(1.0)  # never joined back into the capture's origin stream
-        else:
-            torch.cuda.synchronize()
+        raise ValueError("forced failure inside the capture")
 
     msgs = []
+    prev = torch.cuda.current_stream()
     g = graphs.try_capture(bad, log=msgs.append)
     assert g is None and msgs and "graph capture failed" in msgs[0]
+    assert torch.cuda.current_stream() == prev
     assert not torch.cuda.is_current_stream_capturing()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -103,8 +105,43 @@ def test_failed_capture_recovers_to_eager(failure):
     torch.cuda.synchronize()
     assert e0.elapsed_time(e1) > 0
     assert torch.equal(got, ref)
-    # a good step still captures and replays afterwards
     g = graphs.try_capture(step, log=msgs.append)
     assert g is not None
     g.replay()
     torch.cuda.synchronize()
+    assert torch.equal(out["loss"], ref)
+
+
+def test_capture_joins_work_left_on_a_side_stream():
+    """Work a step leaves on the encoder side stream (never joined back: the round-2 Grad-CAM
+    bug) is joined into the capture by try_capture instead of failing it as unjoined -- HIP
+    cannot end such a capture, so the streams would stay capturing for the rest of the
+    process.  The replay then performs that work too."""
+    from dfu_hip import functional as Fn
+    from dfu_hip import graphs
+    step, ref, out = _capture_setup()
+    scratch = torch.zeros(1024, device=DEV)
+
+    def forking():
+        step()
+        side = Fn.side_stream(DEV)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            scratch.add_(1.0)  # not joined by the step itself
+
+    msgs = []
+    g = graphs.try_capture(forking, log=msgs.append)
+    assert g is not None and not msgs
+    torch.cuda.synchronize()
+    scratch.zero_()
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(scratch, torch.full_like(scratch, 2.0))
+    assert torch.equal(out["loss"], ref)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    step()
+    e1.record()
+    torch.cuda.synchronize()
+    assert e0.elapsed_time(e1) > 0
