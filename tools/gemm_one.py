@@ -3,7 +3,8 @@
   python tools/gemm_one.py <case> [--tile T] [--iters N]
   cases: fc1_fwd (12608x3072x768, KM x KM, BF16), fc1_gelu (same, GELU epilogue),
          fc2_dgrad (12608x3072x768, KM x MN, DGELU), fc1_wgrad (3072x768x12608, MN x MN, F32_ACC),
-         l1c3_fwd (200704x256x64 1x1 conv, STATS)
+         l1c3_fwd (200704x256x64 1x1 conv, STATS), fc2_fwd_resid (12608x768x3072, F32_RESID),
+         fc2_wgrad / qkv_wgrad / proj_wgrad (768x3072 / 2304x768 / 768x768 x 12608, F32_ACC)
 """
 import argparse
 import os
@@ -55,6 +56,22 @@ def build(case, tile):
                                                    epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N,
                                                    tile=tile)
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16,
+                                               tile=tile)
+    if case == "fc2_fwd_resid":  # the step's fc2 forward: fp32 residual-stream epilogue
+        M, N, K = 12608, 768, 3072
+        A, B = T(M, K), T(N, K)
+        C, X = T(M, N, dtype=torch.float32), T(M, N, dtype=torch.float32)
+        bias = T(N, dtype=torch.float32)
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N,
+                                               epilogue=L.EPI_F32_RESID, bias=bias, aux=X,
+                                               ldaux=N, tile=tile)
+    if case in ("fc2_wgrad", "qkv_wgrad", "proj_wgrad"):
+        M, N, K = {"fc2_wgrad": (768, 3072, 12608), "qkv_wgrad": (2304, 768, 12608),
+                   "proj_wgrad": (768, 768, 12608)}[case]
+        A, B = T(K, M), T(K, N)
+        C = torch.zeros(M, N, device="cuda")
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, M, B, N, C, N, a_mode=L.OPND_MNMAJOR,
+                                               b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC,
                                                tile=tile)
     if case == "fc1_wgrad":
         M, N, K = 3072, 768, 12608
