@@ -4,6 +4,8 @@ North-star head (grad_cam_visualization.py:289-302, extended_metrics.py:338-350)
     cat([f_rgb (2048), f_th (768)]) -> Linear(2816, 512) -> ReLU -> Dropout(p) -> Linear(512, 2)
 ``hidden_dims=(512, 256)`` builds the train-script variant (train_multimodal_fusion.py:305-313).
 """
+import os
+
 import torch
 import torch.nn as tnn
 
@@ -36,6 +38,50 @@ class MLPFusion(tnn.Module):
     def forward(self, rgb_feat, thermal_feat):
         fused = Fn.ConcatFn.apply(rgb_feat, thermal_feat)
         return self.classifier(fused)
+
+
+# DFU_INTERLEAVE_ENCODERS=0: run the ViT's forward, then the ResNet's (A/B).  Interleaved, the
+# host enqueues ViT and ResNet stages alternately, so both streams start at once, and the
+# autograd engine -- which runs ready backward nodes latest-created first -- alternates between
+# the branches in backward instead of enqueueing the whole ResNet backward before the ViT's
+# (the critical path) gets its first kernel.
+_INTERLEAVE = os.environ.get("DFU_INTERLEAVE_ENCODERS", "1") != "0"
+
+
+def _stageable(net):
+    """The encoder has forward_stages and no hook on a container forward_stages bypasses."""
+    if not hasattr(net, "forward_stages"):
+        return False
+    return not any(m._forward_hooks or m._forward_pre_hooks for m in net.stage_containers())
+
+
+def _interleave(rgen, vgen, side):
+    """Advance the ResNet generator (current stream) and the ViT generator (side stream) one
+    stage at a time, in proportion to their stage counts (18 and 14); returns both outputs."""
+    out = [None, None]
+    live = [True, True]
+    credit = [0.0, 0.0]
+    share = (18.0 / 14.0, 1.0)
+
+    def advance(i):
+        try:
+            if i == 0:
+                next(rgen)
+            else:
+                with torch.cuda.stream(side):
+                    next(vgen)
+        except StopIteration as e:
+            out[i] = e.value
+            live[i] = False
+
+    while live[0] or live[1]:
+        for i in (1, 0):  # the ViT (critical path) first
+            if live[i]:
+                credit[i] += share[i]
+                while live[i] and credit[i] >= 1.0:
+                    credit[i] -= 1.0
+                    advance(i)
+    return out[0], out[1]
 
 
 class MultimodalFusionModel(tnn.Module):
@@ -81,10 +127,14 @@ class MultimodalFusionModel(tnn.Module):
         side = Fn.side_stream(rgb.device)
         side.wait_stream(main)
         with Fn.concurrent_encoders():
-            with torch.cuda.stream(side):
-                thermal.record_stream(side)
-                th_feat = th_net(thermal)
-            rgb_feat = rgb_net(rgb)
+            thermal.record_stream(side)
+            if _INTERLEAVE and _stageable(rgb_net) and _stageable(th_net):
+                rgb_feat, th_feat = _interleave(rgb_net.forward_stages(rgb),
+                                                th_net.forward_stages(thermal), side)
+            else:
+                with torch.cuda.stream(side):
+                    th_feat = th_net(thermal)
+                rgb_feat = rgb_net(rgb)
         main.wait_stream(side)
         th_feat.record_stream(main)
         return rgb_feat, th_feat

@@ -123,6 +123,25 @@ class ResNet(tnn.Module):
         x = torch.flatten(x, 1)
         return self.fc(x)
 
+    def forward_stages(self, x):
+        """forward() as a generator that yields after the stem and after every Bottleneck and
+        returns the output (StopIteration.value): models.fusion interleaves the two encoders'
+        stages so both streams get work early and their backward nodes alternate in the
+        autograd engine's queue.  The same modules are called as in forward(); only the
+        containers' own calls are skipped (fusion uses it when no hook sits on them)."""
+        x = Fn.StemFn.apply(x, self.conv1.weight, self.bn1.weight, self.bn1.bias, self)
+        yield
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                x = blk(x)
+                yield
+        x = self.avgpool(x)
+        x = torch.flatten(x, 1)
+        return self.fc(x)
+
+    def stage_containers(self):
+        return (self, self.layer1, self.layer2, self.layer3, self.layer4)
+
 
 def resnet50(num_classes=1000, zero_init_residual=False):
     return ResNet((3, 4, 6, 3), num_classes=num_classes, zero_init_residual=zero_init_residual)

@@ -157,6 +157,22 @@ class VisionTransformer(tnn.Module):
         x = self.head_drop(x)
         return self.head(x)
 
+    def forward_stages(self, x):
+        """forward() as a generator yielding after the embedding and every Block (see
+        models.resnet.ResNet.forward_stages)."""
+        x = self._embed(x)
+        yield
+        for blk in self.blocks:
+            x = blk(x)
+            yield
+        x = Fn.TokenNormFn.apply(x, self.norm.weight, self.norm.bias, self.norm)
+        x = self.fc_norm(x)
+        x = self.head_drop(x)
+        return self.head(x)
+
+    def stage_containers(self):
+        return (self, self.blocks)
+
 
 def vit_base_patch16_224(num_classes=1000, **kw):
     return VisionTransformer(img_size=224, patch_size=16, embed_dim=768, depth=12, num_heads=12,
