@@ -51,7 +51,15 @@ def test_eval_logits_and_probabilities():
     print(f"\n[eval B={B}] |logits|max={f32.abs().max().item():.3e}  HIP vs bf16 oracle {d_emu:.3e}, "
           f"HIP vs fp32 oracle {d_f32:.3e}, bf16 vs fp32 oracle {gap:.3e}")
     assert torch.isfinite(out).all()
-    assert d_f32 <= max(1e-3, 1.5 * gap + 1e-3)
+    assert d_f32 <= 5e-3  # fixed bar for bf16 (the bf16-rounded oracle's own gap is ~2e-3)
+    # the fp32-accurate forward: north_star's 1e-3, fixed
+    from dfu_hip import functional as Fn
+    with torch.no_grad(), Fn.precision("bf16x3"):
+        out3 = hip(rgb.to(DEV), th.to(DEV)).float().cpu()
+    d3 = (out3 - f32).abs().max().item()
+    print(f"  bf16x3 eval vs fp32 oracle {d3:.3e} (bar 1e-3)")
+    assert d3 <= 1e-3
+    assert (torch.softmax(out3, 1)[:, 1] - torch.softmax(f32, 1)[:, 1]).abs().max().item() < 1e-3
     p_hip = torch.softmax(out, 1)[:, 1]
     p_ref = torch.softmax(f32, 1)[:, 1]
     assert (p_hip - p_ref).abs().max().item() < 1e-3

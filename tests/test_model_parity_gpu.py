@@ -10,12 +10,16 @@ ResNet initialisation, train-mode BatchNorm:
     max |logits(HIP) - logits(fp32 oracle)| <= 1e-3 (LOGIT_ATOL, train_multimodal_fusion.py:
     374-376), and the same for the loss.
   * precision "bf16" (the default, benchmarked mode): bf16 storage alone moves the logits of the
-    fp32 oracle itself by more than 1e-3, so it is held to the oracle's own bf16
-    band: no further from the bf16-rounded oracle than two realisations of that oracle (CPU,
-    GPU) are from each other.  Its fp32-oracle delta is reported.
+    fp32 oracle itself by 7.2e-2 at C3 with torchvision's default (zero_init_residual=False)
+    initialisation -- the random-init ResNet amplifies rounding chaotically -- and
+    by 2.4e-3 with zero_init_residual=True.  Held to FIXED bars: 0.1 at default init, 5e-3
+    with zero-init residuals (both at B = 64).
+  * gradients (the backward is bf16 in both modes): FIXED bars per parameter against the fp32
+    oracle -- relative L2 error and cosine similarity -- so a wrong-sign or garbage gradient
+    fails; the bf16-rounded oracle's own errors are recorded beside them.
 
-Every measured delta is written to gpurun_out/parity_r03.json (DFU_PARITY_JSON overrides) and
-committed as profiles/r03_parity.json.
+Every measured delta is written to gpurun_out/parity_r10.json (DFU_PARITY_JSON overrides) and
+committed as profiles/r10_parity.json.
 """
 import copy
 import json
@@ -32,7 +36,7 @@ LOGIT_ATOL = 1e-3  # north_star: "logits match the reference CPU path within 1e-
 B_C3 = 64          # BASELINE.json C3: fusion bs=64
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PARITY_JSON = os.environ.get("DFU_PARITY_JSON",
-                             os.path.join(REPO, "gpurun_out", "parity_r03.json"))
+                             os.path.join(REPO, "gpurun_out", "parity_r10.json"))
 
 
 def _record(key, value):
@@ -143,29 +147,49 @@ def test_c3_logits_bf16x3_within_1e3_of_fp32_oracle(c3):
     assert dl <= LOGIT_ATOL
 
 
+def _grad_errors(grads, ref_m, other_m=None):
+    """[(rel L2 err, cosine, other's rel err, name)] per parameter with a non-zero reference
+    gradient, worst first."""
+    rp = dict(ref_m.named_parameters())
+    ro = dict(other_m.named_parameters()) if other_m is not None else {}
+    out = []
+    for n, g in grads.items():
+        r = rp[n].grad
+        if r.norm().item() == 0.0:
+            continue
+        cos = torch.nn.functional.cosine_similarity(g.flatten().double(), r.flatten().double(),
+                                                    dim=0).item()
+        out.append((rel(g, r), cos, rel(ro[n].grad, r) if n in ro else None, n))
+    return sorted(out, key=lambda t: t[0], reverse=True)
+
+
+# fixed gradient bars (the backward is bf16): every parameter, and the median
+GRAD_REL_MAX, GRAD_COS_MIN, GRAD_REL_MEDIAN = 0.3, 0.95, 0.03
+
+
 def test_c3_grads_bf16x3_vs_fp32_oracle(c3):
-    """Parameter gradients of the bf16x3 step against the fp32 oracle.  Its backward is the
-    bf16 one, so every parameter is held to the bf16-rounded oracle's own distance from the
-    fp32 oracle (relative L2, x1.5 + 1e-2).  (The head's gradients are not held tighter: the
-    few-1e-4 feature differences of the chaotic default-init ResNet flip a handful of the
-    64 x 512 head ReLU masks; the head's own arithmetic is pinned to the reference's code at
-    rtol 1e-5 by tests/test_golden_gpu.py.)"""
+    """Parameter gradients of the bf16x3 step against the fp32 oracle at C3 (default init),
+    FIXED bars: rel L2 <= 0.3 and cosine >= 0.95 for every parameter, median rel <= 0.03.
+    (The bf16-rounded oracle itself misses these by far on the early BN parameters -- rel
+    1.2-1.6: its forward is chaotic at this init -- which is why the forward is bf16x3 here.)"""
     f32, emu, h = c3["f32"], c3["emu"], c3["x3"]
-    rp = dict(f32["m"].named_parameters())
-    re = dict(emu["m"].named_parameters())
-    errs = sorted(((rel(g, rp[n].grad), rel(re[n].grad, rp[n].grad), n)
-                   for n, g in h["grads"].items()), reverse=True)
-    for e, b, n in errs[:6]:
-        print(f"  grad rel err vs fp32 oracle {n}: {e:.3e} (bf16 oracle: {b:.3e})")
-    _record("c3_b64_bf16x3_grads", {"worst": [[n, e, b] for e, b, n in errs[:10]],
-                                    "median": errs[len(errs) // 2][0],
-                                    "columns": "param, HIP bf16x3 rel err, bf16 oracle rel err"})
-    for e, b, n in errs:
-        assert e <= 1.5 * b + 1e-2, (n, e, b)
+    errs = _grad_errors(h["grads"], f32["m"], emu["m"])
+    for e, c, b, n in errs[:6]:
+        print(f"  grad vs fp32 oracle {n}: rel {e:.3e} cos {c:.5f} (bf16 oracle rel {b:.3e})")
+    med = errs[len(errs) // 2][0]
+    _record("c3_b64_bf16x3_grads", {"worst": [[n, e, c, b] for e, c, b, n in errs[:10]],
+                                    "median": med, "min_cos": min(c for _, c, _, _ in errs),
+                                    "bars": [GRAD_REL_MAX, GRAD_COS_MIN, GRAD_REL_MEDIAN],
+                                    "columns": "param, HIP rel err, cosine, bf16 oracle rel err"})
+    for e, c, b, n in errs:
+        assert e <= GRAD_REL_MAX and c >= GRAD_COS_MIN, (n, e, c)
+    assert med <= GRAD_REL_MEDIAN, med
 
 
-def test_c3_logits_bf16_within_oracle_band(c3):
-    """Default bf16 precision: within the oracle's own bf16 band (see module docstring)."""
+def test_c3_logits_bf16_fixed_bar(c3):
+    """Default bf16 precision at C3, default init: FIXED bar 0.1 against the fp32 oracle (the
+    bf16-rounded oracle's own gap is 7.2e-2 here, see the module docstring); the
+    bf16-rounded oracle's CPU-vs-GPU band is recorded beside it."""
     f32, emu, emu_gpu, h = c3["f32"], c3["emu"], c3["emu_gpu"], c3["bf16"]
     band = _maxd(emu_gpu, emu)
     d_emu, d_f32 = _maxd(h, emu), _maxd(h, f32)
@@ -176,9 +200,40 @@ def test_c3_logits_bf16_within_oracle_band(c3):
     _record("c3_b64_bf16", {"max_abs_logits_vs_bf16_oracle": d_emu,
                             "max_abs_logits_vs_fp32_oracle": d_f32,
                             "oracle_bf16_cpu_vs_gpu_band": band,
-                            "oracle_bf16_vs_fp32_gap": q_gap})
-    assert d_emu <= 2 * band + LOGIT_ATOL
-    assert d_f32 <= 2 * q_gap + LOGIT_ATOL
+                            "oracle_bf16_vs_fp32_gap": q_gap, "bar": 0.1})
+    assert d_f32 <= 0.1
+
+
+def test_c3_zero_init_residual_fixed_bars():
+    """C3's batch (B = 64) with torchvision's zero_init_residual=True (the well-conditioned
+    init): bf16x3 logits within 1e-3 of the fp32 oracle, bf16 logits within 5e-3 (the
+    bf16-rounded oracle's own gap: 2.4e-3), and both modes' gradients under the fixed bars
+    (bf16: rel <= 0.4, cosine >= 0.9, median <= 0.1 -- the bf16-rounded oracle's own worst is
+    0.2 and median 0.05 here: the BN backward's mean subtraction amplifies bf16 rounding)."""
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref, hip = _models(zero_init_residual=True)
+    rgb, th, y = R.synthetic_batch(B_C3, seed=42)
+    w = R.class_weights(y)
+    f32 = _oracle(ref, rgb, th, y, w, False)
+    x3 = _hip(hip, rgb, th, y, w, "bf16x3")
+    bf = _hip(hip, rgb, th, y, w, "bf16")
+    d3, db = _maxd(x3, f32), _maxd(bf, f32)
+    e3 = _grad_errors(x3["grads"], f32["m"])
+    eb = _grad_errors(bf["grads"], f32["m"])
+    print(f"\n[C3 B={B_C3} zero-init] logits vs fp32 oracle: bf16x3 {d3:.3e} (bar 1e-3), bf16 "
+          f"{db:.3e} (bar 5e-3); grads worst rel bf16x3 {e3[0][0]:.3e} bf16 {eb[0][0]:.3e}")
+    _record("c3_b64_zero_init", {"bf16x3_max_abs_logits_vs_fp32_oracle": d3,
+                                 "bf16_max_abs_logits_vs_fp32_oracle": db,
+                                 "bf16x3_grads_worst": [[n, e, c] for e, c, _, n in e3[:5]],
+                                 "bf16_grads_worst": [[n, e, c] for e, c, _, n in eb[:5]],
+                                 "bf16x3_grads_median": e3[len(e3) // 2][0],
+                                 "bf16_grads_median": eb[len(eb) // 2][0]})
+    assert d3 <= LOGIT_ATOL and db <= 5e-3
+    for errs, rmax, cmin, med in ((e3, GRAD_REL_MAX, GRAD_COS_MIN, GRAD_REL_MEDIAN),
+                                  (eb, 0.4, 0.9, 0.1)):
+        for e, c, _, n in errs:
+            assert e <= rmax and c >= cmin, (n, e, c)
+        assert errs[len(errs) // 2][0] <= med
 
 
 def test_well_conditioned_b8_grads_within_oracle_band():
