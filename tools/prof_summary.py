@@ -92,6 +92,9 @@ def main():
     ap.add_argument("--traffic-json", help="write the GEMM-family traffic per launch here")
     ap.add_argument("--bench")
     ap.add_argument("--title", default="rocprofv3 --kernel-trace --stats of bench.py")
+    ap.add_argument("--trace", help="the run's kernel_trace.csv: also report the GEMM family's "
+                                    "per-launch time over bench.py's timed roofline replays")
+    ap.add_argument("--replays", type=int, default=3, help="timed replays (bench.py: 3)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.stats)))
     S = a.steps
@@ -132,6 +135,21 @@ def main():
     print(f"\nGEMM family (gemm_kernel + its split-K reductions): {g_calls} launches, "
           f"**{per_launch_us:.2f} us per launch** (bench.py's `avg_launch_us` measures the same "
           f"launches with HIP events around back-to-back replays).\n")
+    if a.trace and a.bench:
+        b = json.loads(open(a.bench).read().strip().splitlines()[-1])
+        L = b["roofline"]["launches_per_step"]
+        ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                    for r in csv.DictReader(open(a.trace)))
+        fam = [k for k in ks if is_gemm(k[2]) or "k_splitk_reduce" in k[2]]
+        gi = [i for i, k in enumerate(fam) if is_gemm(k[2])]
+        first = gi[-a.replays * L]  # the first GEMM of the timed replays (the last ones traced)
+        win = fam[first:]
+        busy = sum(e - st for st, e, _ in win) / 1e3 / (a.replays * L)
+        wall = (win[-1][1] - win[0][0]) / 1e3 / (a.replays * L)
+        print(f"Over bench.py's {a.replays} timed roofline replays in this trace (the same "
+              f"{L} launches back to back on one stream, as `avg_launch_us` times them): "
+              f"**{busy:.2f} us per launch** of kernel time, {wall:.2f} us per launch from the "
+              f"first start to the last end (bench line: {b['roofline']['avg_launch_us']} us).\n")
     if a.fetch and a.write:
         fetch, fn = pmc_by_kernel(a.fetch, "FETCH_SIZE")
         write, wn = pmc_by_kernel(a.write, "WRITE_SIZE")
