@@ -34,5 +34,8 @@ dq = torch.empty_like(qkv)
 fl = 4.0 * N * N * dh * B * H
 tf = timeit(lambda: ops.attention_fwd(qkv, B, N, H, dh, scale))
 tb = timeit(lambda: ops.attention_bwd(qkv, o, dout, lse, B, N, H, dh, scale, dq))
+qf = qkv.float()
+qb = torch.empty_like(qkv)
+tx = timeit(lambda: ops.attention_fwd_f32(qf, B, N, H, dh, scale, qkv_bf16=qb))
 print(f"attention fwd {tf:.1f} us ({fl / tf / 1e6:.0f} TFLOP/s)  bwd {tb:.1f} us "
-      f"({2.5 * fl / tb / 1e6:.0f} TFLOP/s)")
+      f"({2.5 * fl / tb / 1e6:.0f} TFLOP/s)  fwd bf16x3 {tx:.1f} us")
