@@ -478,7 +478,7 @@ DFU_DEV void load_bias(const float* bias, int n0w, int N, int lane, float (&b)[F
 // v_permlane16_swap per dword so every lane stores 8 consecutive columns (16 B): lane group g
 // takes columns 16j + 16(g&1) + 8(g>>1) .. +7, the 4 lanes of a row cover 64 contiguous bytes,
 // and one dwordx4 replaces two dwordx2 (HIP guide T21, for the 16x16 accumulator layout).
-template <int FN>
+template <int FN, int AUX = 0>
 DFU_DEV void st_row_bf16(rsrc_t r, int64_t rowe, bool okm, int n0w, int N, bool n8, bool n4,
                          int lane, const float (&v)[FN][4]) {
   static_assert(FN % 2 == 0, "fragment pairs");
@@ -493,7 +493,7 @@ DFU_DEV void st_row_bf16(rsrc_t r, int64_t rowe, bool okm, int n0w, int N, bool 
       const auto ry = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
       const u32x4 q = {rx[0], ry[0], rx[1], ry[1]};
       const int col = n0w + 16 * j + cofs;
-      __builtin_amdgcn_raw_buffer_store_b128(q, r, boff(okm && col < N, (rowe + col) * 2), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(q, r, boff(okm && col < N, (rowe + col) * 2), 0, AUX);
     }
   } else {
     const int lcol = 4 * (lane >> 4);

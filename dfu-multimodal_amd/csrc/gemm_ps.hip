@@ -22,7 +22,7 @@ namespace {
 
 // Timing ablations (tools/build_ablate.sh builds a separate library with -DDFU_PS_ABLATE=mask;
 // the product build is 0): 1 no epilogue, 2 no MFMA, 4 no DMA, 8 no fragment reads (zero
-// fragments), 16 no K-step barrier.  Results are wrong in every ablated build.
+// fragments), 16 no K-step barrier, 32 epilogue accesses out of range (issued, no traffic).  Results are wrong in every ablated build.
 #ifndef DFU_PS_ABLATE
 #define DFU_PS_ABLATE 0
 #endif
@@ -35,6 +35,11 @@ constexpr int kAbl = DFU_PS_ABLATE;
 #define DFU_PS_SCHED 0
 #endif
 constexpr int kSched = DFU_PS_SCHED;
+// Cache-policy bits of the epilogue's output stores (experiment builds: -DDFU_PS_STAUX=2 = nt)
+#ifndef DFU_PS_STAUX
+#define DFU_PS_STAUX 0
+#endif
+constexpr int kStAux = DFU_PS_STAUX;
 
 constexpr int PS_IMG = 256 * 128;   // one operand image: 256 rows x 64 k x 2 B
 constexpr int PS_BUF = 2 * PS_IMG;  // A + B
@@ -81,7 +86,8 @@ DFU_DEV void bl16(rsrc_t r, uint32_t off, char* lds_dst) {
 
 // Half-tile h of K-step k0 into `img` (two wave-instructions per thread; wave = tid >> 6, kept
 // wave-uniform by the caller so the LDS destination is scalar).
-template <bool KC>
+// NCH: 64-row chunks of a K-contiguous image (4; 3 for the 192-row A operand: chunk 3 unused).
+template <bool KC, int NCH = 4>
 DFU_DEV void ps_issue(const PsSrc<KC>& s, rsrc_t r, int64_t ld, int k0, int K, int h, char* img,
                       int tid, int wave) {
   if constexpr (KC) {
@@ -89,6 +95,7 @@ DFU_DEV void ps_issue(const PsSrc<KC>& s, rsrc_t r, int64_t ld, int k0, int K, i
     const bool kin = k0 + kc_lane_chunk(tid & 63) * 8 < K;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (2 * h + i >= NCH) continue;  // (h is a literal at every call: folds)
       const bool ok = kin & s.ok[2 * h + i];
       bl16(r, ok ? s.off[2 * h + i] + 2u * (uint32_t)k0 : kOOB,
            img + h * 16384 + i * 8192 + wave * 1024);
@@ -104,23 +111,26 @@ DFU_DEV void ps_issue(const PsSrc<KC>& s, rsrc_t r, int64_t ld, int k0, int K, i
   }
 }
 
-// Vector-memory instructions a wave issues in one epilogue after its last waited load.
-template <int EPI>
+// Vector-memory instructions a wave issues in one epilogue after its last waited load
+// (FMH: 16-row fragments per wave per tile half; 2 FMH fragment rows per wave).
+template <int EPI, int FMH = 4>
 DFU_DEV int ps_epi_stores(const GemmArgs& p) {
   constexpr bool bf16_out = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_GELU ||
                             EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD;
-  const int per = bf16_out && p.n8 ? 16 : 32 * (p.n4 ? 1 : 4);
+  constexpr int NI = 2 * FMH;
+  const int per = bf16_out && p.n8 ? 2 * NI : 4 * NI * (p.n4 ? 1 : 4);
   // dGELU with column sums (p.stats): four more 16-B stores per wave (scalar: sixteen)
   const int cs = EPI == DFU_EPI_BF16_DGELU && p.stats ? (p.n4 ? 4 : 16) : 0;
-  if constexpr (EPI == DFU_EPI_X3_GELU) return 4 * (p.n8 ? 16 : 32 * (p.n4 ? 1 : 4));
+  if constexpr (EPI == DFU_EPI_X3_GELU) return 4 * (p.n8 ? 2 * NI : 4 * NI * (p.n4 ? 1 : 4));
   return (EPI == DFU_EPI_BF16_GELU ? 2 * per : per) + cs;
 }
 
-// lane holds C[m0 + (i>>2)*128 + wr*64 + (i&3)*16 + (lane&15)]
+// lane holds C[m0 + (i / FMH) * 32 FMH + wr * 16 FMH + (i % FMH) * 16 + (lane&15)]
 //              [n0 + (j>>1)*128 + wc*32 + (j&1)*16 + 4*(lane>>4) + r]
-template <int EPI>
-DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc,
-                         int lane, int sidx) {
+// (FMH = 4: the 256-row tile, m0 + (i>>2)*128 + wr*64 + (i&3)*16; FMH = 3: the 192-row tile)
+template <int EPI, int FMH = 4>
+DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, int n0, int wr,
+                         int wc, int lane, int sidx) {
   const bool n4 = p.n4 != 0;
   const int M = p.M, N = p.N;
   const rsrc_t rc = make_rsrc(p.C);
@@ -156,9 +166,9 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
     }
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + (i >> 2) * 128 + wr * 64 + (i & 3) * 16 + (lane & 15);
-    const bool okm = m < M;
+  for (int i = 0; i < 2 * FMH; ++i) {
+    const int m = m0 + (i / FMH) * 32 * FMH + wr * 16 * FMH + (i % FMH) * 16 + (lane & 15);
+    const bool okm = (kAbl & 32) ? (m < 0) : (m < M);  // ablation 32: every access out of range
     const int64_t mc = okm ? m : 0;
 #pragma unroll
     for (int hb = 0; hb < 2; ++hb) {
@@ -169,15 +179,15 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[jj][r] = acc[i][2 * hb + jj][r] * p.alpha + bias[2 * hb + jj][r];
       if constexpr (EPI == DFU_EPI_BF16) {
-        st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+        st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
       } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
         float g[2][4], d[2][4];
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
           for (int r = 0; r < 4; ++r) gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
-        st_row_bf16<2>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
-        st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, kStAux>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
+        st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
       } else if constexpr (EPI == DFU_EPI_X3_GELU) {
         // gelu(pre) as the split triple hi = bf16(g), lo = bf16(g - hi): segments hi | lo | hi
         float g[2][4], d[2][4], lo[2][4];
@@ -188,15 +198,15 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
             gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
             lo[jj][r] = g[jj][r] - bf2f(f2bf(g[jj][r]));
           }
-        st_row_bf16<2>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
-        st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
-        st_row_bf16<2>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, lo);
-        st_row_bf16<2>(rc, mc * p.ldc + 2 * N, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, kStAux>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
+        st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, kStAux>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, lo);
+        st_row_bf16<2, kStAux>(rc, mc * p.ldc + 2 * N, okm, n0w, N, p.n8, n4, lane, g);
       } else if constexpr (EPI == DFU_EPI_F32) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int n = n0w + jj * 16 + 4 * (lane >> 4);
-          st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+          st4_f32<kStAux>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
         }
       } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
 #pragma unroll
@@ -214,7 +224,7 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) cs[hb][jj][r] += okm ? bf2f(f2bf(v[jj][r])) : 0.f;
         }
-        st_row_bf16<2>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+        st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
       } else if constexpr (EPI == DFU_EPI_F32_ACC) {  // split-K slab, or C += acc unsplit
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
@@ -226,7 +236,7 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
             ld4_f32(rc, mc * p.ldc + n, okm, n, N, n4, c);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[jj][r] += c[r];
-            st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+            st4_f32<kStAux>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
           }
         }
       } else {  // DFU_EPI_F32_RESID
@@ -237,15 +247,15 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
           ld4_f32(ra, mc * p.ldaux + n, okm, n, N, n4, x);
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[jj][r] += x[r];
-          st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+          st4_f32<kStAux>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
         }
       }
     }
   }
   if constexpr (EPI == DFU_EPI_BF16_DGELU) {
-    if (p.stats) {  // row (m0 / 256) * 2 + wr of the [2 * tiles_m][N] partial slab
+    if (p.stats) {  // row (m0 / TM) * 2 + wr of the [2 * tiles_m][N] partial slab
       const rsrc_t rs = make_rsrc(p.stats);
-      const int64_t prow = (int64_t)(m0 / 256) * 2 + wr;
+      const int64_t prow = (int64_t)(m0 / (64 * FMH)) * 2 + wr;
       const bool lead = (lane & 15) == 0;
 #pragma unroll
       for (int hb = 0; hb < 2; ++hb)
@@ -261,10 +271,15 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, 
   }
 }
 
-template <int AMODE, int BMODE, int EPI>
+// TMH: rows per tile half (128: the 256 x 256 tile; 96: 192 x 256, K-contiguous A only -- for
+// N = 768 outputs, whose 256-row tiling leaves 41 % of the CUs idle: 150 tiles at M = 12608).
+template <int AMODE, int BMODE, int EPI, int TMH = 128>
 __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   constexpr bool AK_ = AMODE == DFU_OPND_KMAJOR;  // A K-contiguous (else MN-major: wgrad)
   constexpr bool BK_ = BMODE == DFU_OPND_KMAJOR;  // B K-contiguous (else MN-major)
+  constexpr int FMH = TMH / 32;  // 16-row fragments per wave per half
+  constexpr int TMt = 2 * TMH;
+  static_assert(TMH == 128 || (TMH == 96 && AK_), "192-row tile: K-contiguous A only");
   __shared__ __attribute__((aligned(16))) char smem[PS_LDS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
@@ -301,7 +316,7 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     const int g0 = (t / band) * GROUP_M;
     const int gm = min(GROUP_M, p.tiles_m - g0);
     const int within = t - (t / band) * band;
-    m0 = (g0 + within % gm) * 256;
+    m0 = (g0 + within % gm) * TMt;
     n0 = (within / gm) * 256;
     kb = s * p.kt_per_split;
     nk = min(p.ktiles, kb + p.kt_per_split) - kb;
@@ -324,7 +339,7 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
                                                         p.b_bytes, 0x00020000);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto issue_a = [&](int k0_, int h, char* img) {
-    if constexpr (!(kAbl & 4)) ps_issue<AK_>(sa, ra_, p.lda, k0_, p.K, h, img, tid, wave_u);
+    if constexpr (!(kAbl & 4)) ps_issue<AK_, TMt / 64>(sa, ra_, p.lda, k0_, p.K, h, img, tid, wave_u);
   };
   auto issue_b = [&](int k0_, int h, char* img) {
     if constexpr (!(kAbl & 4)) ps_issue<BK_>(sb, rb_, p.ldb, k0_, p.K, h, img, tid, wave_u);
@@ -347,9 +362,9 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     }
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[2 * FMH][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 2 * FMH; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -362,8 +377,79 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     issue_a(k0, 1, smem);
     advance_issue();
   }
-  const int E = (kAbl & 1) ? 0 : ps_epi_stores<EPI>(p);
+  const int E = (kAbl & 1) ? 0 : ps_epi_stores<EPI, FMH>(p);
   bool epi_last = false;  // an epilogue ran at the end of the previous K-step
+  // Fragment registers hold one A half (fa) and one B half (fb); each phase's MFMAs run one
+  // k-half (ks) at a time, and the reads the NEXT group needs go out as soon as the group before
+  // it has consumed the registers they overwrite, so every read has a group of 8 MFMAs (this
+  // wave's and its SIMD partner's) to land under instead of stalling the pipe (the compiler's
+  // lgkmcnt waits are the exact ones for K-contiguous reads; MN-major ones are asm, retired by an
+  // lgkmcnt(0) in front of each group).
+  // kSched bit 2: both B halves stay in registers (fbh[hb]), so phase 4 does not re-read B-left.
+  // kSched bit 4 (16): K-step g+1's DMA wait and barrier move in front of K-step g's last MFMA
+  // group, and K-step g+1's first fragment reads go out right behind that group (the reads'
+  // latency and the barrier's skew land under the group instead of idling the pipe at the top of
+  // every K-step).  RAW: each wave waits for its own DMA of K-step g+1 before the barrier.  WAR:
+  // every wave retires its LDS reads (lgkmcnt(0)) before that barrier, and the DMA that refills
+  // K-step g's buffer is issued after it.
+  // kSched bit 5 (32): the next K-step's DMA goes out two pieces behind each of the first four
+  // MFMA groups (after that group's fragment reads) instead of in two bursts beside the reads.
+  constexpr bool kB2 = (kSched & 4) != 0;
+  constexpr bool kEarly = (kSched & 16) != 0;
+  constexpr bool kSpread = (kSched & 32) != 0;
+  bf16x8 fa[FMH][2], fbh[2][2][2];
+  if constexpr ((kAbl & 8) != 0) {
+#pragma unroll
+    for (int i = 0; i < FMH; ++i) fa[i][0] = fa[i][1] = (bf16x8){};
+    fbh[0][0][0] = fbh[0][0][1] = fbh[0][1][0] = fbh[0][1][1] = (bf16x8){};
+    fbh[1][0][0] = fbh[1][0][1] = fbh[1][1][0] = fbh[1][1][1] = (bf16x8){};
+  }
+  auto rd_a = [&](const char* la, int h, int ks) {
+    if constexpr ((kAbl & 8) != 0) return;
+#pragma unroll
+    for (int i = 0; i < FMH; ++i)
+      fa[i][ks] = read_frag<AK_>(la, h * TMH + wr * (TMH / 2) + i * 16, ks, lane);
+  };
+  auto rd_b = [&](const char* lb, int h, int ks) {
+    if constexpr ((kAbl & 8) != 0) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      fbh[kB2 ? h : 0][j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
+  };
+  // the first group's reads of a K-step (A-top, B-left, both k-halves)
+  auto rd_first = [&](const char* la) {
+    rd_a(la, 0, 0);
+    rd_b(la + PS_IMG, 0, 0);
+    rd_a(la, 0, 1);
+    rd_b(la + PS_IMG, 0, 1);
+  };
+  auto mf = [&](int ha, int hb, int ks) {
+    if constexpr ((kAbl & 2) != 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
+    if constexpr (!AK_ || !BK_) {  // asm (MN-major) fragment reads: retired before use
+      lds_reads_retired();
+#pragma unroll
+      for (int i = 0; i < FMH; ++i) pin(fa[i][ks]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) pin(fbh[kB2 ? hb : 0][j][ks]);
+    }
+    if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FMH; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[ha * FMH + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            fbh[kB2 ? hb : 0][j][ks], fa[i][ks], acc[ha * FMH + i][hb * 2 + j], 0, 0, 0);
+    if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if constexpr (kEarly) {  // K-step 0: landed, published, first reads out
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    rd_first(smem);
+  }
   for (int g = 0; g < total; ++g) {
     const char* la = smem + (g & 1) * PS_BUF;
     const char* lb = la + PS_IMG;
@@ -371,65 +457,16 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     char* nb = na + PS_IMG;
     const bool nxt = g + 1 < total;
     const int k1 = (ikb + ik) * BK;  // the next K-step (issue cursor)
-    // Fragment registers hold one A half (fa) and one B half (fb); each phase's MFMAs run one
-    // k-half (ks) at a time, and the reads the NEXT group needs go out as soon as the group
-    // before it has consumed the registers they overwrite, so every read has a group of 8
-    // MFMAs (this wave's and its SIMD partner's) to land under instead of stalling the pipe
-    // (the compiler's lgkmcnt waits are the exact ones for K-contiguous reads; MN-major ones are
-    // asm, retired by an lgkmcnt(0) in front of each group).
-    // kSched bit 2: both B halves stay in registers (fbh[hb]), so phase 4 does not re-read B-left
-    constexpr bool kB2 = (kSched & 4) != 0;
-    bf16x8 fa[4][2], fbh[2][2][2];
-    if constexpr ((kAbl & 8) != 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i][0] = fa[i][1] = (bf16x8){};
-      fbh[0][0][0] = fbh[0][0][1] = fbh[0][1][0] = fbh[0][1][1] = (bf16x8){};
-      fbh[1][0][0] = fbh[1][0][1] = fbh[1][1][0] = fbh[1][1][1] = (bf16x8){};
-    }
-    auto rd_a = [&](int h, int ks) {
-      if constexpr ((kAbl & 8) != 0) return;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i][ks] = read_frag<AK_>(la, h * 128 + wr * 64 + i * 16, ks, lane);
-    };
-    auto rd_b = [&](int h, int ks) {
-      if constexpr ((kAbl & 8) != 0) return;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fbh[kB2 ? h : 0][j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
-    };
-    auto mf = [&](int ha, int hb, int ks) {
-      if constexpr ((kAbl & 2) != 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        return;
-      }
-      if constexpr (!AK_ || !BK_) {  // asm (MN-major) fragment reads: retired before use
-        lds_reads_retired();
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pin(fa[i][ks]);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) pin(fbh[kB2 ? hb : 0][j][ks]);
-      }
-      if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              fbh[kB2 ? hb : 0][j][ks], fa[i][ks], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
-      if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-    };
     const bool row0 = __builtin_amdgcn_readfirstlane(wr) == 0;
-    // this K-step's DMA landed (younger: only the previous epilogue's stores), then published
-    if (epi_last)
-      wait_vm_le<63>(E);
-    else
-      wait_vmcnt<0>();
-    if constexpr (!(kAbl & 16)) __builtin_amdgcn_s_barrier();
-    rd_a(0, 0);
-    rd_b(0, 0);
-    rd_a(0, 1);
-    rd_b(0, 1);
+    if constexpr (!kEarly) {
+      // this K-step's DMA landed (younger: only the previous epilogue's stores), then published
+      if (epi_last)
+        wait_vm_le<63>(E);
+      else
+        wait_vmcnt<0>();
+      if constexpr (!(kAbl & 16)) __builtin_amdgcn_s_barrier();
+      rd_first(la);
+    }
     if constexpr (kSched & 1) {
       if (nxt && row0) {
         issue_a(k1, 0, na);
@@ -438,15 +475,19 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
         issue_a(k1, 1, na);
         advance_issue();
       }
-    } else if (nxt) {
+    } else if (nxt && !kSpread) {
       issue_a(k1, 0, na);
       issue_b(k1, 0, nb);
     }
     __builtin_amdgcn_sched_barrier(0);
     mf(0, 0, 0);   // A-top x B-left
-    rd_b(1, 0);
+    rd_b(lb, 1, 0);
+    if constexpr (kSpread) {
+      if (nxt) issue_a(k1, 0, na);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     mf(0, 0, 1);
-    rd_b(1, 1);
+    rd_b(lb, 1, 1);
     if constexpr (kSched & 1) {
       if (nxt && !row0) {
         issue_a(k1, 0, na);
@@ -455,6 +496,8 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
         issue_a(k1, 1, na);
         advance_issue();
       }
+    } else if (kSpread) {
+      if (nxt) issue_b(k1, 0, nb);
     } else if (nxt) {
       issue_b(k1, 1, nb);
       issue_a(k1, 1, na);
@@ -462,27 +505,46 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     }
     __builtin_amdgcn_sched_barrier(0);
     mf(0, 1, 0);   // A-top x B-right
-    rd_a(1, 0);
+    rd_a(la, 1, 0);
+    if constexpr (kSpread) {
+      if (nxt) issue_b(k1, 1, nb);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     mf(0, 1, 1);
-    rd_a(1, 1);
+    rd_a(la, 1, 1);
+    if constexpr (kSpread) {
+      if (nxt) {
+        issue_a(k1, 1, na);
+        advance_issue();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     mf(1, 1, 0);   // A-bottom x B-right
-    if constexpr (!kB2) rd_b(0, 0);
+    if constexpr (!kB2) rd_b(lb, 0, 0);
     mf(1, 1, 1);
-    if constexpr (!kB2) rd_b(0, 1);
+    if constexpr (!kB2) rd_b(lb, 0, 1);
     mf(1, 0, 0);   // A-bottom x B-left
+    if constexpr (kEarly) {
+      if (nxt) {  // K-step g+1: landed (older: at most an epilogue's stores), reads retired, published
+        wait_vmcnt<0>();
+        lds_reads_retired();
+        __builtin_amdgcn_s_barrier();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     mf(1, 0, 1);
     epi_last = false;
     if (++ck == cnk) {
       if constexpr (!(kAbl & 1)) {
-        ps_epilogue<EPI>(p, acc, cm0, cn0, wr, wc, lane, cu / tiles);
+        ps_epilogue<EPI, FMH>(p, acc, cm0, cn0, wr, wc, lane, cu / tiles);
       } else {  // keep the accumulators (and so every MFMA) alive without storing them
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 2 * FMH; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 2 * FMH; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
       epi_last = true;
@@ -491,6 +553,9 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
         cu = unit_at(ci);
         unit_geom(cu, cm0, cn0, ckb, cnk);
       }
+    }
+    if constexpr (kEarly) {
+      if (nxt) rd_first(na);
     }
   }
 }
@@ -512,5 +577,18 @@ const Entry kTable256x256ps[] = {
 };
 #undef PS
 const int kTable256x256psN = sizeof(kTable256x256ps) / sizeof(Entry);
+
+// 192 x 256 (K-contiguous A): the N = 768 ViT GEMMs (forward proj / fc2 with the fp32 residual,
+// their bf16x3 forms, and the input gradients to 768 on the transposed weights)
+#define PS192(A, B, E) {A, B, E, T192x256ps, &gemm_ps<A, B, E, 96>, PS_LDS, 512}
+const Entry kTable192x256ps[] = {
+    PS192(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
+    PS192(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_RESID),
+    PS192(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32),
+    PS192(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16),
+    PS192(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_ADD),
+};
+#undef PS192
+const int kTable192x256psN = sizeof(kTable192x256ps) / sizeof(Entry);
 
 }  // namespace dfu

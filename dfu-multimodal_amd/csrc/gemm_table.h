@@ -14,7 +14,8 @@ enum TileId {
   T128x128 = 0, T256x128 = 1, T128x256 = 2, T256x256 = 3, T128x128o2 = 4, T128x128w4 = 5,
   T256x256p8 = 6,  // phased 256x256 (gemm_p8.hip): K-contiguous A and B only
   T256x256ps = 7,  // persistent phased 256x256 (gemm_ps.hip)
-  NTILES = 8
+  T192x256ps = 8,  // persistent phased 192x256 (gemm_ps.hip): K-contiguous A
+  NTILES = 9
 };
 extern const Entry kTable128x128[];
 extern const int kTable128x128N;
@@ -32,6 +33,8 @@ extern const Entry kTable256x256p8[];
 extern const int kTable256x256p8N;
 extern const Entry kTable256x256ps[];
 extern const int kTable256x256psN;
+extern const Entry kTable192x256ps[];
+extern const int kTable192x256psN;
 }  // namespace dfu
 
 #define DFU_ENTRY(A, B, E, TMv, TNv, TID)                                             \

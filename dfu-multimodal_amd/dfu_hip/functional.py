@@ -1003,6 +1003,18 @@ def _linear_dgrad(rows, N, K, g, weight, w_rows, out, epilogue=L.EPI_BF16, **kw)
 # the fused fc1 + GELU triple epilogue, DFU_EPI_X3_GELU); DFU_X3_TILE=0: the cost model's pick
 # and a separate GELU split pass (A/B).
 _X3_TILE = int(os.environ.get("DFU_X3_TILE", "8"))
+# The GEMMs to D = 768 columns (proj and fc2 forward, the fc1 / proj / qkv input gradients) run
+# on the persistent 192 x 256 tile (tile 9: 198 tiles at M = 12608 instead of 150 of 256 rows
+# for 256 CUs; 8-16 % faster standalone, tools/gpu_tile192.sh) when the ViT runs alone.  Inside
+# the two-stream fusion step the 256-row tile's idle CUs run the ResNet's kernels: there tile 9
+# measured 19.11 vs 18.97 ms per step (same box, three rounds), so it keeps the 256-row plan.
+# DFU_GEMM_NO_T192=1: the 256-row plan everywhere (A/B).
+_NO_T192 = os.environ.get("DFU_GEMM_NO_T192", "0") != "0"
+
+
+def _t768():
+    """Tile hint for a ViT GEMM with N = 768 output columns (0: the tuned plan)."""
+    return 9 if _concurrent_encoders[0] == 0 and not _NO_T192 else 0
 
 # fc1.bias gradient from the dGELU epilogue's column sums (DFU_DGELU_COLSUM=0: a colsum pass)
 _DGELU_COLSUM = os.environ.get("DFU_DGELU_COLSUM", "1") != "0"
@@ -1039,8 +1051,9 @@ class ViTBlockFn(torch.autograd.Function):
                  bias=bias(attn.qkv))
         o, lse = ops.attention_fwd(qkv, B, T, H, dh, attn.scale)
         xm = _empty((rows, D), F32, dev)
+        t768 = _t768()
         ops.gemm(rows, D, D, o, D, wproj, D, xm, D, epilogue=L.EPI_F32_RESID, bias=bias(attn.proj),
-                 aux=x2, ldaux=D)
+                 aux=x2, ldaux=D, tile=t768)
         # MLP branch
         xn2 = _empty((rows, D), BF16, dev)
         m2, r2 = _ln_fwd(xm, blk.norm2, rows, D, xn2)
@@ -1050,7 +1063,8 @@ class ViTBlockFn(torch.autograd.Function):
                  aux_out=dgl, ldaux_out=Dh)
         xo = _empty((B, T, D), F32, dev)
         ops.gemm(rows, D, Dh, h, Dh, wfc2, Dh, xo.view(rows, D), D, epilogue=L.EPI_F32_RESID,
-                 bias=bias(mlp.fc2), aux=xm, ldaux=D)
+                 bias=bias(mlp.fc2), aux=xm, ldaux=D, tile=t768)
+        ctx.t768 = t768
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
@@ -1078,6 +1092,11 @@ class ViTBlockFn(torch.autograd.Function):
             return t3, tb, mean, rstd
 
         tl = _X3_TILE
+        # the two GEMMs to D = 768 columns (proj, fc2) on the 192 x 256 persistent tile when
+        # the ViT runs alone (_t768: projx3 61.6-62.6 vs 71.1-71.2 us, fc2x3 250.8-251.0 vs
+        # 270.9-271.9 us standalone; in the fusion step within noise of tile 8)
+        tl_d = (_t768() or tl) if tl == 8 else tl
+        ctx.t768 = _t768()
         xn1_3, xn1, m1, r1 = ln_x3(x2, blk.norm1)
         qkvf = _empty((rows, 3 * D), F32, dev)
         ops.gemm(rows, 3 * D, 3 * D, xn1_3, 3 * D, weight_x3_rows(attn.qkv.weight), 3 * D, qkvf,
@@ -1088,7 +1107,7 @@ class ViTBlockFn(torch.autograd.Function):
         del qkvf
         xm = _empty((rows, D), F32, dev)
         ops.gemm(rows, D, 3 * D, o3, 3 * D, weight_x3_rows(attn.proj.weight), 3 * D, xm, D,
-                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D, tile=tl)
+                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D, tile=tl_d)
         del o3
         xn2_3, xn2, m2, r2 = ln_x3(xm, blk.norm2)
         dgl = _empty((rows, Dh), BF16, dev)  # bf16 gelu'(pre): the DGELU factor
@@ -1110,7 +1129,7 @@ class ViTBlockFn(torch.autograd.Function):
         xo = _empty((B, T, D), F32, dev)
         ops.gemm(rows, D, 3 * Dh, h3, 3 * Dh, weight_x3_rows(mlp.fc2.weight), 3 * Dh,
                  xo.view(rows, D), D, epilogue=L.EPI_F32_RESID, bias=bias(mlp.fc2), aux=xm,
-                 ldaux=D, tile=tl)
+                 ldaux=D, tile=tl_d)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
@@ -1189,20 +1208,20 @@ class ViTBlockFn(torch.autograd.Function):
             _colsum_of_grad(gout if gout.dtype == F32 else g, grad_buffer(mlp.fc2.bias), red)
         wgrad(mlp.fc1, dh_pre, xn2, Dh, partial=cs1)
         dxn2 = _empty((rows, D), BF16, dev)
-        _linear_dgrad(rows, D, Dh, dh_pre, mlp.fc1.weight, wfc1, dxn2)
+        _linear_dgrad(rows, D, Dh, dh_pre, mlp.fc1.weight, wfc1, dxn2, tile=ctx.t768)
         gmb = _empty((rows, D), BF16, dev)
         gsp = _ln_bwd(dxn2, xm, m2, r2, blk.norm2, rows, D, g2, gmb,
                       gsum=_wants(attn.proj.bias), batch=red)  # g2 := g_mid (in place)
         # ---- attention branch: x_mid = x_in + proj(attn(norm1(x_in)))
         wgrad(attn.proj, gmb, o)
         do = _empty((rows, D), BF16, dev)
-        _linear_dgrad(rows, D, D, gmb, attn.proj.weight, wproj, do)
+        _linear_dgrad(rows, D, D, gmb, attn.proj.weight, wproj, do, tile=ctx.t768)
         if _wants(attn.proj.bias):
             red.add(gsp, grad_buffer(attn.proj.bias), D)
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, T, H, dh, attn.scale)
         wgrad(attn.qkv, dqkv, xn1, 3 * D)
         dxn1 = _empty((rows, D), BF16, dev)
-        _linear_dgrad(rows, D, 3 * D, dqkv, attn.qkv.weight, wqkv, dxn1)
+        _linear_dgrad(rows, D, 3 * D, dqkv, attn.qkv.weight, wqkv, dxn1, tile=ctx.t768)
         gib = _empty((B, T, D), BF16, dev)
         gsp = _ln_bwd(dxn1, x2, m1, r1, blk.norm1, rows, D, g2, gib.view(rows, D),
                       gsum=True, batch=red)  # g2 := g_in

@@ -9,7 +9,7 @@ cd "$(dirname "$0")/../dfu-multimodal_amd"
 make -j8 >/dev/null
 for m in "$@"; do
   SRC=gemm_ps
-  case $m in s*) DEF=-DDFU_PS_SCHED=${m#s} ;; *) DEF=-DDFU_PS_ABLATE=$m ;; esac
+  case $m in s*) DEF=-DDFU_PS_SCHED=${m#s} ;; a*) DEF=-DDFU_PS_STAUX=${m#a} ;; *) DEF=-DDFU_PS_ABLATE=$m ;; esac
   OBJS=$(ls build/*.o | grep -v $SRC.hip.o)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $DEF \
       -c csrc/$SRC.hip -o build/ablate_$m.o.tmp

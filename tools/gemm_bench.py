@@ -15,7 +15,7 @@ from dfu_hip import ops  # noqa: E402
 dev = "cuda"
 bf = torch.bfloat16
 TILE_NAMES = ["auto", "128x128", "256x128", "128x256", "256x256", "128x128o2", "128x128w4",
-              "256x256p8", "256x256ps"]
+              "256x256p8", "256x256ps", "192x256ps"]
 
 
 def T(*s, dtype=bf):

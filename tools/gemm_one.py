@@ -22,12 +22,16 @@ def T(*s, dtype=torch.bfloat16):
     return (torch.randn(*s, device="cuda") * 0.1).to(dtype)
 
 
+CHECK = []  # (HIP result, fp32 reference) thunks for --check
+
+
 def build(case, tile):
     if case in ("qkv_fwd", "proj_fwd", "fc2_fwd"):
         M, N, K = {"qkv_fwd": (12608, 2304, 768), "proj_fwd": (12608, 768, 768),
                    "fc2_fwd": (12608, 768, 3072)}[case]
         A, B, C = T(M, K), T(N, K), T(M, N)
         bias = T(N, dtype=torch.float32)
+        CHECK.append(lambda: (C.float(), A.float() @ B.float().t() + bias))
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16,
                                                bias=bias, tile=tile)
     if case in ("fc1_fwd", "fc1_gelu"):
@@ -44,6 +48,7 @@ def build(case, tile):
     if case in ("fc1_dgrad", "qkv_dgrad"):
         M, N, K = {"fc1_dgrad": (12608, 768, 3072), "qkv_dgrad": (12608, 768, 2304)}[case]
         A, B, C = T(M, K), T(K, N), T(M, N)
+        CHECK.append(lambda: (C.float(), A.float() @ B.float()))
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, N, C, N, b_mode=L.OPND_MNMAJOR,
                                                epilogue=L.EPI_BF16, tile=tile)
     if case in ("fc1_dgrad_t", "qkv_dgrad_t", "fc2_dgrad_t"):
@@ -55,13 +60,31 @@ def build(case, tile):
             return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N,
                                                    epilogue=L.EPI_BF16_DGELU, aux=h, ldaux=N,
                                                    tile=tile)
+        CHECK.append(lambda: (C.float(), A.float() @ B.float().t()))
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16,
                                                tile=tile)
+    if case == "proj_dgrad_t":
+        M, N, K = 12608, 768, 768
+        A, B, C = T(M, K), T(N, K), T(M, N)
+        CHECK.append(lambda: (C.float(), A.float() @ B.float().t()))
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_BF16,
+                                               tile=tile)
+    if case in ("proj_fwd_resid", "fc2x3_fwd_resid", "projx3_fwd_resid"):
+        M, N, K = {"proj_fwd_resid": (12608, 768, 768), "fc2x3_fwd_resid": (12608, 768, 9216),
+                   "projx3_fwd_resid": (12608, 768, 2304)}[case]
+        A, B = T(M, K), T(N, K)
+        C, X = T(M, N, dtype=torch.float32), T(M, N, dtype=torch.float32)
+        bias = T(N, dtype=torch.float32)
+        CHECK.append(lambda: (C - X, A.float() @ B.float().t() + bias))
+        return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N,
+                                               epilogue=L.EPI_F32_RESID, bias=bias, aux=X,
+                                               ldaux=N, tile=tile)
     if case == "fc2_fwd_resid":  # the step's fc2 forward: fp32 residual-stream epilogue
         M, N, K = 12608, 768, 3072
         A, B = T(M, K), T(N, K)
         C, X = T(M, N, dtype=torch.float32), T(M, N, dtype=torch.float32)
         bias = T(N, dtype=torch.float32)
+        CHECK.append(lambda: (C - X, A.float() @ B.float().t() + bias))
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, K, B, K, C, N,
                                                epilogue=L.EPI_F32_RESID, bias=bias, aux=X,
                                                ldaux=N, tile=tile)
@@ -70,6 +93,7 @@ def build(case, tile):
                    "proj_wgrad": (768, 768, 12608)}[case]
         A, B = T(K, M), T(K, N)
         C = torch.zeros(M, N, device="cuda")
+        CHECK.append(lambda: (C.clone(), A.float().t() @ B.float()))
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, M, B, N, C, N, a_mode=L.OPND_MNMAJOR,
                                                b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC,
                                                tile=tile)
@@ -94,10 +118,20 @@ def main():
     ap.add_argument("case")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--check", action="store_true", help="one launch checked against torch fp32")
     a = ap.parse_args()
     flops, fn = build(a.case, a.tile)
     fn()
     torch.cuda.synchronize()
+    if a.check:
+        if not CHECK:
+            raise SystemExit(f"--check: no reference for {a.case}")
+        got, ref = CHECK[0]()
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        print(f"{a.case} tile {a.tile}: max rel err {err:.2e}")
+        if not err < 1e-2:
+            raise SystemExit(f"{a.case}: CHECK FAILED")
+        return
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.iters):
