@@ -13,12 +13,13 @@ using namespace dfu;
 namespace {
 
 constexpr int kCUs = 256;
-constexpr int kTM[NTILES] = {128, 256, 128, 256, 128, 128, 256, 256, 192};
-constexpr int kTN[NTILES] = {128, 128, 256, 256, 128, 128, 256, 256, 256};
-constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 2, 1, 1, 1};  // workgroups per CU
+constexpr int kTM[NTILES] = {128, 256, 128, 256, 128, 128, 256, 256, 192, 256, 128};
+constexpr int kTN[NTILES] = {128, 128, 256, 256, 128, 128, 256, 256, 256, 64, 64};
+constexpr int kOcc[NTILES] = {1, 1, 1, 1, 2, 2, 1, 1, 1, 1, 2};  // workgroups per CU
 // the tile whose fitted step time a variant borrows (the persistent phased 256x256: the phased)
-constexpr int kBase[NTILES] = {0, 1, 2, 3, 4, 5, 6, 6, 6};
-constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false, false, false};
+constexpr int kBase[NTILES] = {0, 1, 2, 3, 4, 5, 6, 6, 6, 9, 10};
+constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false, false, false,
+                                  false, false};
 // Wave-quantisation cost model: a launch takes ceil(tiles * splits / 256) rounds (one 512-thread
 // workgroup per CU), each costing kRoundUs (prologue fill + epilogue) + k-steps * kStepUs.
 // Fitted on MI355X to tools/gemm_bench.py --sweep (ViT qkv K=768 vs fc2 K=3072 forward rows,
@@ -27,13 +28,14 @@ constexpr bool kTailOK[NTILES] = {true, false, false, false, true, false, false,
 // The 2-per-CU 128x128 variant: two co-resident workgroups share the MFMA pipe (step cost per
 // workgroup ~doubles) but hide each other's fill and epilogue.
 // (the phased 256x256 kernels are priced high: only the offline-tuned table selects them)
-constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70, 0.65, 3.0, 3.0, 3.0};
-constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1, 6.1, 20.0, 20.0, 20.0};
+// (the 64-column tiles are priced high too: only tuned plans select them)
+constexpr double kStepUs[NTILES] = {0.57, 0.89, 0.90, 1.41, 0.70, 0.65, 3.0, 3.0, 3.0, 3.0, 3.0};
+constexpr double kRoundUs[NTILES] = {4.8, 8.3, 7.4, 13.9, 6.1, 6.1, 20.0, 20.0, 20.0, 20.0, 20.0};
 constexpr double kSlabGBs = 5000.0;  // split-K: slab write + reduce (read slabs, RMW C)
 constexpr double kReduceLaunchUs = 2.0;
 // Persistent schedule (gemm_kernel.h): a workgroup owning several work units pays one
 // prologue fill for all of them plus, per unit, the epilogue time its MFMAs do not hide.
-constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0, 3.0, 3.0};
+constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0, 3.0, 3.0, 3.0, 3.0};
 int g_persistent = getenv("DFU_GEMM_PERSISTENT") ? atoi(getenv("DFU_GEMM_PERSISTENT")) : 1;  // dfu_gemm_set_persistent (env: A/B)
 int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
@@ -43,10 +45,12 @@ int g_tail_split = 1;       // dfu_gemm_set_tail_split
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
                                kTable128x128o2, kTable128x128w4, kTable256x256p8,
-                               kTable256x256ps, kTable192x256ps};
+                               kTable256x256ps, kTable192x256ps, kTable256x64,
+                               kTable128x64o2};
   const int ns[NTILES] = {kTable128x128N, kTable256x128N, kTable128x256N, kTable256x256N,
                           kTable128x128o2N, kTable128x128w4N, kTable256x256p8N,
-                          kTable256x256psN, kTable192x256psN};
+                          kTable256x256psN, kTable192x256psN, kTable256x64N,
+                          kTable128x64o2N};
   for (int i = 0; i < ns[tile]; ++i) {
     const Entry& en = tabs[tile][i];
     if (en.a == a && en.b == b && en.e == e) return &en;

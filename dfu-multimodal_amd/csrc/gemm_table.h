@@ -15,7 +15,9 @@ enum TileId {
   T256x256p8 = 6,  // phased 256x256 (gemm_p8.hip): K-contiguous A and B only
   T256x256ps = 7,  // persistent phased 256x256 (gemm_ps.hip)
   T192x256ps = 8,  // persistent phased 192x256 (gemm_ps.hip): K-contiguous A
-  NTILES = 9
+  T256x64 = 9,     // 4-wave 256x64 (64-channel convs; K-contiguous B)
+  T128x64o2 = 10,  // 4-wave 128x64 at 2 workgroups per CU
+  NTILES = 11
 };
 extern const Entry kTable128x128[];
 extern const int kTable128x128N;
@@ -35,6 +37,10 @@ extern const Entry kTable256x256ps[];
 extern const int kTable256x256psN;
 extern const Entry kTable192x256ps[];
 extern const int kTable192x256psN;
+extern const Entry kTable256x64[];
+extern const int kTable256x64N;
+extern const Entry kTable128x64o2[];
+extern const int kTable128x64o2N;
 }  // namespace dfu
 
 #define DFU_ENTRY(A, B, E, TMv, TNv, TID)                                             \

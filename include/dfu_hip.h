@@ -121,7 +121,9 @@ typedef struct dfu_gemm_desc {
                           128x128 at 2 workgroups/CU (8 waves, 4 waves), phased
                           256x256 (K-contiguous A and B only); 8 = persistent
                           phased 256x256 (K-contiguous or MN-major A and B);
-                          9 = persistent phased 192x256 (K-contiguous A)       */
+                          9 = persistent phased 192x256 (K-contiguous A);
+                          10, 11 = 4-wave 256x64, 128x64 at 2/CU (K-contiguous
+                          or implicit-conv A, K-contiguous B)                  */
   void* workspace;     /* split-K fp32 slabs (dfu_gemm_workspace_bytes); NULL =  */
   int64_t workspace_bytes; /*   split-K partials accumulate with fp32 atomics     */
   /* Split-K with slabs: NULL = a second kernel adds the slabs into C.  Otherwise a zeroed
@@ -139,7 +141,7 @@ int dfu_gemm_stats_tiles(int32_t M);
 /* Workspace bytes for this descriptor: deterministic split-K slabs (F32_ACC) or tail-split
  * slabs (other epilogues); 0 if the launch needs none. */
 int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* desc);
-/* The tile (1..9, as dfu_gemm_desc.tile) and split-K the cost model picks for this descriptor. */
+/* The tile (1..11, as dfu_gemm_desc.tile) and split-K the cost model picks for this descriptor. */
 int dfu_gemm_plan(const dfu_gemm_desc* desc, int32_t* tile, int32_t* split_k);
 /* GEMM schedule switch (tests, A/B timing): 1 (default) = persistent workgroups, each walking
  * several work units as one continuous K-step stream; 0 = one workgroup per work unit.  The

@@ -56,7 +56,7 @@ static void check_plan(const dfu_gemm_desc& d, const char* what) {
   const int rc = dfu_gemm_plan(&d, &tile, &split);
   EXPECT(rc == DFU_OK, "%s: plan rc %d (%s)", what, rc, dfu_last_error_string());
   if (rc != DFU_OK) return;
-  EXPECT(tile >= 1 && tile <= 9, "%s: tile %d", what, tile);
+  EXPECT(tile >= 1 && tile <= 11, "%s: tile %d", what, tile);
   EXPECT(split >= 1 && split <= 256, "%s: split %d", what, split);
   EXPECT(split == 1 || d.epilogue == DFU_EPI_F32_ACC, "%s: split %d on a non-ACC epilogue", what,
          split);
@@ -145,7 +145,7 @@ static void random_sweep() {
     EXPECT(rc == DFU_OK || rc == DFU_E_UNSUPPORTED, "sweep: rc %d", rc);
     if (rc == DFU_OK) {
       ++planned;
-      EXPECT(tile >= 1 && tile <= 9 && split >= 1, "sweep: tile %d split %d", tile, split);
+      EXPECT(tile >= 1 && tile <= 11 && split >= 1, "sweep: tile %d split %d", tile, split);
       EXPECT(dfu_gemm_workspace_bytes(&d) >= 0, "sweep: workspace");
     } else {
       EXPECT(strlen(dfu_last_error_string()) > 0, "sweep: empty error");

@@ -17,7 +17,7 @@ from dfu_hip import ops
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TILES = [1, 2, 3, 4, 5, 6, 7, 8, 9]
+TILES = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]
 
 
 def drnd(*shape, scale=1.0, dtype=torch.bfloat16, seed=0):

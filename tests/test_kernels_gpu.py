@@ -28,8 +28,9 @@ def close(a, b, atol, rtol=0.0, what=""):
 
 
 # ------------------------------------------------------------------------------ GEMM
-TILES = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9]  # auto, 128x128, 256x128, 128x256, 256x256,
-# 128x128 @2/CU (8, 4 waves), phased 256x256, persistent phased 256x256 and 192x256
+TILES = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]  # auto, 128x128, 256x128, 128x256, 256x256,
+# 128x128 @2/CU (8, 4 waves), phased 256x256, persistent phased 256x256 and 192x256, 4-wave
+# 256x64 and 128x64 @2/CU
 
 
 def gemm_t(*args, tile=0, **kw):

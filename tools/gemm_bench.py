@@ -15,7 +15,7 @@ from dfu_hip import ops  # noqa: E402
 dev = "cuda"
 bf = torch.bfloat16
 TILE_NAMES = ["auto", "128x128", "256x128", "128x256", "256x256", "128x128o2", "128x128w4",
-              "256x256p8", "256x256ps", "192x256ps"]
+              "256x256p8", "256x256ps", "192x256ps", "256x64", "128x64o2"]
 
 
 def T(*s, dtype=bf):
@@ -91,11 +91,21 @@ def conv(name, B, H, C, K, R, stride):
              b_mode=L.OPND_CONV_WGRAD_X, epilogue=L.EPI_F32_ACC, conv=g)
 
 
+def stem(name, M, N, K, epi=L.EPI_BF16_STATS):
+    A, W = T(M, K), T(N, K)
+    y = torch.empty(M, N, dtype=bf if epi == L.EPI_BF16_STATS else torch.float32, device=dev)
+    st = torch.empty(ops.stats_tiles(M), 2, N, device=dev)
+    case(f"cfwd {name} {M}x{N}x{K}", 2 * M * N * K, (M, N, K, A, K, W, K, y, N), epilogue=epi,
+         stats=st)
+
+
 TOK = 64 * 197
 lin("qkv", TOK, 2304, 768)
 lin("proj", TOK, 768, 768)
 lin("fc1", TOK, 3072, 768)
 lin("fc2", TOK, 768, 3072)
+stem("stem im2col", 802816, 64, 160)
+stem("x3 l1c1 1x1 256->64 56", 200704, 64, 768, L.EPI_F32_STATS)
 conv("l1c1 1x1 256->64 56", 64, 56, 256, 64, 1, 1)
 conv("l1c2 3x3 64 56", 64, 56, 64, 64, 3, 1)
 conv("l1c3 1x1 64->256 56", 64, 56, 64, 256, 1, 1)
@@ -110,6 +120,9 @@ flt = args[0] if args else ""
 sweep = "--sweep" in sys.argv
 ab = "--ab" in sys.argv  # persistent vs one-workgroup-per-unit schedule, auto plan
 tiles = range(len(TILE_NAMES)) if sweep else [0]
+for a in sys.argv[1:]:
+    if a.startswith("--tiles="):  # e.g. --tiles=0,6,10,11
+        tiles = [int(t) for t in a.split("=", 1)[1].split(",")]
 print(f"{'case':42s} " + " ".join(f"{TILE_NAMES[t]:>16s}" for t in tiles) +
       (f" {'one-shot':>16s}" for _ in [0]).__next__() * ab)
 tot_us = 0.0

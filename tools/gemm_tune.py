@@ -24,7 +24,7 @@ from dfu_hip import ops  # noqa: E402
 SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256]
 OPND = ["KM", "MN", "CONV_FWD", "CONV_DGRAD", "CONV_DGRAD_W", "CONV_WGRAD_X"]
 EPI = ["BF16", "BF16_RELU", "BF16_GELU", "F32", "F32_RESID", "BF16_DGELU", "BF16_ADD", "F32_ACC",
-       "F32_ACC_CONVW", "BF16_STATS", "PATCH"]
+       "F32_ACC_CONVW", "BF16_STATS", "PATCH", "F32_STATS", "BF16_DSTATS", "X3_GELU"]
 CONV_FIELDS = ("conv_n", "conv_h", "conv_w", "conv_c", "conv_k", "conv_r", "conv_s",
                "conv_stride", "conv_pad")
 
@@ -70,7 +70,9 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "dfu-multimodal_amd", "csrc",
                                                   "gemm_tuned.inc"))
     ap.add_argument("--append", action="store_true", help="keep entries already in --out")
-    ap.add_argument("--tiles", default="1-8", help="tile ids to try, e.g. 1-8 or 6,8")
+    ap.add_argument("--tiles", default="1-11", help="tile ids to try, e.g. 1-11 or 6,8")
+    ap.add_argument("--precision", default="bf16", help="record the step in this mode (bf16x3: "
+                    "its forward GEMMs with tripled K)")
     ap.add_argument("--dump", default=None,
                     help="also write every timing (shape -> {tile/split: us}) to this JSON")
     a = ap.parse_args()
@@ -86,9 +88,11 @@ def main():
     opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
     crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
     rgb, th, y = bench.synthetic(a.batch, dev, 42)
+    from dfu_hip import functional as Fn
     ops.gemm_record = []
     opt.zero_grad()
-    crit(fwd(model, rgb, th), y).backward()
+    with Fn.precision(a.precision):
+        crit(fwd(model, rgb, th), y).backward()
     opt.step()
     rec, ops.gemm_record = ops.gemm_record, None
     torch.cuda.synchronize()
@@ -145,7 +149,7 @@ def main():
     with open(a.out, "w") as f:
         f.write("// Generated by tools/gemm_tune.py on MI355X (gfx950): fastest tile/split-K per GEMM of\n"
                 "// the DFU training step. Fields: a_mode, b_mode, epilogue, M, N, K, conv n,h,w,c,k,r,s,"
-                "stride,pad,\n// tile (1..12), split.\n")
+                "stride,pad,\n// tile (1..11), split.\n")
         for ln in keep + lines:
             f.write(ln + "\n")
     print(f"wrote {len(keep) + len(lines)} entries to {a.out}")
