@@ -456,6 +456,10 @@ DFU_DEV void load_bias(const float* bias, int n0w, int N, int lane, float (&b)[F
   typedef const __attribute__((address_space(4))) float cfloat;
   const cfloat* bp = (const cfloat*)bias;
   const int g = lane >> 4;
+  // n0w is wave-uniform (the wave's column base) but derived from threadIdx.x: without the
+  // readfirstlane hipcc cannot prove it and emits VECTOR loads plus s_waitcnt vmcnt(0), which
+  // drains the next tile's in-flight DMA (and the previous epilogue's stores) at every epilogue
+  n0w = __builtin_amdgcn_readfirstlane(n0w);
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int nb = n0w + 16 * j;

@@ -111,6 +111,27 @@ DFU_DEV void ps_issue(const PsSrc<KC>& s, rsrc_t r, int64_t ld, int k0, int K, i
   }
 }
 
+// Raw epilogue loads (unpacked where used, so the load can be issued steps ahead): four fp32 /
+// bf16 columns n..n+3 at element e; out-of-range lanes read zeros (kOOB offset).
+template <bool N4>
+DFU_DEV u32x4 ldraw_f32(rsrc_t r, int64_t e, bool okr, int n, int N) {
+  if constexpr (N4) return __builtin_amdgcn_raw_buffer_load_b128(r, boff(okr && n < N, e * 4), 0, 0);
+  u32x4 x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    x[q] = __builtin_amdgcn_raw_buffer_load_b32(r, boff(okr && n + q < N, (e + q) * 4), 0, 0);
+  return x;
+}
+template <bool N4>
+DFU_DEV u32x2 ldraw_bf16(rsrc_t r, int64_t e, bool okr, int n, int N) {
+  if constexpr (N4) return __builtin_amdgcn_raw_buffer_load_b64(r, boff(okr && n < N, e * 2), 0, 0);
+  uint32_t h[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    h[q] = __builtin_amdgcn_raw_buffer_load_b16(r, boff(okr && n + q < N, (e + q) * 2), 0, 0);
+  return (u32x2){h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+}
+
 // Vector-memory instructions a wave issues in one epilogue after its last waited load
 // (FMH: 16-row fragments per wave per tile half; 2 FMH fragment rows per wave).
 template <int EPI, int FMH = 4>
@@ -128,10 +149,12 @@ DFU_DEV int ps_epi_stores(const GemmArgs& p) {
 // lane holds C[m0 + (i / FMH) * 32 FMH + wr * 16 FMH + (i % FMH) * 16 + (lane&15)]
 //              [n0 + (j>>1)*128 + wc*32 + (j&1)*16 + 4*(lane>>4) + r]
 // (FMH = 4: the 256-row tile, m0 + (i>>2)*128 + wr*64 + (i&3)*16; FMH = 3: the 192-row tile)
-template <int EPI, int FMH = 4>
-DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, int n0, int wr,
-                         int wc, int lane, int sidx) {
-  const bool n4 = p.n4 != 0;
+// N4 (p.n4 at compile time): no control flow around the epilogue's loads, so hipcc's wait
+// counts stay exact instead of falling back to vmcnt(0) where branches join.
+template <int EPI, int FMH, bool N4>
+DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, int n0, int wr,
+                           int wc, int lane, int sidx) {
+  constexpr bool n4 = N4;
   const int M = p.M, N = p.N;
   const rsrc_t rc = make_rsrc(p.C);
   const rsrc_t ra = make_rsrc(p.aux);
@@ -165,13 +188,50 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, in
       }
     }
   }
+  // The epilogue walks its 4 FMH steps (fragment row i, column half hb).  Epilogues that read
+  // (the residual / C for RESID and unsplit ACC, gelu' or the addend for DGELU / ADD) issue a
+  // step's loads PD steps ahead, in front of the stores of the steps between: vmcnt retires in
+  // issue order, so a load issued after a store would wait for that store too, and the loads of
+  // one step after the previous step's stores serialised the epilogue on memory latency (one
+  // round trip per step: 19 us of the 89 us fc2 forward, standalone).
+  constexpr bool kLdF = EPI == DFU_EPI_F32_RESID || EPI == DFU_EPI_F32_ACC;
+  constexpr bool kLdH = EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD;
+  constexpr int NS = 4 * FMH, PD = 2;
+  const bool ld_c = EPI == DFU_EPI_F32_RESID || p.slab == nullptr;  // ACC: C += acc unsplit
+  u32x4 af[NS][2];
+  u32x2 ah[NS][2];
+  auto row_of = [&](int i) {
+    return m0 + (i / FMH) * 32 * FMH + wr * 16 * FMH + (i % FMH) * 16 + (lane & 15);
+  };
+  auto load_step = [&](int st) {
+    if constexpr (kLdF || kLdH) {
+      const int i = st >> 1, hb = st & 1;
+      const int m = row_of(i);
+      const bool okm = (kAbl & 32) ? (m < 0) : (m < M);
+      const int64_t mc = okm ? m : 0;
 #pragma unroll
-  for (int i = 0; i < 2 * FMH; ++i) {
-    const int m = m0 + (i / FMH) * 32 * FMH + wr * 16 * FMH + (i % FMH) * 16 + (lane & 15);
+      for (int jj = 0; jj < 2; ++jj) {
+        const int n = n0 + hb * 128 + wc * 32 + jj * 16 + 4 * (lane >> 4);
+        if constexpr (EPI == DFU_EPI_F32_RESID)
+          af[st][jj] = ldraw_f32<N4>(ra, mc * p.ldaux + n, okm, n, N);
+        else if constexpr (EPI == DFU_EPI_F32_ACC) {
+          if (ld_c) af[st][jj] = ldraw_f32<N4>(rc, mc * p.ldc + n, okm, n, N);
+        } else
+          ah[st][jj] = ldraw_bf16<N4>(ra, mc * p.ldaux + n, okm, n, N);
+      }
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < PD; ++st) load_step(st);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    if (st + PD < NS) load_step(st + PD);
+    if constexpr (kLdF || kLdH) __builtin_amdgcn_sched_barrier(0);
+    const int i = st >> 1, hb = st & 1;
+    const int m = row_of(i);
     const bool okm = (kAbl & 32) ? (m < 0) : (m < M);  // ablation 32: every access out of range
     const int64_t mc = okm ? m : 0;
-#pragma unroll
-    for (int hb = 0; hb < 2; ++hb) {
+    {
       const int n0w = n0 + hb * 128 + wc * 32;
       float v[2][4];
 #pragma unroll
@@ -213,7 +273,7 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, in
         for (int jj = 0; jj < 2; ++jj) {
           const int n = n0w + jj * 16 + 4 * (lane >> 4);
           float x[4];
-          ld4_bf16(ra, mc * p.ldaux + n, okm, n, N, n4, x);
+          unpack4(ah[st][jj], x);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             v[jj][r] = EPI == DFU_EPI_BF16_DGELU ? v[jj][r] * x[r] : v[jj][r] + x[r];
@@ -232,10 +292,8 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, in
           if (p.slab != nullptr) {
             st4_f32(make_rsrc(p.slab), ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v[jj]);
           } else {
-            float c[4];
-            ld4_f32(rc, mc * p.ldc + n, okm, n, N, n4, c);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[jj][r] += c[r];
+            for (int r = 0; r < 4; ++r) v[jj][r] += __uint_as_float(af[st][jj][r]);
             st4_f32<kStAux>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
           }
         }
@@ -243,10 +301,8 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, in
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int n = n0w + jj * 16 + 4 * (lane >> 4);
-          float x[4];
-          ld4_f32(ra, mc * p.ldaux + n, okm, n, N, n4, x);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[jj][r] += x[r];
+          for (int r = 0; r < 4; ++r) v[jj][r] += __uint_as_float(af[st][jj][r]);
           st4_f32<kStAux>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
         }
       }
@@ -269,6 +325,15 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, in
         }
     }
   }
+}
+
+template <int EPI, int FMH>
+DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, int n0, int wr,
+                         int wc, int lane, int sidx) {
+  if (p.n4)
+    ps_epilogue_n<EPI, FMH, true>(p, acc, m0, n0, wr, wc, lane, sidx);
+  else
+    ps_epilogue_n<EPI, FMH, false>(p, acc, m0, n0, wr, wc, lane, sidx);
 }
 
 // TMH: rows per tile half (128: the 256 x 256 tile; 96: 192 x 256, K-contiguous A only -- for
