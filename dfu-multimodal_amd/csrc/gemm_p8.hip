@@ -66,63 +66,107 @@ DFU_DEV void p8_issue_half_mn(const bf16_t* base, int64_t ld, int col0, int col_
   }
 }
 
-template <int EPI>
-DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc,
-                         int lane, int sidx) {
-  const bool n4 = p.n4 != 0;
+// Epilogue, compiled per n4 (N4) so that no control flow surrounds its loads and hipcc's wait
+// counts stay exact.  Bias by scalar loads (load_bias: the wave's column base is uniform); the
+// reading epilogues (residual, gelu', addend, C) issue each step's load PD steps ahead of the
+// stores between (vmcnt retires in issue order: a load issued behind a store waits for it).
+template <int EPI, bool N4>
+DFU_DEV void p8_epilogue_n(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc,
+                           int lane, int sidx) {
+  constexpr bool n4 = N4;
   const int M = p.M, N = p.N;
   const rsrc_t rc = make_rsrc(p.C);
   const rsrc_t ra = make_rsrc(p.aux);
   const rsrc_t ro = make_rsrc(p.aux_out);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + 4 * (lane >> 4);
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bias[r] = n + r < N ? p.bias[n + r] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + (i >> 2) * 128 + wr * 64 + (i & 3) * 16 + (lane & 15);
+  constexpr bool kLdF = EPI == DFU_EPI_F32_RESID || EPI == DFU_EPI_F32_ACC;
+  constexpr bool kLdH = EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD;
+  constexpr int NS = 32, PD = 4;  // steps (j, i): fragment column j outer, row i inner
+  const bool ld_c = EPI == DFU_EPI_F32_RESID || p.slab == nullptr;
+  u32x4 af[NS];
+  u32x2 ah[NS];
+  auto col_of = [&](int j) { return n0 + (j >> 1) * 128 + wc * 32 + (j & 1) * 16 + 4 * (lane >> 4); };
+  auto row_of = [&](int i) { return m0 + (i >> 2) * 128 + wr * 64 + (i & 3) * 16 + (lane & 15); };
+  auto load_step = [&](int st) {
+    if constexpr (kLdF || kLdH) {
+      const int n = col_of(st >> 3), m = row_of(st & 7);
       const bool okm = m < M;
       const int64_t mc = okm ? m : 0;
-      float v[4];
+      if constexpr (EPI == DFU_EPI_F32_RESID)
+        af[st] = ldraw_f32<N4>(ra, mc * p.ldaux + n, okm, n, N);
+      else if constexpr (EPI == DFU_EPI_F32_ACC) {
+        if (ld_c) af[st] = ldraw_f32<N4>(rc, mc * p.ldc + n, okm, n, N);
+      } else
+        ah[st] = ldraw_bf16<N4>(ra, mc * p.ldaux + n, okm, n, N);
+    }
+  };
+  float bias[4][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha + bias[r];
-      if constexpr (EPI == DFU_EPI_BF16) {
-        st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
-      } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
-        float g[4], d[4];
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) gelu_and_grad(v[r], g[r], d[r]);
-        st4_bf16(ro, mc * p.ldaux_out + n, okm, n, N, n4, d);
-        st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, g);
-      } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
-        float x[4];
-        ld4_bf16(ra, mc * p.ldaux + n, okm, n, N, n4, x);
+    for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
+  if (p.bias) {  // (before the loads: no control flow between a load and its use)
+    float b2[2][4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          v[r] = EPI == DFU_EPI_BF16_DGELU ? v[r] * x[r] : v[r] + x[r];
-        st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
-      } else if constexpr (EPI == DFU_EPI_F32_ACC) {  // split-K slab, or C += acc unsplit
-        if (p.slab != nullptr) {
-          st4_f32(make_rsrc(p.slab), ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v);
-        } else {
-          float c[4];
-          ld4_f32(rc, mc * p.ldc + n, okm, n, N, n4, c);
+    for (int hb = 0; hb < 2; ++hb) {
+      load_bias<2>(p.bias, n0 + hb * 128 + wc * 32, N, lane, b2);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += c[r];
-          st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v);
-        }
-      } else {  // DFU_EPI_F32_RESID
-        float x[4];
-        ld4_f32(ra, mc * p.ldaux + n, okm, n, N, n4, x);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += x[r];
-        st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v);
+      for (int r = 0; r < 4; ++r) {
+        bias[2 * hb][r] = b2[0][r];
+        bias[2 * hb + 1][r] = b2[1][r];
       }
     }
   }
+#pragma unroll
+  for (int st = 0; st < PD; ++st) load_step(st);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    if (st + PD < NS) load_step(st + PD);
+    if constexpr (kLdF || kLdH) __builtin_amdgcn_sched_barrier(0);
+    const int j = st >> 3, i = st & 7;
+    const int n = col_of(j);
+    const int m = row_of(i);
+    const bool okm = m < M;
+    const int64_t mc = okm ? m : 0;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha + bias[j][r];
+    if constexpr (EPI == DFU_EPI_BF16) {
+      st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
+    } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
+      float g[4], d[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gelu_and_grad(v[r], g[r], d[r]);
+      st4_bf16(ro, mc * p.ldaux_out + n, okm, n, N, n4, d);
+      st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, g);
+    } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
+      float x[4];
+      unpack4(ah[st], x);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        v[r] = EPI == DFU_EPI_BF16_DGELU ? v[r] * x[r] : v[r] + x[r];
+      st4_bf16(rc, mc * p.ldc + n, okm, n, N, n4, v);
+    } else if constexpr (EPI == DFU_EPI_F32_ACC) {  // split-K slab, or C += acc unsplit
+      if (p.slab != nullptr) {
+        st4_f32(make_rsrc(p.slab), ((int64_t)sidx * M + mc) * N + n, okm, n, N, n4, v);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += __uint_as_float(af[st][r]);
+        st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v);
+      }
+    } else {  // DFU_EPI_F32_RESID
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += __uint_as_float(af[st][r]);
+      st4_f32(rc, mc * p.ldc + n, okm, n, N, n4, v);
+    }
+  }
+}
+template <int EPI>
+DFU_DEV void p8_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc,
+                         int lane, int sidx) {
+  if (p.n4)
+    p8_epilogue_n<EPI, true>(p, acc, m0, n0, wr, wc, lane, sidx);
+  else
+    p8_epilogue_n<EPI, false>(p, acc, m0, n0, wr, wc, lane, sidx);
 }
 
 template <int AMODE, int BMODE, int EPI>

@@ -111,27 +111,6 @@ DFU_DEV void ps_issue(const PsSrc<KC>& s, rsrc_t r, int64_t ld, int k0, int K, i
   }
 }
 
-// Raw epilogue loads (unpacked where used, so the load can be issued steps ahead): four fp32 /
-// bf16 columns n..n+3 at element e; out-of-range lanes read zeros (kOOB offset).
-template <bool N4>
-DFU_DEV u32x4 ldraw_f32(rsrc_t r, int64_t e, bool okr, int n, int N) {
-  if constexpr (N4) return __builtin_amdgcn_raw_buffer_load_b128(r, boff(okr && n < N, e * 4), 0, 0);
-  u32x4 x;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    x[q] = __builtin_amdgcn_raw_buffer_load_b32(r, boff(okr && n + q < N, (e + q) * 4), 0, 0);
-  return x;
-}
-template <bool N4>
-DFU_DEV u32x2 ldraw_bf16(rsrc_t r, int64_t e, bool okr, int n, int N) {
-  if constexpr (N4) return __builtin_amdgcn_raw_buffer_load_b64(r, boff(okr && n < N, e * 2), 0, 0);
-  uint32_t h[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    h[q] = __builtin_amdgcn_raw_buffer_load_b16(r, boff(okr && n + q < N, (e + q) * 2), 0, 0);
-  return (u32x2){h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
-}
-
 // Vector-memory instructions a wave issues in one epilogue after its last waited load
 // (FMH: 16-row fragments per wave per tile half; 2 FMH fragment rows per wave).
 template <int EPI, int FMH = 4>

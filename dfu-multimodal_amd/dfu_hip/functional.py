@@ -1016,8 +1016,9 @@ def _t768():
     """Tile hint for a ViT GEMM with N = 768 output columns (0: the tuned plan)."""
     return 9 if _concurrent_encoders[0] == 0 and not _NO_T192 else 0
 
-# fc1.bias gradient from the dGELU epilogue's column sums (DFU_DGELU_COLSUM=0: a colsum pass)
-_DGELU_COLSUM = os.environ.get("DFU_DGELU_COLSUM", "1") != "0"
+# fc1.bias gradient from the dGELU epilogue's column sums when the ViT runs alone
+# (DFU_DGELU_COLSUM=0: a colsum pass everywhere; 2: the epilogue's sums in the fusion step too)
+_DGELU_COLSUM = int(os.environ.get("DFU_DGELU_COLSUM", "1"))
 
 
 class ViTBlockFn(torch.autograd.Function):
@@ -1192,7 +1193,8 @@ class ViTBlockFn(torch.autograd.Function):
         # the ViT's critical stream measured 0.07 ms slower per step than the separate pass,
         # thermal-only 0.13 ms faster)
         cs1 = None
-        if _DGELU_COLSUM and ctx.beside and _wants(mlp.fc1.bias) and g.is_cuda:
+        if (_DGELU_COLSUM == 2 or (_DGELU_COLSUM and ctx.beside)) and _wants(mlp.fc1.bias) and \
+                g.is_cuda:
             cs1 = _empty((2 * ((rows + 255) // 256), Dh), F32, dev)
             try:
                 _linear_dgrad(rows, Dh, D, gb, mlp.fc2.weight, wfc2, dh_pre,

@@ -19,7 +19,8 @@ from dfu_hip import _lib as L  # noqa: E402
 from dfu_hip import ops  # noqa: E402
 
 OPND = ["KM", "MN", "CFWD", "CDGD", "CDGW", "CWGX"]
-EPI = ["BF16", "RELU", "GELU", "F32", "RESID", "DGELU", "ADD", "ACC", "ACCW", "STATS", "PATCH"]
+EPI = ["BF16", "RELU", "GELU", "F32", "RESID", "DGELU", "ADD", "ACC", "ACCW", "STATS", "PATCH", "F32STATS",
+       "DSTATS", "X3GELU"]
 TILE = ["auto", "128x128", "256x128", "128x256", "256x256", "128x128o2", "128x128w4", "256x256p8",
         "256x256ps", "192x256ps", "256x64", "128x64o2"]
 
