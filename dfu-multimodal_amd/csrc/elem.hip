@@ -193,20 +193,21 @@ __global__ __launch_bounds__(256) void k_im2col_lds(
   }
 }
 
-template <bool X3 = false>
+// VEC: unit-stride rows with 16-byte aligned 8-float runs (two float4 loads per thread; the
+// host checks); the vector count fits 32 bits (host-checked), so the index math is 32-bit.
+template <bool X3 = false, bool VEC = false>
 __global__ void k_patchify_f32(const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh,
                                int64_t sw, int B, int C, int H, int W, int ps,
                                bf16_t* __restrict__ out) {
   const int gh = H / ps, gw = W / ps;
   const int K = C * ps * ps;
   const int vec_per_row = K / 8;
-  const int64_t n = (int64_t)B * gh * gw * vec_per_row;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / vec_per_row;
-    const int kv = (int)(i - m * vec_per_row);
-    const int b = (int)(m / (gh * gw));
-    const int pidx = (int)(m - (int64_t)b * gh * gw);
+  const int n = B * gh * gw * vec_per_row;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int m = i / vec_per_row;
+    const int kv = i - m * vec_per_row;
+    const int b = m / (gh * gw);
+    const int pidx = m - b * gh * gw;
     const int py = pidx / gw, px = pidx - (pidx / gw) * gw;
     const int k0 = kv * 8;
     const int c = k0 / (ps * ps);
@@ -214,8 +215,17 @@ __global__ void k_patchify_f32(const float* __restrict__ x, int64_t sn, int64_t 
     const int kh = rem / ps, kw0 = rem - (rem / ps) * ps;  // ps % 8 == 0: 8 consecutive kw
     const float* src = x + b * sn + c * sc + (py * ps + kh) * sh + (px * ps + kw0) * sw;
     float f[8];
+    if constexpr (VEC) {
+      const f32x4 a = *(const f32x4*)src, a2 = *(const f32x4*)(src + 4);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = src[e * sw];
+      for (int e = 0; e < 4; ++e) {
+        f[e] = a[e];
+        f[4 + e] = a2[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = src[e * sw];
+    }
     if constexpr (X3) {
       store_triple8(out + m * 3 * K, K, k0, f);
     } else {
@@ -585,10 +595,20 @@ __global__ void k_vit_embed_bwd(const float* __restrict__ gx, int B, int T, int 
     const int t = (int)(i / D);
     const int d = (int)(i - (int64_t)t * D);
     float s = 0.f;
-    for (int b = 0; b < B; ++b) {
-      const float v = gx[((int64_t)b * T + t) * D + d];
-      s += v;
-      if (t > 0) gpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = f2bf(v);
+    // eight images' loads in flight before their stores (a load issued behind a store would
+    // wait for it: vmcnt retires in issue order); the sum keeps the image order
+    constexpr int U = 8;
+    for (int b0 = 0; b0 < B; b0 += U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u] = b0 + u < B ? gx[((int64_t)(b0 + u) * T + t) * D + d] : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (b0 + u >= B) break;
+        s += v[u];
+        if (t > 0) gpatch[((int64_t)(b0 + u) * (T - 1) + t - 1) * D + d] = f2bf(v[u]);
+      }
     }
     if (dpos) dpos[i] += s;
     if (t == 0) {
@@ -599,12 +619,26 @@ __global__ void k_vit_embed_bwd(const float* __restrict__ gx, int B, int T, int 
     }
   }
 }
-__global__ void k_sum_rows_add(const float* __restrict__ partial, int T, int D,
-                               float* __restrict__ out) {
-  for (int d = blockIdx.x * blockDim.x + threadIdx.x; d < D; d += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int t = 0; t < T; ++t) s += partial[(int64_t)t * D + d];
-    out[d] += s;
+// out[d] += sum_t partial[t][d]: 16 columns x 16 row lanes per block (lane r sums rows r, r + 16,
+// ..., then the 16 lane sums are added in r order), D / 16 blocks.
+constexpr int SRA_C = 16, SRA_R = 16;
+__global__ __launch_bounds__(SRA_C * SRA_R) void k_sum_rows_add(const float* __restrict__ partial,
+                                                                int T, int D,
+                                                                float* __restrict__ out) {
+  __shared__ float red[SRA_R][SRA_C];
+  const int c = threadIdx.x % SRA_C, r = threadIdx.x / SRA_C;
+  const int d = blockIdx.x * SRA_C + c;
+  float s = 0.f;
+  if (d < D) {
+#pragma unroll 4
+    for (int t = r; t < T; t += SRA_R) s += partial[(int64_t)t * D + d];
+  }
+  red[r][c] = s;
+  __syncthreads();
+  if (r == 0 && d < D) {
+    float a = 0.f;
+    for (int k = 0; k < SRA_R; ++k) a += red[k][c];
+    out[d] += a;
   }
 }
 
@@ -705,6 +739,11 @@ __global__ void k_reduce_partials_batch(const ReduceBatch b) {
 }
 
 }  // namespace
+
+// k_patchify_f32's vector form: unit-stride rows, 16-byte aligned 8-float runs
+inline bool patchify_vec(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw) {
+  return sw == 1 && ((uintptr_t)x & 15) == 0 && sn % 4 == 0 && sc % 4 == 0 && sh % 4 == 0;
+}
 
 #define LAUNCH(kern, n, stream, ...)                                                     \
   do {                                                                                   \
@@ -838,7 +877,11 @@ extern "C" int dfu_patchify_f32(const float* x, int64_t sn, int64_t sc, int64_t 
   DFU_CHECK_ARG(x && out && ps % 8 == 0 && H % ps == 0 && W % ps == 0,
                 "dfu_patchify_f32: bad patch size %d for %dx%d", ps, H, W);
   const int64_t n = (int64_t)B * (H / ps) * (W / ps) * (C * ps * ps / 8);
-  LAUNCH(k_patchify_f32<false>, n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
+  DFU_CHECK_ARG(n < (1ll << 31), "dfu_patchify_f32: too many vectors");
+  if (patchify_vec(x, sn, sc, sh, sw))
+    LAUNCH((k_patchify_f32<false, true>), n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
+  else
+    LAUNCH((k_patchify_f32<false, false>), n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
   return DFU_OK;
 }
 
@@ -870,7 +913,11 @@ extern "C" int dfu_patchify_f32_x3(const float* x, int64_t sn, int64_t sc, int64
   DFU_CHECK_ARG(x && out && ps % 8 == 0 && H % ps == 0 && W % ps == 0,
                 "dfu_patchify_f32_x3: bad patch size %d for %dx%d", ps, H, W);
   const int64_t n = (int64_t)B * (H / ps) * (W / ps) * (C * ps * ps / 8);
-  LAUNCH(k_patchify_f32<true>, n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
+  DFU_CHECK_ARG(n < (1ll << 31), "dfu_patchify_f32_x3: too many vectors");
+  if (patchify_vec(x, sn, sc, sh, sw))
+    LAUNCH((k_patchify_f32<true, true>), n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
+  else
+    LAUNCH((k_patchify_f32<true, false>), n, stream, x, sn, sc, sh, sw, B, C, H, W, ps, (bf16_t*)out);
   return DFU_OK;
 }
 
@@ -1029,7 +1076,11 @@ extern "C" int dfu_vit_embed_bwd(const float* gx, int32_t B, int32_t T, int32_t 
                                  void* stream) {
   DFU_CHECK_ARG(gx && gpatch && partial && B > 0 && T > 1 && D > 0, "dfu_vit_embed_bwd: bad args");
   LAUNCH(k_vit_embed_bwd, (int64_t)T * D, stream, gx, B, T, D, dcls, dpos, (bf16_t*)gpatch, partial);
-  if (dbias) LAUNCH(k_sum_rows_add, (int64_t)D, stream, partial, T, D, dbias);
+  if (dbias) {
+    hipLaunchKernelGGL(k_sum_rows_add, dim3((D + SRA_C - 1) / SRA_C), dim3(SRA_C * SRA_R), 0,
+                       (hipStream_t)stream, partial, T, D, dbias);
+    DFU_LAUNCH_CHECK();
+  }
   return DFU_OK;
 }
 

@@ -41,6 +41,9 @@ int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: of
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
 const int g_wide_reduce = getenv("DFU_GEMM_WIDE_REDUCE") ? atoi(getenv("DFU_GEMM_WIDE_REDUCE")) : 1;
 int g_tail_split = 1;       // dfu_gemm_set_tail_split
+// DFU_GEMM_SPLIT_DIV=d: tuned split-K counts divided by d (A/B: fewer fp32 slabs and reduce
+// traffic against longer weight-gradient GEMMs)
+const int g_split_div = getenv("DFU_GEMM_SPLIT_DIV") ? atoi(getenv("DFU_GEMM_SPLIT_DIV")) : 1;
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
@@ -102,6 +105,7 @@ Plan plan_gemm(const dfu_gemm_desc* d) {
       pl.tile = tp->tile - 1;
       pl.entry = find_entry(d->a_mode, d->b_mode, d->epilogue, pl.tile);
       pl.split = acc_epi ? tp->split : 1;
+      if (g_split_div > 1 && pl.split > 1) pl.split = (pl.split + g_split_div - 1) / g_split_div;
       pl.cost = 0.0;
       if (pl.entry) return pl;
     }
