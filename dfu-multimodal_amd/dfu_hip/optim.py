@@ -83,6 +83,8 @@ class FlatParams:
         self.t_params = []   # parameters with a transposed (p._dfu_shadow_T) or flipped
         self.t_pairs = []    # (p._dfu_shadow_F) shadow, and their (src, dst) transpose jobs
         self.t_jobs = None
+        self.t_pairs_of = {}  # id(p) -> its transpose jobs
+        self._range_jobs = {}  # (lo, hi) -> (jobs of the parameters inside, jobs of the rest)
         with torch.no_grad():
             for p, o, kr in zip(self.params, self.offsets, self.krsc):
                 view = _view(self.data, o, p, kr)
@@ -131,14 +133,32 @@ class FlatParams:
     def _add_jobs(self, p, pairs):
         self.t_params.append(p)
         self.t_pairs += pairs
+        self.t_pairs_of[id(p)] = pairs
         self.t_jobs = ops.TransposeJobs(self.t_pairs)
+        self._range_jobs = {}
 
-    def shadows_rewritten(self):
+    def range_jobs(self, lo, hi):
+        """(TransposeJobs of the transposed parameters inside flat range [lo, hi), those of the
+        rest), either None when empty; cached per range."""
+        key = (lo, hi)
+        if key not in self._range_jobs:
+            inside, rest = [], []
+            for i, p in enumerate(self.params):
+                pairs = self.t_pairs_of.get(id(p))
+                if pairs:
+                    (inside if lo <= self.offsets[i] < hi else rest).extend(pairs)
+            self._range_jobs[key] = (ops.TransposeJobs(inside) if inside else None,
+                                     ops.TransposeJobs(rest) if rest else None)
+        return self._range_jobs[key]
+
+    def shadows_rewritten(self, done=None):
         """Every shadow was just rewritten (AdamW, refresh): re-derive the transposed ones (the
-        flipped conv copies follow on their next use: gen changed)."""
+        flipped conv copies follow on their next use: gen changed).  done = (lo, hi): the
+        transposed parameters in that range were already re-derived (the early update)."""
         self.gen += 1
-        if self.t_jobs is not None:
-            self.t_jobs.launch()
+        jobs = self.t_jobs if done is None else self.range_jobs(*done)[1]
+        if jobs is not None:
+            jobs.launch()
         for p in self.t_params:
             p._dfu_sgen = p._dfu_tgen = self.gen
 
@@ -170,6 +190,11 @@ class FlatParams:
             elif g.data_ptr() != v.data_ptr():
                 v.copy_(g)
                 p.grad = v
+
+
+# DFU_EARLY_TRANSPOSE=0: the early-updated block's transposed shadows are re-derived in the
+# step's tail with the rest (A/B)
+_EARLY_T = os.environ.get("DFU_EARLY_TRANSPOSE", "1") != "0"
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -252,6 +277,11 @@ class FusedAdamW(torch.optim.Optimizer):
             with torch.cuda.stream(st):
                 ops.step_increment(self.step_dev)  # the rest runs after the join: sees it
                 self._adamw(lo, hi)
+                # the block's transposed shadows right behind its update, beside the other
+                # branch's backward tail instead of in the step's serial end
+                inside = fp.range_jobs(lo, hi)[0] if fp.t_jobs is not None and _EARLY_T else None
+                if inside is not None:
+                    inside.launch()
             cur.wait_stream(st)  # the rest, the step counter and the shadow transposes after it
         Fn.join_grad_streams()
         if rebind:
@@ -266,7 +296,8 @@ class FusedAdamW(torch.optim.Optimizer):
         for p in fp.params:
             p._dfu_grad_stream = None
         self.last_early = None if early is None else early[:2]
-        fp.shadows_rewritten()
+        fp.shadows_rewritten(None if early is None or fp.t_jobs is None or not _EARLY_T
+                             else early[:2])
         self._grad_version = fp.grad._version
         return loss
 
