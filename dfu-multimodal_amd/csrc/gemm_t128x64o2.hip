@@ -9,6 +9,7 @@ const Entry kTable128x64o2[] = {
     E(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
     E(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_STATS),
     E(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_STATS),
+    E(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_ADD),  // 1x1 dgrad on the transposed weight
     E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_BF16_STATS),
     E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_F32_STATS),
     E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_BF16),  // stride-1 dgrad on flipped weights

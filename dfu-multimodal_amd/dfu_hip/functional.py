@@ -388,6 +388,22 @@ def conv_weight_flipped(w):
     return w._dfu_shadow_F
 
 
+# 1x1 stride-1 input gradients of at most this many input channels (layer 1's 64: the N = 64
+# GEMMs, which the 64-column tiles run only with a K-contiguous weight operand) on the
+# transposed weight shadow (weight_bf16_T, refreshed with the optimizer's batched transposes).
+# DFU_DGRAD_T1X1_MAXC=0: the MN-major weight view (A/B timing).
+_DGRAD_T1X1_MAXC = int(os.environ.get("DFU_DGRAD_T1X1_MAXC", "64"))
+
+
+def conv1x1_weight_T(conv, geom):
+    """The transposed bf16 shadow [C][K] of a FusedAdamW-managed 1x1 stride-1 conv weight with
+    at most _DGRAD_T1X1_MAXC input channels (conv_dgrad's w_t), else None."""
+    if (geom.r == 1 and geom.s == 1 and geom.stride == 1 and geom.pad == 0
+            and geom.c <= _DGRAD_T1X1_MAXC):
+        return weight_bf16_T(conv.weight)
+    return None
+
+
 def conv_weight_bf16(w):
     """fp32 OIHW conv weight -> bf16 KRSC GEMM operand: the shadow view for a 1x1 conv (OIHW ==
     KRSC) and for a FusedAdamW-managed weight stored channels-last; else a packing kernel."""
@@ -506,14 +522,22 @@ def conv_fwd_x3(x3_rows, geom, w3, y, stats):
                  epilogue=L.EPI_F32_STATS, stats=stats, conv=g3)
 
 
-def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, bn=None, y=None, w_flip=None):
+def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, bn=None, y=None, w_flip=None, w_t=None):
     """dx[N*H*W, C] = dgrad(dy) (+ add, bf16).  With bn (a _BN whose input y is this conv's
     input, BN + ReLU without residual; stride 1): the epilogue also reduces that BN's
     backward sums over dx (DFU_EPI_BF16_DSTATS); returns the [tiles][2][C] records for
     _BN.backward_from_dstats.  With w_flip (conv_weight_flipped; stride 1, no add, no bn): dx
-    is the forward convolution of dy (K input channels, pad R-1-pad) with the flipped weight."""
+    is the forward convolution of dy (K input channels, pad R-1-pad) with the flipped weight.
+    With w_t (conv1x1_weight_T; a 1x1 stride-1 conv, no bn): dx = dy W as a K-contiguous GEMM
+    on the transposed [C][K] weight."""
     g = geom
     Mx = g.n * g.h * g.w
+    if (w_t is not None and bn is None and g.r == 1 and g.s == 1 and g.stride == 1
+            and g.pad == 0):
+        ops.gemm(Mx, g.c, g.k, dy_rows, g.k, w_t, g.k, dx, g.c,
+                 epilogue=L.EPI_BF16_ADD if add is not None else L.EPI_BF16, aux=add,
+                 ldaux=g.c if add is not None else 0)
+        return None
     if w_flip is not None and add is None and bn is None and g.stride == 1:
         gd = ops.ConvGeom(g.n, g.p, g.q, g.k, g.c, g.r, g.s, 1, g.r - 1 - g.pad)
         if (gd.p, gd.q) == (g.h, g.w) and g.r - 1 - g.pad >= 0:
@@ -809,7 +833,8 @@ class BottleneckFn(torch.autograd.Function):
         # conv3 (bf16 mode: bn2's backward sums reduced in its dgrad epilogue)
         fuse = not ctx.x3 and FUSE_BN_DSTATS and g2.k >= FUSE_BN_DSTATS_MIN_C
         da2 = torch.empty_like(a2)
-        st2 = conv_dgrad(dy3, g3, w3, da2, bn=s2 if fuse else None, y=y2)
+        st2 = conv_dgrad(dy3, g3, w3, da2, bn=s2 if fuse else None, y=y2,
+                         w_t=None if fuse else conv1x1_weight_T(mod.conv3, g3))
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[1], from_rows(da2, B, g2.p, g2.q, g2.k))
         if _wants(mod.conv3.weight):
@@ -842,11 +867,13 @@ class BottleneckFn(torch.autograd.Function):
         dx = None
         if ctx.x_requires_grad:
             dxr = _empty((M1, Cin), BF16, dev)
+            w1t = conv1x1_weight_T(mod.conv1, g1)
             if dyd is None:  # identity shortcut: its gradient rides in conv1's dgrad epilogue
-                conv_dgrad(dy1, g1, w1, dxr, add=dres)
+                conv_dgrad(dy1, g1, w1, dxr, add=dres, w_t=w1t)
             else:  # downsample: conv1's dgrad, then the (strided) 1x1 dgrad added in place
-                conv_dgrad(dy1, g1, w1, dxr)
-                conv_dgrad(dyd, gd, wd, dxr, add=dxr)
+                conv_dgrad(dy1, g1, w1, dxr, w_t=w1t)
+                conv_dgrad(dyd, gd, wd, dxr, add=dxr,
+                           w_t=conv1x1_weight_T(mod.downsample[0], gd))
             dx = from_rows(dxr, B, H, W, Cin)
         if _wants(mod.conv1.weight):
             conv_wgrad(dy1, xr, g1, grad_buffer(mod.conv1.weight))

@@ -299,3 +299,53 @@ def test_stride1_dgrad_on_flipped_weights(monkeypatch):
     wb = Fn.weight_bf16_rows(w).view(256, 3, 3, 256).permute(0, 3, 1, 2).float()
     ref = torch.nn.grad.conv2d_input((4, 256, 14, 14), wb, dy.float(), padding=1)
     assert rel(dx.view(4, 14, 14, 256).permute(0, 3, 1, 2), ref) < 2e-2
+
+
+def test_1x1_dgrad_on_transposed_weights(monkeypatch):
+    """Layer 1's 1x1 input gradients to 64 channels (conv3 of every block, conv1 and the
+    downsample of block 0: N = 64 GEMMs) run K-contiguous on the transposed bf16 shadow
+    (functional.conv1x1_weight_T, kept current by the optimizer's batched transposes): outputs
+    unchanged; every gradient matches the MN-major weight form to summation-order rounding of
+    the bf16 input gradients (relative L2 < 1e-2), before and after optimizer steps; the
+    transposed copy equals the shadow's transpose after each step; the ADD form against torch."""
+    from models.resnet import resnet50
+    from dfu_hip import functional as Fn
+    from dfu_hip.optim import FusedAdamW
+    torch.manual_seed(0)
+    net = resnet50(num_classes=0).to(DEV).train()
+    stage = net.layer1
+    opt = FusedAdamW(stage.parameters(), lr=1e-3, weight_decay=1e-4)
+    x0 = torch.randn(4, 64, 56, 56, device=DEV).contiguous(memory_format=torch.channels_last)
+    x0.requires_grad_(True)
+    for step in range(2):
+        res = []
+        for maxc in (0, 64):
+            monkeypatch.setattr(Fn, "_DGRAD_T1X1_MAXC", maxc)
+            opt.zero_grad()
+            x0.grad = None
+            y = stage(x0)
+            Rg = torch.randn(y.shape, device=DEV,
+                             generator=torch.Generator(device=DEV).manual_seed(step))
+            (y.float() * Rg).sum().backward()
+            res.append((y.detach().float(), x0.grad.float().clone(),
+                        [p.grad.clone() for p in stage.parameters()]))
+        torch.cuda.synchronize()
+        assert torch.equal(res[0][0], res[1][0]), "forward changed"
+        assert rel(res[1][1], res[0][1]) < 1e-2, (step, rel(res[1][1], res[0][1]))
+        for (n, _), g0, g1 in zip(stage.named_parameters(), res[0][2], res[1][2]):
+            assert rel(g1, g0) < 1e-2, (step, n, rel(g1, g0))
+        for conv in (stage[0].conv1, stage[0].conv3, stage[0].downsample[0], stage[2].conv3):
+            w = conv.weight
+            assert torch.equal(w._dfu_shadow_T, w._dfu_shadow.t()), (step, tuple(w.shape))
+        opt.step()
+    # the ADD form (downsample dgrad added in place) against torch on one conv
+    monkeypatch.setattr(Fn, "_DGRAD_T1X1_MAXC", 64)
+    conv = stage[0].downsample[0]
+    g = Fn._geom(conv, 4, 56, 56)
+    dy = torch.randn(4 * 56 * 56, 256, device=DEV).to(torch.bfloat16)
+    base = torch.randn(4 * 56 * 56, 64, device=DEV).to(torch.bfloat16)
+    dx = base.clone()
+    Fn.conv_dgrad(dy, g, None, dx, add=dx, w_t=Fn.conv1x1_weight_T(conv, g))
+    wb = Fn.weight_bf16_rows(conv.weight).float()  # [256][64]
+    ref = dy.float() @ wb + base.float()
+    assert rel(dx, ref) < 1e-2
