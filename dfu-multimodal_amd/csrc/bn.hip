@@ -386,6 +386,47 @@ __global__ void k_bn_bwd_apply(const bf16_t* __restrict__ dout, const bf16_t* __
   }
 }
 
+// ---------------------------------------------------------------- standalone statistics
+// The (sum, M2) record per 128-row tile and channel that the GEMM's BN-statistics epilogue
+// writes, computed from stored bf16 rows instead (a BatchNorm2d not fused behind a conv).
+// Block = 64 channel lanes x 4 row groups of 32 rows; pass 1 sums (tile mean), pass 2 sums the
+// squared deviations from it over the same rows (L1/L2-resident).
+__global__ __launch_bounds__(256) void k_bn_tile_stats(const bf16_t* __restrict__ x, int M, int C,
+                                                       float* __restrict__ stats) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane;
+  const int r0 = blockIdx.x * 128, nb = min(128, M - r0);
+  const int ra = r0 + g * 32, rb = min(r0 + nb, ra + 32);
+  float v[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int r = ra + i;
+    v[i] = (c < C && r < rb) ? bf2f(x[(int64_t)r * C + c]) : 0.f;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) s += v[i];
+  red[g][lane] = s;
+  __syncthreads();
+  const float tot = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  const float mu = tot / (float)nb;
+  __syncthreads();
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const float d = ra + i < rb ? v[i] - mu : 0.f;
+    q += d * d;
+  }
+  red[g][lane] = q;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    stats[((int64_t)blockIdx.x * 2 + 0) * C + c] = tot;
+    stats[((int64_t)blockIdx.x * 2 + 1) * C + c] = red[0][lane] + red[1][lane] + red[2][lane] +
+                                                    red[3][lane];
+  }
+}
+
 inline unsigned grid_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 65536) b = 65536;
@@ -424,6 +465,15 @@ extern "C" int dfu_bn_finalize(const float* stats, int32_t tiles, int32_t M, int
   hipLaunchKernelGGL(kern, dim3(gx, S), dim3(64 * FIN_WAVES), 0, (hipStream_t)stream, stats,
                      tiles, tps, M, C, gamma, beta, eps, momentum, running_mean, running_var,
                      num_batches, mean_out, invstd_out, scale_out, shift_out, ws, counters);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_bn_tile_stats(const void* x, int64_t M, int32_t C, float* stats,
+                                 void* stream) {
+  DFU_CHECK_ARG(x && stats && M > 0 && M < (1ll << 31) && C > 0, "dfu_bn_tile_stats: bad args");
+  hipLaunchKernelGGL(k_bn_tile_stats, dim3((unsigned)((M + 127) / 128), (C + 63) / 64), dim3(256),
+                     0, (hipStream_t)stream, (const bf16_t*)x, (int)M, C, stats);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -102,6 +102,7 @@ PROTOTYPES = {
     "dfu_bn_bwd_finalize_ws_bytes": [I32, I32],
     "dfu_bn_eval_coeffs": [P, P, P, P, F, I32, P, P, P],
     "dfu_bn_apply": [P, P, P, P, I32, P, I64, I32, P],
+    "dfu_bn_tile_stats": [P, I64, I32, P, P],
     "dfu_bn_apply_mask": [P, P, P, P, I32, P, P, I64, I32, P],
     "dfu_bn_bwd_blocks": [I64, I32],
     "dfu_bn_bwd_reduce": [P, P, P, I32, P, P, P, P, I64, I32, P, P],

@@ -12,62 +12,115 @@ import torch
 import torch.distributed as dist
 import torch.nn as tnn
 
+from . import _lib as L
 from . import functional as Fn
 from . import ops
 
 
 class Conv2d(tnn.Conv2d):
-    """Standalone NHWC implicit-GEMM convolution (bias-free, groups=1, dilation=1).
-    Inside ResNet the convolutions run fused with their BatchNorm (functional.BottleneckFn)."""
+    """Standalone convolution (bias-free, groups=1, dilation=1).  Inside ResNet the
+    convolutions run fused with their BatchNorm (functional.BottleneckFn).  NHWC implicit GEMM
+    when the input channels are a multiple of 64 (or a 1x1 stride-1 conv); otherwise, for
+    weights stored OIHW (channels not a multiple of 8: an image stem's 1 or 3), an explicit
+    im2col + GEMM as the ResNet stem runs (functional.StemFn)."""
 
     def forward(self, x):
         if self.bias is not None or self.groups != 1 or self.dilation != (1, 1):
             raise NotImplementedError("dfu_hip.nn.Conv2d: bias/groups/dilation unsupported")
+        C = x.shape[1]
+        R, S = self.kernel_size
+        plain = R == 1 and S == 1 and self.stride == (1, 1) and self.padding == (0, 0)
+        if C % 64 != 0 and not plain:
+            if Fn._krsc_strided(self.weight):
+                raise NotImplementedError(
+                    "dfu_hip.nn.Conv2d: a channels-last (FusedAdamW) weight needs C % 64 == 0")
+            return Conv2dIm2colFn.apply(x, self.weight, self)
         return Conv2dFn.apply(x, self.weight, self)
 
 
-class Conv2dFn(torch.autograd.Function):
+class Conv2dIm2colFn(torch.autograd.Function):
+    """Explicit im2col (bf16 [M][Kp], K = C*R*S padded to 16, (c, r, s) order as OIHW) + GEMM;
+    backward: weight gradient over the same columns, input gradient as fp32 dcol = dY W and its
+    col2im adjoint."""
+
     @staticmethod
     def forward(ctx, x, w, mod):
-        x = Fn.nhwc_bf16(x.detach())
         B, C, H, W = x.shape
-        g = Fn._geom(mod, B, H, W)
-        if C % 64 != 0 and not (g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0):
-            raise NotImplementedError("dfu_hip.nn.Conv2d: implicit GEMM needs C % 64 == 0")
-        wk = Fn.conv_weight_bf16(w)
-        M = B * g.p * g.q
-        y = torch.empty((M, g.k), dtype=torch.bfloat16, device=x.device)
-        stats = torch.empty((ops.stats_tiles(M), 2, g.k), dtype=torch.float32, device=x.device)
-        xr = Fn.rows_view(x)
-        Fn.conv_fwd(xr, g, wk, y, stats)
-        ctx.g, ctx.mod = g, mod
-        ctx.save_for_backward(xr, wk)
-        return Fn.from_rows(y, B, g.p, g.q, g.k)
+        R, S = mod.kernel_size
+        st, pad = mod.stride, mod.padding
+        if st[0] != st[1] or pad[0] != pad[1]:
+            raise NotImplementedError("dfu_hip.nn.Conv2d: square stride/padding only")
+        Kp = ((C * R * S + 15) // 16) * 16
+        xf = x.detach().float() if x.dtype != torch.float32 else x.detach()
+        col, P, Q = ops.im2col_f32(xf, R, S, st[0], pad[0], Kp)
+        wb = Fn.weight_bf16_rows(w, ld=Kp)
+        Cout, M = w.shape[0], B * P * Q
+        y = torch.empty((M, Cout), dtype=torch.bfloat16, device=x.device)
+        ops.gemm(M, Cout, Kp, col, Kp, wb, Kp, y, Cout, epilogue=L.EPI_BF16)
+        ctx.mod, ctx.dims, ctx.xdtype = mod, (B, C, H, W, P, Q, Kp, R, S, st[0], pad[0]), x.dtype
+        ctx.save_for_backward(col, wb)
+        return Fn.from_rows(y, B, P, Q, Cout)
 
     @staticmethod
     def backward(ctx, gy):
-        xr, wk = ctx.saved_tensors
-        g, mod = ctx.g, ctx.mod
+        col, wb = ctx.saved_tensors
+        B, C, H, W, P, Q, Kp, R, S, st, pad = ctx.dims
+        mod = ctx.mod
+        Cout, M, K = wb.shape[0], B * P * Q, C * R * S
         dy = Fn.rows_view(Fn.nhwc_bf16(gy))
+        if Fn._wants(mod.weight):
+            ops.gemm(Cout, K, M, dy, Cout, col, Kp, Fn.grad_buffer(mod.weight).view(Cout, K), K,
+                     a_mode=L.OPND_MNMAJOR, b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+            Fn.grads_done(mod.weight)
         dx = None
         if ctx.needs_input_grad[0]:
-            dxr = torch.empty((g.n * g.h * g.w, g.c), dtype=torch.bfloat16, device=xr.device)
-            Fn.conv_dgrad(dy, g, wk, dxr)
-            dx = Fn.from_rows(dxr, g.n, g.h, g.w, g.c)
-        if Fn._wants(mod.weight):
-            Fn.conv_wgrad(dy, xr, g, Fn.grad_buffer(mod.weight))
-            Fn.grads_done(mod.weight)
+            dcol = torch.empty((M, Kp), dtype=torch.float32, device=dy.device)
+            ops.gemm(M, Kp, Cout, dy, Cout, wb, Kp, dcol, Kp, b_mode=L.OPND_MNMAJOR,
+                     epilogue=L.EPI_F32)
+            dx = ops.col2im_f32(dcol, B, C, H, W, R, S, st, pad, P, Q, Kp)
+            if ctx.xdtype != torch.float32:
+                dx = dx.to(ctx.xdtype)
         return dx, None, None
 
 
 class BatchNorm2d(tnn.BatchNorm2d):
-    """Parameter/buffer holder; the normalisation runs fused into the producing convolution's
-    GEMM epilogue (statistics) and its apply/backward kernels (functional._BN)."""
+    """torch.nn.BatchNorm2d.  Inside ResNet blocks the normalisation runs fused with the
+    producing convolution (statistics from its GEMM epilogue, functional._BN); standalone, the
+    tile statistics come from the stored input (dfu_bn_tile_stats) and the same finalize /
+    apply / backward kernels run.  Output: bf16 channels_last."""
 
     def forward(self, x):
-        raise NotImplementedError(
-            "dfu_hip.nn.BatchNorm2d runs fused with its convolution inside ResNet blocks; "
-            "standalone BatchNorm2d is not part of the hot path")
+        return BatchNorm2dFn.apply(x, self.weight, self.bias, self)
+
+
+class BatchNorm2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, mod):
+        x = Fn.nhwc_bf16(x.detach())
+        B, C, H, W = x.shape
+        cv = C // 8  # 8-channel vectors; the backward reduce spreads min(cv, 64) over a block
+        if C % 8 != 0 or (cv < 64 and cv & (cv - 1)) or (cv >= 64 and cv % 64):
+            raise NotImplementedError("dfu_hip.nn.BatchNorm2d: channels must be 8, 16, 32, 64, "
+                                      "128, 256 or a multiple of 512")
+        M = B * H * W
+        xr = Fn.rows_view(x)
+        st = Fn._BN(mod, M, C, x.device)
+        st.forward_coeffs(ops.bn_tile_stats(xr, M, C) if st.training else None)
+        out = torch.empty((M, C), dtype=torch.bfloat16, device=x.device)
+        ops.bn_apply(xr, st.scale, st.shift, None, 0, out, M, C)
+        ctx.st = st
+        ctx.save_for_backward(xr)
+        return Fn.from_rows(out, B, H, W, C)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (xr,) = ctx.saved_tensors
+        M, C = xr.shape
+        g = Fn.rows_view(Fn.nhwc_bf16(gy))
+        dx = torch.empty_like(xr)
+        ctx.st.backward(g, xr, None, False, dx, None)
+        B, _, H, W = gy.shape
+        return Fn.from_rows(dx, B, H, W, C), None, None, None
 
 
 class ReLU(tnn.ReLU):

@@ -385,6 +385,15 @@ def bn_eval_coeffs(gamma, beta, rm, rv, eps, scale_out, shift_out):
           "dfu_bn_eval_coeffs")
 
 
+def bn_tile_stats(x, M, C):
+    """[ceil(M/128)][2][C] (sum, M2) records of bf16 rows x[M][C] (dfu_bn_finalize's input)."""
+    _req(x, BF16, "bn_tile_stats")
+    stats = torch.empty((stats_tiles(M), 2, C), dtype=F32, device=x.device)
+    check(lib().dfu_bn_tile_stats(ptr(x), int(M), int(C), ptr(stats), stream_ptr()),
+          "dfu_bn_tile_stats")
+    return stats
+
+
 def bn_apply(y, scale, shift, residual, relu, out, M, C, mask=None):
     """out = act(y * scale + shift (+ residual)); with `mask` (uint8 [M * C / 8]) also the bitmask
     of out > 0 that bn_bwd(relu=3) reads in place of out."""

@@ -247,6 +247,10 @@ int dfu_bn_finalize(const float* stats, int32_t tiles, int32_t M, int32_t C, con
  * tiles are reduced in parallel slices whose last block combines them in slice order (same
  * result for any arrival order); ws or counters NULL: one serial pass per channel group. */
 int64_t dfu_bn_finalize_ws_bytes(int32_t tiles, int32_t C);
+/* The per-128-row-tile (sum, M2) records of dfu_bn_finalize's `stats` ([ceil(M/128)][2][C],
+ * M2 about the tile mean) computed from stored bf16 rows x[M][C] -- a BatchNorm2d that does not
+ * follow a conv with the statistics epilogue (torch.nn.BatchNorm2d.forward, train mode). */
+int dfu_bn_tile_stats(const void* x, int64_t M, int32_t C, float* stats, void* stream);
 /* Eval-mode BN: scale/shift from running stats. */
 int dfu_bn_eval_coeffs(const float* gamma, const float* beta, const float* running_mean,
                        const float* running_var, float eps, int32_t C, float* scale_out,
