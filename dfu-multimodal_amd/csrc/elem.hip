@@ -127,6 +127,36 @@ __global__ __launch_bounds__(VPR * 16) void k_im2col_f32(
   }
 }
 
+// Any Kp (a standalone conv with few input channels, nn.Conv2d): one thread per 16-B output
+// vector, taps decoded per vector.
+__global__ __launch_bounds__(256) void k_im2col_f32_any(
+    const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int B, int C,
+    int H, int W, int R, int S, int stride, int pad, int P, int Q, int Kp,
+    bf16_t* __restrict__ out) {
+  const int vpr = Kp / 8, RS = R * S, KK = C * RS;
+  const int64_t n = (int64_t)B * P * Q * vpr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / vpr;
+    const int kv = (int)(i - m * vpr);
+    const int b = (int)(m / ((int64_t)P * Q));
+    const int rem = (int)(m - (int64_t)b * P * Q);
+    const int oh = rem / Q, ow = rem - (rem / Q) * Q;
+    const int ih0 = oh * stride - pad, iw0 = ow * stride - pad;
+    const float* xb = x + b * sn;
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = kv * 8 + e;
+      const int c = k / RS, rs = k - (k / RS) * RS;
+      const int ih = ih0 + rs / S, iw = iw0 + (rs - (rs / S) * S);
+      const bool ok = k < KK && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      f[e] = ok ? xb[c * sc + ih * sh + iw * sw] : 0.f;
+    }
+    *(u32x4*)(out + m * Kp + kv * 8) = pack8(f);
+  }
+}
+
 // The same rows staged through LDS: one block per output row (b, oh) loads the C x R input rows
 // that row's windows touch (rows outside the image as zeros) with coalesced fp32 reads, then
 // writes the Q x Kp output row segment with 16-B stores.  A thread owns one 8-tap chunk kv of
@@ -863,9 +893,12 @@ extern "C" int dfu_im2col_f32(const float* x, int64_t sn, int64_t sc, int64_t sh
       hipLaunchKernelGGL(k_im2col_f32<20>, dim3(blocks), dim3(320), 0, st, x, sn, sc, sh, sw, B,
                          C, H, W, R, S, stride, pad, P, Q, (bf16_t*)out);
       break;
-    default:
-      dfu_set_error("dfu_im2col_f32: Kp=%d not instantiated (160 = the ResNet 7x7x3 stem)", Kp);
-      return DFU_E_UNSUPPORTED;
+    default: {
+      const int64_t n = rows * (Kp / 8);
+      const unsigned g = (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
+      hipLaunchKernelGGL(k_im2col_f32_any, dim3(g), dim3(256), 0, st, x, sn, sc, sh, sw, B, C, H,
+                         W, R, S, stride, pad, P, Q, Kp, (bf16_t*)out);
+    }
   }
   DFU_LAUNCH_CHECK();
   return DFU_OK;

@@ -202,7 +202,8 @@ int dfu_transpose_bf16(const dfu_transpose_job* jobs, int32_t njobs, int32_t nti
 int dfu_cast_rows_f32(const void* in, int64_t ld_in, float* out, int64_t ld_out, int32_t rows,
                       int32_t cols, void* stream);
 /* Stem im2col (resnet conv1 7x7/s2/p3, train_multimodal_fusion.py:294): fp32 input with
- * arbitrary NCHW strides -> bf16 [B*P*Q][Kp], k = c*R*S + r*S + s (OIHW flatten order). */
+ * arbitrary NCHW strides -> bf16 [B*P*Q][Kp], k = c*R*S + r*S + s (OIHW flatten order), any
+ * Kp % 8 == 0 >= C*R*S (dfu_hip.nn.Conv2d's explicit path for other channel counts). */
 int dfu_im2col_f32(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
                    int32_t C, int32_t H, int32_t W, int32_t R, int32_t S, int32_t stride,
                    int32_t pad, int32_t P, int32_t Q, void* out, int32_t Kp, void* stream);
