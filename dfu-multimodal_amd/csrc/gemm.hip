@@ -44,6 +44,9 @@ int g_tail_split = 1;       // dfu_gemm_set_tail_split
 // DFU_GEMM_SPLIT_DIV=d: tuned split-K counts divided by d (A/B: fewer fp32 slabs and reduce
 // traffic against longer weight-gradient GEMMs)
 const int g_split_div = getenv("DFU_GEMM_SPLIT_DIV") ? atoi(getenv("DFU_GEMM_SPLIT_DIV")) : 1;
+// DFU_GEMM_SLOT_CAP=c: a persistent launch holds at most c CUs' worth of workgroups (A/B: leave
+// CUs to the other encoder stream of the fusion step instead of waiting for all of them)
+const int g_slot_cap = getenv("DFU_GEMM_SLOT_CAP") ? atoi(getenv("DFU_GEMM_SLOT_CAP")) : kCUs;
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
@@ -575,7 +578,7 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   // Persistent schedule: at most one wave of workgroups (CUs x occupancy), each walking its
   // work units as one K-step stream; split-K by fp32 atomics (no workspace) keeps one unit
   // per workgroup (its atomics have no fixed vmcnt count).
-  const int slots = kCUs * kOcc[pl.tile];
+  const int slots = (g_slot_cap > 0 && g_slot_cap < kCUs ? g_slot_cap : kCUs) * kOcc[pl.tile];
   a.tail_full = a.tail_r = a.tail_s = a.tail_kps = 0;
   a.tslab = nullptr;
   if (!acc_epi && splits == 1 && kTailOK[pl.tile]) {
