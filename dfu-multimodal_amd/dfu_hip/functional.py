@@ -241,6 +241,10 @@ def wgrad_stream(device):
     return st
 
 
+# DFU_RESNET_WGRAD_STREAM=0: the bottleneck weight-gradient GEMMs stay on the backward's own
+# stream when the ResNet runs alone (A/B)
+_RESNET_WGRAD_STREAM = os.environ.get("DFU_RESNET_WGRAD_STREAM", "1") != "0"
+
 _concurrent_encoders = [0]
 # DFU_VIT_WGRAD_BESIDE_FUSED=1: the ViT weight gradients run on the wgrad stream also while the
 # ResNet branch runs concurrently (A/B; default: inline on the ViT's own stream there)
@@ -786,6 +790,9 @@ class BottleneckFn(torch.autograd.Function):
             y3, out, s3 = conv_bn(a2, g3, w3, mod.bn3, True, residual=idn, mask=mask3)
         ctx.x3 = x3mode
         ctx.mod = mod
+        # weight gradients beside the input-gradient chain when the ResNet runs alone (as the ViT
+        # blocks'; inside the two-stream fusion step the other encoder fills the idle CUs)
+        ctx.beside = _RESNET_WGRAD_STREAM and _concurrent_encoders[0] == 0
         ctx.geo = (g1, g2, g3, gd)
         ctx.bns = (s1, s2, s3, sd)
         ctx.shape = (B, Cin, H, W)
@@ -817,6 +824,19 @@ class BottleneckFn(torch.autograd.Function):
         dev = xr.device
         g = rows_view(nhwc_bf16(gout))
         M1, M2 = y1.shape[0], y3.shape[0]
+        convs = (mod.conv1, mod.conv2, mod.conv3) + (
+            (mod.downsample[0],) if mod.downsample is not None else ())
+        # (no fork without work: a graph capture rejects an unjoined side stream)
+        bw = _Beside(wgrad_stream(dev) if ctx.beside and g.is_cuda and
+                     any(_wants(c.weight) for c in convs) else None)
+
+        def wgrad(conv, dy, x, geom):
+            if _wants(conv.weight):
+                def fn():
+                    conv_wgrad(dy, x, geom, grad_buffer(conv.weight))
+                    grads_done(conv.weight)
+                bw.run(fn, dy, x)
+
         # bn3 (+ residual) + relu: the mask from the forward's bitmask (bf16) or its output (x3)
         dy3 = torch.empty_like(y3)
         dres = torch.empty_like(y3)
@@ -826,10 +846,7 @@ class BottleneckFn(torch.autograd.Function):
         if yd is not None:
             dyd = torch.empty_like(yd)
             sd.backward(dres, yd, None, False, dyd, None)
-            dconv = mod.downsample[0]
-            if _wants(dconv.weight):
-                conv_wgrad(dyd, xr, gd, grad_buffer(dconv.weight))
-                grads_done(dconv.weight)
+            wgrad(mod.downsample[0], dyd, xr, gd)
         # conv3 (bf16 mode: bn2's backward sums reduced in its dgrad epilogue)
         fuse = not ctx.x3 and FUSE_BN_DSTATS and g2.k >= FUSE_BN_DSTATS_MIN_C
         da2 = torch.empty_like(a2)
@@ -837,9 +854,7 @@ class BottleneckFn(torch.autograd.Function):
                          w_t=None if fuse else conv1x1_weight_T(mod.conv3, g3))
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[1], from_rows(da2, B, g2.p, g2.q, g2.k))
-        if _wants(mod.conv3.weight):
-            conv_wgrad(dy3, a2, g3, grad_buffer(mod.conv3.weight))
-            grads_done(mod.conv3.weight)
+        wgrad(mod.conv3, dy3, a2, g3)
         # bn2 + relu, conv2
         # BN + ReLU masks: recomputed from y (bf16), or in bf16x3 mode (fp32 pre-activations)
         # read from the forward's outputs
@@ -855,9 +870,7 @@ class BottleneckFn(torch.autograd.Function):
                          conv_weight_flipped(mod.conv2.weight))
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[0], from_rows(da1, B, g1.p, g1.q, g1.k))
-        if _wants(mod.conv2.weight):
-            conv_wgrad(dy2, a1, g2, grad_buffer(mod.conv2.weight))
-            grads_done(mod.conv2.weight)
+        wgrad(mod.conv2, dy2, a1, g2)
         # bn1 + relu, conv1 (+ identity gradient fused in the dgrad epilogue)
         dy1 = torch.empty_like(y1)
         if st1 is not None:
@@ -875,9 +888,7 @@ class BottleneckFn(torch.autograd.Function):
                 conv_dgrad(dyd, gd, wd, dxr, add=dxr,
                            w_t=conv1x1_weight_T(mod.downsample[0], gd))
             dx = from_rows(dxr, B, H, W, Cin)
-        if _wants(mod.conv1.weight):
-            conv_wgrad(dy1, xr, g1, grad_buffer(mod.conv1.weight))
-            grads_done(mod.conv1.weight)
+        wgrad(mod.conv1, dy1, xr, g1)
         n_params = len(ctx.needs_input_grad) - 2
         return (dx,) + (None,) * n_params + (None,)
 
