@@ -241,9 +241,10 @@ def wgrad_stream(device):
     return st
 
 
-# DFU_RESNET_WGRAD_STREAM=0: the bottleneck weight-gradient GEMMs stay on the backward's own
-# stream when the ResNet runs alone (A/B)
-_RESNET_WGRAD_STREAM = os.environ.get("DFU_RESNET_WGRAD_STREAM", "1") != "0"
+# DFU_RESNET_WGRAD_STREAM=1: the bottleneck weight-gradient GEMMs run on the wgrad stream when
+# the ResNet runs alone (A/B; off: RGB-only 10.0-11.9 vs 9.1-10.2 ms per step, same box -- the
+# conv wgrads are not small gap-fillers, they compete with the input-gradient chain)
+_RESNET_WGRAD_STREAM = os.environ.get("DFU_RESNET_WGRAD_STREAM", "0") != "0"
 
 _concurrent_encoders = [0]
 # DFU_VIT_WGRAD_BESIDE_FUSED=1: the ViT weight gradients run on the wgrad stream also while the
