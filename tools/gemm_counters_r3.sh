@@ -5,7 +5,7 @@
 # instruction counts.  tools/gemm_counters_summary.py turns gpurun_out/ctr3 into a table.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$R/gpurun_out/ctr3
+OUT=$R/gpurun_out/${CTR:-ctr3}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 PA="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
