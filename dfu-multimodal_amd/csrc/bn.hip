@@ -13,7 +13,10 @@ namespace {
 // then a 16-way LDS reduction.  Per tile t (nb rows): sum sb and M2 qb -> sum of squares
 // qb + sb^2/nb.  fp64 sums of x and x^2 over <= 1e6 rows of bf16-scale values keep
 // var = E[x^2] - mean^2 exact to ~1e-12 relative, and the tile loop is independent adds.
-constexpr int FIN_WAVES = 16;
+#ifndef DFU_FIN_WAVES
+#define DFU_FIN_WAVES 16  // (-DDFU_FIN_WAVES=n: A/B builds, tools/build_fin.sh)
+#endif
+constexpr int FIN_WAVES = DFU_FIN_WAVES;
 
 // CPW channels per block: a wave's 64 lanes cover CPW channels x (64 / CPW) tile slots, so
 // narrow layers (C = 64 over up to 6272 stem tiles) spread their tile loop over more lanes.
@@ -48,7 +51,7 @@ DFU_DEV bool last_slice(int* counter, int S, int* flag) {
 }
 
 template <int CPW>
-__global__ __launch_bounds__(1024) void k_bn_finalize(
+__global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_finalize(
     const float* __restrict__ stats, int tiles, int tps, int M, int C,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
@@ -293,7 +296,7 @@ __global__ void k_bn_bwd_reduce(const bf16_t* __restrict__ dout, const bf16_t* _
 // 16 waves x 64 channel-lanes per workgroup (coalesced 256-B row segments of the partials, the
 // waves stride the row-blocks); fp64 sums, 16-way LDS reduction.
 // Slices over the row-blocks as k_bn_finalize (blockIdx.y, last arriver sums in slice order).
-__global__ __launch_bounds__(1024) void k_bn_bwd_finalize(
+__global__ __launch_bounds__(64 * FIN_WAVES) void k_bn_bwd_finalize(
     const float* __restrict__ partial, int blocks, int bps, int64_t M, int C,
     const float* __restrict__ gamma, const float* __restrict__ invstd, int batch_stats,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef,
