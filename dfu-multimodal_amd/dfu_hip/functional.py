@@ -417,9 +417,64 @@ def conv_weight_bf16(w):
     return ops.pack_conv_weight(w.detach())
 
 
+# bf16x3 weight operands ([hi | hi | lo] rows) are cached per parameter and re-derived, after
+# the weights change, for every weight of a stream's group in ONE launch (ops.SplitJobs): the
+# group is the set of weights first split on that stream (an encoder's), so the first stale
+# weight an encoder asks for in a step refreshes all of its weights at once instead of one
+# launch per layer.  DFU_X3_WEIGHT_CACHE=0: one split per use (A/B).
+_X3_CACHE = os.environ.get("DFU_X3_WEIGHT_CACHE", "1") != "0"
+_x3_groups = {}  # raw stream -> _X3Group
+
+
+def _x3_key(w):
+    """Changes whenever w's values may have: an in-place edit (version counter) or a FusedAdamW
+    step or refresh (its FlatParams generation: kernel writes do not bump the version)."""
+    flat = getattr(w, "_dfu_flat", None)
+    return (w._version, flat.gen if flat is not None else None)
+
+
+class _X3Group:
+    def __init__(self, stream):
+        self.stream = stream
+        self.params = []
+        self.jobs = None
+
+    def add(self, w):
+        # (the table is rebuilt here, on first use -- the first step -- not in a refresh, which
+        # may run under a graph capture)
+        self.params.append(w)
+        self.jobs = ops.SplitJobs([(p.detach().reshape(p.shape[0], -1), p._dfu_x3w[0], ops.X3_B)
+                                   for p in self.params])
+
+    def refresh(self):
+        self.jobs.launch()
+        for w in self.params:
+            w._dfu_x3w[2] = _x3_key(w)
+
+
 def weight_x3_rows(w, seg=None):
     """fp32 [N, K...] parameter -> bf16x3 GEMM B operand [N, 3 seg] = [hi | hi | lo]."""
-    return ops.split_x3(w.detach().reshape(w.shape[0], -1), ops.X3_B, seg=seg)
+    w2 = w.detach().reshape(w.shape[0], -1)
+    if not (_X3_CACHE and w.is_cuda and w2.stride(1) == 1):
+        return ops.split_x3(w2, ops.X3_B, seg=seg)
+    seg = (w2.shape[1] + 7) // 8 * 8 if seg is None else int(seg)
+    ent = getattr(w, "_dfu_x3w", None)
+    st = ops.stream_ptr().value
+    if ent is None:
+        grp = _x3_groups.get(st)
+        if grp is None:
+            grp = _x3_groups[st] = _X3Group(st)
+        buf = ops.split_x3(w2, ops.X3_B, seg=seg)
+        w._dfu_x3w = [buf, seg, _x3_key(w), grp]
+        grp.add(w)
+        return buf
+    if ent[1] != seg or ent[3].stream != st:
+        # another padding, or another stream than its group's (whose refreshes would race with
+        # this use): a split of its own
+        return ops.split_x3(w2, ops.X3_B, seg=seg)
+    if ent[2] != _x3_key(w):
+        ent[3].refresh()
+    return ent[0]
 
 
 def conv_weight_x3(w):

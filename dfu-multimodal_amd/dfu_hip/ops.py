@@ -729,6 +729,33 @@ def split_x3(x, pattern, seg=None, hi_out=None):
     return out
 
 
+class SplitJobs:
+    """A device table of bf16x3 splits (dfu_split_x3_batch) launched as ONE kernel: jobs
+    (src fp32 [rows, cols] with unit column stride, out bf16 [rows, 3 seg], pattern)."""
+
+    def __init__(self, jobs):
+        import struct
+        raw, v0 = bytearray(), 0
+        for src, out, pattern in jobs:
+            _req(src, F32, "split_x3_batch")
+            _req(out, BF16, "split_x3_batch")
+            rows, cols = src.shape
+            seg = out.shape[1] // 3
+            if (src.stride(1) != 1 or out.shape != (rows, 3 * seg) or not out.is_contiguous()
+                    or seg % 8 or seg < cols or out.data_ptr() % 16):
+                raise ValueError(f"split_x3_batch: [{rows}, {cols}] -> {tuple(out.shape)}")
+            raw += struct.pack("<QQqqiiii", src.data_ptr(), out.data_ptr(), src.stride(0), v0,
+                               rows, cols, seg, int(pattern))
+            v0 += rows * (seg // 8)
+        self.jobs = list(jobs)  # keep the buffers alive as long as the table
+        self.njobs, self.nvec = len(self.jobs), v0
+        self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.jobs[0][0].device)
+
+    def launch(self):
+        check(lib().dfu_split_x3_batch(ptr(self.table), self.njobs, self.nvec, stream_ptr()),
+              "dfu_split_x3_batch")
+
+
 def pack_conv_weight_x3(w):
     """fp32 OIHW -> bf16 KRSC' (C' = 3C, pattern 1)."""
     _req(w, F32, "pack_conv_weight_x3")

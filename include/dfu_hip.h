@@ -433,6 +433,12 @@ int dfu_metrics_accumulate(const float* logits, const int64_t* labels, int32_t r
  * columns past cols zero); optional plain bf16 copy hi_out [rows][ld_hi >= seg]. */
 int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_t cols, int32_t seg,
                  void* out, int32_t pattern, void* hi_out, int64_t ld_hi, void* stream);
+/* Many dfu_split_x3 (pattern and seg per job) as ONE launch.  jobs: a DEVICE array of njobs
+ * records {const float* in; void* out; int64_t ld_in; int64_t v0; int32_t rows, cols, seg,
+ * pattern;} (48 bytes each), v0 = the job's first 8-column vector = the sum of rows * seg / 8
+ * over the jobs before it (ascending); nvec = that sum over all jobs.  The bf16x3 weight
+ * operands of an encoder, re-derived once per optimizer step (dfu_hip.functional). */
+int dfu_split_x3_batch(const void* jobs, int32_t njobs, int64_t nvec, void* stream);
 /* fp32 OIHW conv weight -> bf16 KRSC' with C' = 3C, pattern 1 along the channels. */
 int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int32_t C, int32_t R, int32_t S,
                             void* stream);
