@@ -421,8 +421,11 @@ def conv_weight_bf16(w):
 # the weights change, for every weight of a stream's group in ONE launch (ops.SplitJobs): the
 # group is the set of weights first split on that stream (an encoder's), so the first stale
 # weight an encoder asks for in a step refreshes all of its weights at once instead of one
-# launch per layer.  DFU_X3_WEIGHT_CACHE=0: one split per use (A/B).
-_X3_CACHE = os.environ.get("DFU_X3_WEIGHT_CACHE", "1") != "0"
+# launch per layer.  Off by default (DFU_X3_WEIGHT_CACHE=1 enables it): the bf16x3 fusion step
+# measured 26.87-26.94 ms with it against 26.76-26.85 ms without (same box) -- the one batched
+# refresh sits at the head of each encoder stream, while the per-layer splits overlap the other
+# stream's work.
+_X3_CACHE = os.environ.get("DFU_X3_WEIGHT_CACHE", "0") != "0"
 _x3_groups = {}  # raw stream -> _X3Group
 
 
