@@ -24,6 +24,7 @@ view) and ``p.grad`` into a matching flat gradient buffer, so:
     ``FlatParams.refresh_shadow()`` after those.
 """
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -197,6 +198,26 @@ class FlatParams:
 _EARLY_T = os.environ.get("DFU_EARLY_TRANSPOSE", "1") != "0"
 
 
+def _order_hook(wref):
+    """Grad-ready hook of one FusedAdamW (weakly referenced): notes the completion order of its
+    parameters' gradients and records the early main block's trigger event."""
+    def hook(p):
+        o = wref()
+        if o is None:
+            return
+        i = o._pidx.get(id(p))
+        if i is None or i in o._seen:
+            return
+        o._seen.add(i)
+        o._order.append(i)
+        t = o._trigger
+        if t is not None and i == t[0] and o.early_main:
+            ev = torch.cuda.Event()
+            ev.record()  # on the stream that produced the gradient (the current one)
+            o._trig_ev = ev
+    return hook
+
+
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
                  amsgrad=False, maximize=False):
@@ -215,6 +236,23 @@ class FusedAdamW(torch.optim.Optimizer):
         self.check_grads = True  # set False inside captured graphs (pointers are static)
         # update a side stream's parameter block on that stream (step); DFU_EARLY_ADAMW=0: off
         self.early_update = os.environ.get("DFU_EARLY_ADAMW", "1") != "0"
+        # the main stream's early block (DFU_EARLY_ADAMW_MAIN=0: off): the parameters whose
+        # gradients the backward's own stream finishes first (the ResNet's deep stages: its
+        # backward runs layer4 -> stem) are updated on an optimizer stream as soon as the last
+        # of them is done (an event recorded by a grad-ready hook), beside the rest of that
+        # backward instead of in the step's serial tail; learned from the previous step's
+        # completion order.  Its AdamW reads its own step counter (step_dev_b, kept equal).
+        self.early_main = os.environ.get("DFU_EARLY_ADAMW_MAIN", "1") != "0"
+        self.step_dev_b = torch.zeros((), dtype=torch.int64, device=dev)
+        self._pidx = {id(p): i for i, p in enumerate(self.flat.params)}
+        self._order, self._seen = [], set()
+        self._trigger = None   # (param index, lo, hi) learned from a step's completion order
+        self._learned_n = -1
+        self._trig_ev = None   # recorded this step when the trigger parameter completed
+        self._ost = None
+        self.last_early_main = None
+        if dev.type == "cuda":
+            Fn.register_grad_ready_hook(_order_hook(weakref.ref(self)))
         self._dfu_joins_itself = True  # step() joins the gradient streams (functional)
         # the flat gradient buffer's autograd version at the last zero_grad / step: the kernels
         # write gradients through raw pointers (no bump), so a change means user code edited
@@ -244,13 +282,45 @@ class FusedAdamW(torch.optim.Optimizer):
                 best = run
         return best if best is not None and best[1] - best[0] >= (1 << 20) else None
 
-    def _adamw(self, lo, hi):
+    def _adamw(self, lo, hi, step_dev=None):
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         fp = self.flat
         ops.adamw_flat(fp.data[lo:hi], fp.grad[lo:hi], self.exp_avg[lo:hi],
                        self.exp_avg_sq[lo:hi], g["lr"], b1, b2, g["eps"], g["weight_decay"],
-                       self.step_dev, shadow=None if fp.shadow is None else fp.shadow[lo:hi])
+                       self.step_dev if step_dev is None else step_dev,
+                       shadow=None if fp.shadow is None else fp.shadow[lo:hi])
+
+    def _learn_trigger(self, cur):
+        """From this step's completion order: the largest run of parameters, contiguous in the
+        flat buffers, all produced on `cur` and complete while at most 90% of that stream's
+        gradient elements are -> (index of the parameter whose completion closes the run, lo,
+        hi), or None (runs are merged as their parameters complete: interval union)."""
+        fp = self.flat
+        main = [i for i in self._order if fp.params[i]._dfu_grad_stream == cur]
+        n = len(fp.params)
+        size = [_aligned(p.numel()) for p in fp.params]
+        total = sum(size[i] for i in main)
+        pre = [0]
+        for z in size:
+            pre.append(pre[-1] + z)
+        left, right = {}, {}
+        best, acc = None, 0
+        for i in main:
+            acc += size[i]
+            if acc > 0.9 * total:
+                break
+            lo_i = left[i - 1] if i - 1 in right else i
+            hi_i = right[i + 1] if i + 1 in left else i
+            right[lo_i], left[hi_i] = hi_i, lo_i
+            left.setdefault(i, lo_i)
+            right.setdefault(i, hi_i)
+            run = pre[hi_i + 1] - pre[lo_i]
+            if best is None or run > best[2] - best[1]:
+                best = (i, fp.offsets[lo_i], fp.offsets[hi_i] + size[hi_i])
+        if best is None or best[2] - best[1] < (1 << 20) or n == 0:
+            return None
+        return best
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -271,9 +341,16 @@ class FusedAdamW(torch.optim.Optimizer):
         if (self.early_update and fp.data.is_cuda and not _dp_world() and not rebind
                 and not touched):
             early = self._early_range(torch.cuda.current_stream(fp.data.device))
+        cur = torch.cuda.current_stream(fp.data.device) if fp.data.is_cuda else None
+        early_main = None
+        if (self.early_main and fp.data.is_cuda and not _dp_world() and not rebind and not touched
+                and self._trigger is not None and self._trig_ev is not None):
+            tr = self._trigger
+            if fp.params[tr[0]]._dfu_grad_stream == cur and (
+                    early is None or tr[2] <= early[0] or tr[1] >= early[1]):
+                early_main = tr[1:]
         if early is not None:
             lo, hi, st = early
-            cur = torch.cuda.current_stream(fp.data.device)
             with torch.cuda.stream(st):
                 ops.step_increment(self.step_dev)  # the rest runs after the join: sees it
                 self._adamw(lo, hi)
@@ -283,18 +360,34 @@ class FusedAdamW(torch.optim.Optimizer):
                 if inside is not None:
                     inside.launch()
             cur.wait_stream(st)  # the rest, the step counter and the shadow transposes after it
+        if early_main is not None:
+            if self._ost is None:
+                self._ost = Fn.new_stream(fp.data.device.index)
+            self._ost.wait_event(self._trig_ev)
+            with torch.cuda.stream(self._ost):
+                ops.step_increment(self.step_dev_b)
+                self._adamw(early_main[0], early_main[1], self.step_dev_b)
+            cur.wait_stream(self._ost)
+        else:
+            ops.step_increment(self.step_dev_b)
         Fn.join_grad_streams()
         if rebind:
             fp.rebind_grads()
         if early is None:
             ops.step_increment(self.step_dev)
-            self._adamw(0, fp.numel)
-        else:
-            for a, b in ((0, early[0]), (early[1], fp.numel)):
-                if b > a:
-                    self._adamw(a, b)
+        done = sorted(r for r in (None if early is None else early[:2], early_main) if r)
+        a = 0
+        for r in done + [(fp.numel, fp.numel)]:
+            if r[0] > a:
+                self._adamw(a, r[0])
+            a = max(a, r[1])
+        if self.early_main and cur is not None and len(self._order) != self._learned_n:
+            self._trigger = self._learn_trigger(cur)  # (the order is the same every step)
+            self._learned_n = len(self._order)
+        self._order, self._seen, self._trig_ev = [], set(), None
         for p in fp.params:
             p._dfu_grad_stream = None
+        self.last_early_main = early_main
         self.last_early = None if early is None else early[:2]
         fp.shadows_rewritten(None if early is None or fp.t_jobs is None or not _EARLY_T
                              else early[:2])
@@ -334,4 +427,6 @@ class FusedAdamW(torch.optim.Optimizer):
         if len(steps) > 1:
             raise ValueError(f"FusedAdamW: parameters at different steps {sorted(steps)}")
         if steps:
-            self.step_dev.fill_(steps.pop())
+            n = steps.pop()
+            self.step_dev.fill_(n)
+            self.step_dev_b.fill_(n)
