@@ -236,13 +236,13 @@ class FusedAdamW(torch.optim.Optimizer):
         self.check_grads = True  # set False inside captured graphs (pointers are static)
         # update a side stream's parameter block on that stream (step); DFU_EARLY_ADAMW=0: off
         self.early_update = os.environ.get("DFU_EARLY_ADAMW", "1") != "0"
-        # the main stream's early block (DFU_EARLY_ADAMW_MAIN=0: off): the parameters whose
+        # the main stream's early block (DFU_EARLY_ADAMW_MAIN=1: on): the parameters whose
         # gradients the backward's own stream finishes first (the ResNet's deep stages: its
         # backward runs layer4 -> stem) are updated on an optimizer stream as soon as the last
         # of them is done (an event recorded by a grad-ready hook), beside the rest of that
         # backward instead of in the step's serial tail; learned from the previous step's
         # completion order.  Its AdamW reads its own step counter (step_dev_b, kept equal).
-        self.early_main = os.environ.get("DFU_EARLY_ADAMW_MAIN", "1") != "0"
+        self.early_main = os.environ.get("DFU_EARLY_ADAMW_MAIN", "0") != "0"
         self.step_dev_b = torch.zeros((), dtype=torch.int64, device=dev)
         self._pidx = {id(p): i for i, p in enumerate(self.flat.params)}
         self._order, self._seen = [], set()

@@ -74,7 +74,7 @@ def test_early_adamw_on_side_stream_is_bitwise_equal():
         fwd = lambda m, r, t: m(r, t)  # noqa: E731
         opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
         opt.early_update = early
-        opt.early_main = early
+        opt.early_main = early  # (default off: DFU_EARLY_ADAMW_MAIN)
         crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
         rgb, th, y = bench.synthetic(4, dev, seed=3)
         for _ in range(3):
