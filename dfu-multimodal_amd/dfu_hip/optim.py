@@ -244,6 +244,7 @@ class FusedAdamW(torch.optim.Optimizer):
         # completion order.  Its AdamW reads its own step counter (step_dev_b, kept equal).
         self.early_main = os.environ.get("DFU_EARLY_ADAMW_MAIN", "0") != "0"
         self.step_dev_b = torch.zeros((), dtype=torch.int64, device=dev)
+        self._b_valid = True  # step_dev_b == step_dev (not kept while the block is off)
         self._pidx = {id(p): i for i, p in enumerate(self.flat.params)}
         self._order, self._seen = [], set()
         self._trigger = None   # (param index, lo, hi) learned from a step's completion order
@@ -348,7 +349,7 @@ class FusedAdamW(torch.optim.Optimizer):
             tr = self._trigger
             if fp.params[tr[0]]._dfu_grad_stream == cur and (
                     early is None or tr[2] <= early[0] or tr[1] >= early[1]):
-                early_main = tr[1:]
+                early_main = tr[1:] if self._b_valid else None
         if early is not None:
             lo, hi, st = early
             with torch.cuda.stream(st):
@@ -368,7 +369,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 ops.step_increment(self.step_dev_b)
                 self._adamw(early_main[0], early_main[1], self.step_dev_b)
             cur.wait_stream(self._ost)
-        else:
+        elif self.early_main and self._b_valid:
             ops.step_increment(self.step_dev_b)
         Fn.join_grad_streams()
         if rebind:
@@ -387,6 +388,9 @@ class FusedAdamW(torch.optim.Optimizer):
         self._order, self._seen, self._trig_ev = [], set(), None
         for p in fp.params:
             p._dfu_grad_stream = None
+        if self.early_main and not self._b_valid:  # (re-)enabled: resync its step counter
+            self.step_dev_b.copy_(self.step_dev)
+        self._b_valid = self.early_main
         self.last_early_main = early_main
         self.last_early = None if early is None else early[:2]
         fp.shadows_rewritten(None if early is None or fp.t_jobs is None or not _EARLY_T
@@ -430,3 +434,4 @@ class FusedAdamW(torch.optim.Optimizer):
             n = steps.pop()
             self.step_dev.fill_(n)
             self.step_dev_b.fill_(n)
+            self._b_valid = self.early_main
