@@ -287,7 +287,7 @@ class _Beside:
 def grads_done(*params):
     for p in params:
         if p is not None:
-            for h in _grad_ready_hooks:
+            for h in tuple(_grad_ready_hooks):  # (a hook may be removed meanwhile: GC)
                 h(p)
 
 

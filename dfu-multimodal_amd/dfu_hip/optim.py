@@ -203,7 +203,7 @@ def _order_hook(wref):
     parameters' gradients and records the early main block's trigger event."""
     def hook(p):
         o = wref()
-        if o is None:
+        if o is None or not o.early_main:
             return
         i = o._pidx.get(id(p))
         if i is None or i in o._seen:
@@ -211,7 +211,7 @@ def _order_hook(wref):
         o._seen.add(i)
         o._order.append(i)
         t = o._trigger
-        if t is not None and i == t[0] and o.early_main:
+        if t is not None and i == t[0]:
             ev = torch.cuda.Event()
             ev.record()  # on the stream that produced the gradient (the current one)
             o._trig_ev = ev
@@ -255,7 +255,8 @@ class FusedAdamW(torch.optim.Optimizer):
         self._ost = None
         self.last_early_main = None
         if dev.type == "cuda":
-            Fn.register_grad_ready_hook(_order_hook(weakref.ref(self)))
+            hook = Fn.register_grad_ready_hook(_order_hook(weakref.ref(self)))
+            weakref.finalize(self, Fn.remove_grad_ready_hook, hook)
         self._dfu_joins_itself = True  # step() joins the gradient streams (functional)
         # the flat gradient buffer's autograd version at the last zero_grad / step: the kernels
         # write gradients through raw pointers (no bump), so a change means user code edited
