@@ -125,10 +125,11 @@ def cpu_baseline(config, threads, warmup=3, timed=10, B=8, sweep=True):
     """The oracle (plain PyTorch fp32, oracle/torch_ref.py) timed on the host cores on a bounded
     sample of the same workload, as BASELINE.md prescribes: the full train step (fwd + bwd +
     AdamW) at batch B, `warmup` untimed steps, then the median of `timed` steps.  `threads` is
-    the host's physical core count; with `sweep` one step is also timed at 1/2, 1/4 and 1/8 of
-    it and the fastest count is used (on the 2 x 64-core EPYC hosts all 128 threads ran the
-    step 6.6x SLOWER than 16: cross-socket traffic and oneDNN's per-op thread start-up at
-    batch 8), so the baseline is the best this host does, with every count tried reported."""
+    the host's physical core count; with `sweep` the count is halved until the step time rises
+    (best of two steps per count after a warm-up; on the 2 x 64-core EPYC hosts all 128 threads
+    ran the step 6.6x SLOWER than 16: cross-socket traffic and oneDNN's per-op thread start-up
+    at batch 8) and the fastest count is used -- an interior minimum of the sweep, so the
+    baseline is the best this host does, with every count tried reported."""
     import statistics
     from oracle import torch_ref as R
     torch.manual_seed(0)
@@ -153,14 +154,26 @@ def cpu_baseline(config, threads, warmup=3, timed=10, B=8, sweep=True):
         opt.step()
 
     tried = {}
-    cands = [threads] + ([t for t in (threads // 2, threads // 4, threads // 8) if t >= 1]
-                         if sweep else [])
-    for t in dict.fromkeys(cands):
+
+    def probe(t):
         torch.set_num_threads(t)
         step()  # warm this thread count
-        t0 = time.perf_counter()
-        step()
-        tried[t] = time.perf_counter() - t0
+        best = float("inf")
+        for _ in range(2):
+            t0 = time.perf_counter()
+            step()
+            best = min(best, time.perf_counter() - t0)
+        tried[t] = best
+
+    # halve the thread count from the physical cores until the step time rises (and at least
+    # once past the fastest count), so the count used is an interior minimum of the sweep
+    t = threads
+    probe(t)
+    while sweep and t > 1:
+        t //= 2
+        probe(t)
+        if tried[t] > min(tried.values()):
+            break
     use = min(tried, key=tried.get)
     torch.set_num_threads(use)
     for _ in range(warmup):
@@ -180,7 +193,8 @@ def cpu_baseline(config, threads, warmup=3, timed=10, B=8, sweep=True):
                       f"{sum(times):.1f} s) after {warmup} warm-up, "
                       f"torch.set_num_threads({use}), the fastest of {sorted(tried)} on a "
                       f"host with {cores.get('physical_cores', '?')} physical cores "
-                      f"(os.cpu_count() {cores['os_cpu_count']}; one step each)"}
+                      f"(os.cpu_count() {cores['os_cpu_count']}; best of two steps each, halved "
+                      f"until the time rose)"}
 
 
 def cpu_baseline_gradcam(threads, budget_s=10.0):
@@ -381,7 +395,8 @@ def main_gradcam(args, rank, world, dev):
                        "model": "resnet50+vit_base_patch16_224 late fusion",
                        "global_batch": args.batch * args.gpus, "per_gpu_batch": args.batch,
                        "image": 224, "parallelism": f"replicas{args.gpus}",
-                       "hip_graph": graph is not None, "graph_vs_eager_ms": choice or None},
+                       "hip_graph": graph is not None, "graph_vs_eager_ms": choice or None,
+                       "dist": args.dist},
             "roofline": {"bound": "mfma", "achieved": round(gr["achieved"], 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(gr["achieved"] / PEAK_BF16_TFLOPS, 4),
@@ -497,7 +512,7 @@ def main_pipeline(args, rank, world, dev):
                                    "RandomRotation(30) + ColorJitter (RGB, p 0.6) + RandomAffine "
                                    "(p 0.6) + ToTensor + Normalize, both modalities",
                        "per_gpu_batch": args.batch, "source": f"{W0}x{H0}",
-                       "parallelism": f"replicas{args.gpus}"},
+                       "parallelism": f"replicas{args.gpus}", "dist": args.dist},
             "pcie_inclusive_pairs_per_sec": round(incl, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
                          "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
@@ -607,12 +622,50 @@ class _Wrap(torch.nn.Module):
         return self.backbone(x)
 
 
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`--gpus N` (N > 1) without a launcher: this process, which has not touched the GPU
+    (torch.cuda.device_count() does not initialise it), starts the N ranks as ONE child
+    process -- torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1 -- and exits
+    with its status.  It never times one process and multiplies by N.  Fails (exit 2) when the
+    node has fewer than N GPUs, unless DFU_SHARE_DEVICE=1 (the gloo rehearsal that puts every
+    rank on device 0)."""
+    import subprocess
+    have = torch.cuda.device_count()
+    if have < n and os.environ.get("DFU_SHARE_DEVICE", "0") != "1":
+        print(f"[bench] --gpus {n} needs {n} GPUs, this node has {have}; not running "
+              f"(a one-process run is never reported as {n} GPUs)", file=sys.stderr)
+        sys.exit(2)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        launch_ranks(args.gpus)
     from dfu_hip import parallel
     rank, world, local = parallel.init_from_env()
-    if world > 1 and world != args.gpus:
-        args.gpus = world
+    if world != args.gpus:
+        print(f"[bench] rank {rank}: --gpus {args.gpus} but WORLD_SIZE {world}: the line would "
+              f"misreport the job; not running", file=sys.stderr)
+        sys.exit(2)
+    if world > 1 and dist.get_world_size() != args.gpus:
+        print(f"[bench] process group has {dist.get_world_size()} ranks, --gpus {args.gpus}",
+              file=sys.stderr)
+        sys.exit(2)
+    args.dist = {"ranks": world, "backend": dist.get_backend() if world > 1 else None,
+                 "device_count": torch.cuda.device_count(),
+                 "shared_device": os.environ.get("DFU_SHARE_DEVICE", "0") == "1"}
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     # per-rank torch seed (SURVEY §8e: the dropout RNG is seeded per rank; dfu_hip.nn.Dropout
@@ -758,7 +811,7 @@ def main():
                        "model": "resnet50+vit_base_patch16_224 late fusion",
                        "global_batch": args.batch * args.gpus, "per_gpu_batch": args.batch,
                        "image": 224, "parallelism": f"dp{args.gpus}",
-                       "hip_graph": graph is not None},
+                       "hip_graph": graph is not None, "dist": args.dist},
             "gpu_step_ms": {"median": round(pct(durs, 0.5), 3), "p10": round(pct(durs, 0.1), 3),
                             "p90": round(pct(durs, 0.9), 3), "basis": "HIP events after every "
                             "step of the timed window (rank 0)"},

@@ -13,10 +13,7 @@ namespace {
 // then a 16-way LDS reduction.  Per tile t (nb rows): sum sb and M2 qb -> sum of squares
 // qb + sb^2/nb.  fp64 sums of x and x^2 over <= 1e6 rows of bf16-scale values keep
 // var = E[x^2] - mean^2 exact to ~1e-12 relative, and the tile loop is independent adds.
-#ifndef DFU_FIN_WAVES
-#define DFU_FIN_WAVES 16  // (-DDFU_FIN_WAVES=n: A/B builds, tools/build_fin.sh)
-#endif
-constexpr int FIN_WAVES = DFU_FIN_WAVES;
+constexpr int FIN_WAVES = 16;  // (8 / 4 waves measured slower in the fusion step, round 3)
 
 // CPW channels per block: a wave's 64 lanes cover CPW channels x (64 / CPW) tile slots, so
 // narrow layers (C = 64 over up to 6272 stem tiles) spread their tile loop over more lanes.

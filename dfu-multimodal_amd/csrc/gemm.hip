@@ -41,12 +41,6 @@ int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: of
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
 const int g_wide_reduce = getenv("DFU_GEMM_WIDE_REDUCE") ? atoi(getenv("DFU_GEMM_WIDE_REDUCE")) : 1;
 int g_tail_split = 1;       // dfu_gemm_set_tail_split
-// DFU_GEMM_SPLIT_DIV=d: tuned split-K counts divided by d (A/B: fewer fp32 slabs and reduce
-// traffic against longer weight-gradient GEMMs)
-const int g_split_div = getenv("DFU_GEMM_SPLIT_DIV") ? atoi(getenv("DFU_GEMM_SPLIT_DIV")) : 1;
-// DFU_GEMM_SLOT_CAP=c: a persistent launch holds at most c CUs' worth of workgroups (A/B: leave
-// CUs to the other encoder stream of the fusion step instead of waiting for all of them)
-const int g_slot_cap = getenv("DFU_GEMM_SLOT_CAP") ? atoi(getenv("DFU_GEMM_SLOT_CAP")) : kCUs;
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
@@ -85,8 +79,7 @@ const TunedPlan kTuned[] = {
 
 const TunedPlan* find_tuned(const dfu_gemm_desc* d) {
   const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
-  // the BN-statistics dgrad runs the tile its plain-bf16 twin was tuned to
-  const int epi = d->epilogue == DFU_EPI_BF16_DSTATS ? DFU_EPI_BF16 : d->epilogue;
+  const int epi = d->epilogue;
   for (const TunedPlan& t : kTuned) {
     if (t.a != d->a_mode || t.b != d->b_mode || t.e != epi || t.M != d->M ||
         t.N != d->N || t.K != d->K)
@@ -108,7 +101,6 @@ Plan plan_gemm(const dfu_gemm_desc* d) {
       pl.tile = tp->tile - 1;
       pl.entry = find_entry(d->a_mode, d->b_mode, d->epilogue, pl.tile);
       pl.split = acc_epi ? tp->split : 1;
-      if (g_split_div > 1 && pl.split > 1) pl.split = (pl.split + g_split_div - 1) / g_split_div;
       pl.cost = 0.0;
       if (pl.entry) return pl;
     }
@@ -410,12 +402,9 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
     DFU_CHECK_ARG(d->ldb >= round8(d->N), "dfu_gemm: MN-major B needs ldb >= round8(N)");
   if (d->epilogue == DFU_EPI_BF16_STATS || d->epilogue == DFU_EPI_F32_STATS)
     DFU_CHECK_ARG(d->stats != nullptr, "dfu_gemm: STATS epilogue needs a stats slab");
-  if (d->epilogue == DFU_EPI_BF16_DSTATS) {
-    DFU_CHECK_ARG(d->stats != nullptr && d->aux != nullptr && d->bn_coef != nullptr &&
-                      d->ldaux >= d->N,
-                  "dfu_gemm: DSTATS epilogue needs a stats slab, aux (y) and bn_coef");
-    DFU_CHECK_ARG(d->a_mode != DFU_OPND_CONV_DGRAD || d->conv_stride == 1,
-                  "dfu_gemm: DSTATS epilogue on a strided dgrad is not supported");
+  if (d->epilogue == DFU_EPI_BF16_DSTATS) {  // retired in round 4 (measured slower); reserved
+    dfu_set_error("dfu_gemm: the DSTATS epilogue is retired");
+    return DFU_E_UNSUPPORTED;
   }
 
   const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
@@ -499,7 +488,6 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   a.aux = d->aux; a.ldaux = d->ldaux;
   a.aux_out = d->aux_out; a.ldaux_out = d->ldaux_out;
   a.stats = d->stats;
-  a.bn_coef = d->bn_coef;
   a.split = splits;
   a.n4 = (d->N % 4 == 0 && d->ldc % 4 == 0 && (d->aux == nullptr || d->ldaux % 4 == 0) &&
           (d->aux_out == nullptr || d->ldaux_out % 4 == 0))
@@ -578,7 +566,7 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   // Persistent schedule: at most one wave of workgroups (CUs x occupancy), each walking its
   // work units as one K-step stream; split-K by fp32 atomics (no workspace) keeps one unit
   // per workgroup (its atomics have no fixed vmcnt count).
-  const int slots = (g_slot_cap > 0 && g_slot_cap < kCUs ? g_slot_cap : kCUs) * kOcc[pl.tile];
+  const int slots = kCUs * kOcc[pl.tile];
   a.tail_full = a.tail_r = a.tail_s = a.tail_kps = 0;
   a.tslab = nullptr;
   if (!acc_epi && splits == 1 && kTailOK[pl.tile]) {

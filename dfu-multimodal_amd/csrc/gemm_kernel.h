@@ -80,7 +80,6 @@ struct GemmArgs {
   // round.  Each split stores its fp32 accumulators to tslab; the last to arrive on the tile's
   // counter sums the slabs in split order and runs the normal epilogue.
   int tail_full, tail_r, tail_s, tail_kps;
-  const float* bn_coef;  // DFU_EPI_BF16_DSTATS: [4][N] scale, shift, mean, invstd
   float* tslab;  // [tail_s][tail_r][FM*FN][threads] f32x4, lane-linear
   int n4;       // N and every leading dimension % 4 == 0: one vector access per 4 columns
   int n8;       // N, ldc (, ldaux_out) % 8 == 0 and 16-B aligned bf16 outputs: paired stores
@@ -536,8 +535,7 @@ template <int EPI, class T>
 DFU_DEV int epi_stores(const GemmArgs& p) {
   constexpr bool bf16_out = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU ||
                             EPI == DFU_EPI_BF16_GELU || EPI == DFU_EPI_BF16_DGELU ||
-                            EPI == DFU_EPI_BF16_ADD || EPI == DFU_EPI_BF16_STATS ||
-                            EPI == DFU_EPI_BF16_DSTATS;
+                            EPI == DFU_EPI_BF16_ADD || EPI == DFU_EPI_BF16_STATS;
   const int per = bf16_out && p.n8 ? T::FM * T::FN / 2 : T::FM * T::FN * (p.n4 ? 1 : 4);
   if constexpr (EPI == DFU_EPI_BF16_GELU) return 2 * per;
   if constexpr (EPI == DFU_EPI_F32_ACC)
@@ -679,8 +677,7 @@ DFU_DEV bool tail_reduce(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int v, f
 // Each lane's 4 columns of fragment (i, j) as two packed bf16 pairs.
 template <int EPI, class T>
 constexpr bool aux_prefetch() {
-  return (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD || EPI == DFU_EPI_BF16_DSTATS) &&
-         T::FM * T::FN <= 16;
+  return (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) && T::FM * T::FN <= 16;
 }
 template <class T>
 struct AuxPre {
@@ -701,8 +698,7 @@ DFU_DEV void aux_load(const GemmArgs& p, int m0, int n0, int tid, AuxPre<T>& pre
     const int m = m0 + wr * T::WTM + 16 * i + lrow;
     const bool okm = m < p.M;
     const int mc = okm ? m : 0;
-    const int64_t mo = (EPI != DFU_EPI_BF16_DSTATS && AMODE == DFU_OPND_CONV_DGRAD)
-                           ? out_row(p, mc) : (int64_t)mc;
+    const int64_t mo = AMODE == DFU_OPND_CONV_DGRAD ? out_row(p, mc) : (int64_t)mc;
 #pragma unroll
     for (int j = 0; j < T::FN; ++j) {
       const int n = n0 + wc * T::WTN + 16 * j + lcol;
@@ -828,96 +824,6 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
         }
       }
     }
-  } else if constexpr (EPI == DFU_EPI_BF16_DSTATS) {
-    // BatchNorm backward statistics of the gradient this dgrad produces (bn.hip
-    // k_bn_bwd_reduce, relu mode 2, per 128-row tile instead of per row-block): g = bf16(acc)
-    // is stored unmasked (the BN apply masks it again); the sums use g' = g where the forward's
-    // pre-ReLU fma(y, scale, shift) > 0, and x̂ = (y - mean) invstd, y = aux (bf16).
-    // Per wave in registers (each lane's 4 columns' coefficients by one vector load per
-    // array: the epilogue loads y anyway), then the WGM row-waves of each 128-row block summed
-    // in LDS, records stored before the tile.
-    const int n0w = n0 + wc * WTN;
-    const rsrc_t rcf = make_rsrc(p.bn_coef);
-    float sc[FN][4], sf[FN][4], mu[FN][4], is[FN][4];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0w + 16 * j + lcol;
-      ld4_f32(rcf, n, true, n, N, n4, sc[j]);
-      ld4_f32(rcf, (int64_t)N + n, true, n, N, n4, sf[j]);
-      ld4_f32(rcf, (int64_t)2 * N + n, true, n, N, n4, mu[j]);
-      ld4_f32(rcf, (int64_t)3 * N + n, true, n, N, n4, is[j]);
-    }
-    const rsrc_t ra = make_rsrc(p.aux);
-    float sg[FN][4], sx[FN][4];
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sg[j][r] = sx[j][r] = 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wr * WTM + 16 * i + lrow;
-      const bool okm = m < M;
-      const int mc = okm ? m : 0;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0w + 16 * j + lcol;
-        float y[4];
-        if constexpr (kPre)
-          unpack4(pre.v[i][j], y);
-        else
-          ld4_bf16(ra, (int64_t)mc * p.ldaux + n, okm, n, N, n4, y);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = bf2f(f2bf(acc[i][j][r] * p.alpha));
-          acc[i][j][r] = g;
-          const float gm = (okm && (fmaf(y[r], sc[j][r], sf[j][r]) + 0.f) > 0.f) ? g : 0.f;
-          sg[j][r] += gm;
-          sx[j][r] += gm * (y[r] - mu[j][r]) * is[j][r];
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float a = row16_sum(sg[j][r]), b = row16_sum(sx[j][r]);
-        if (lrow == 0) {
-          const int c = wc * WTN + 16 * j + lcol + r;
-          red[(wr * TN + c) * 2 + 0] = a;
-          red[(wr * TN + c) * 2 + 1] = b;
-        }
-      }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const rsrc_t rs = make_rsrc(p.stats);
-    constexpr int HALVES = TM / 128;
-    for (int idx = tid; idx < TN * HALVES; idx += T::NT) {
-      const int c = idx % TN, h = idx / TN;
-      const int n = n0 + c;
-      float S = 0.f, Q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WGM; ++w) {
-        if ((w * WTM) / 128 != h) continue;
-        S += red[(w * TN + c) * 2 + 0];
-        Q += red[(w * TN + c) * 2 + 1];
-      }
-      const bool ok = n < N && m0 + 128 * h < M;
-      const int64_t blk = m0 / 128 + h;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(S), rs,
-                                            boff(ok, ((blk * 2 + 0) * N + n) * 4), 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(Q), rs,
-                                            boff(ok, ((blk * 2 + 1) * N + n) * 4), 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wr * WTM + 16 * i + lrow;
-      float v[FN][4];
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[j][r] = acc[i][j][r];
-      st_row_bf16<FN>(rc, (int64_t)m * p.ldc, m < M, n0w, N, p.n8, n4, lane, v);
-    }
   } else {
     constexpr bool kBias = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_RELU || EPI == DFU_EPI_F32 ||
                            EPI == DFU_EPI_F32_RESID || EPI == DFU_EPI_BF16_GELU ||
@@ -1029,8 +935,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   using T = Tile<TM, TN, OCC, NST, NW>;
   constexpr int WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
   constexpr int FM = T::FM, FN = T::FN, NSTAGE = T::NSTAGE;
-  constexpr int SCRATCH = (EPI == DFU_EPI_BF16_STATS || EPI == DFU_EPI_F32_STATS ||
-                           EPI == DFU_EPI_BF16_DSTATS)
+  constexpr int SCRATCH = (EPI == DFU_EPI_BF16_STATS || EPI == DFU_EPI_F32_STATS)
                               ? T::STATS_BYTES
                               : 16;  // stats / flag
   // ALL LDS in one array: a second __shared__ object can make hipcc drain the DMA per K-step

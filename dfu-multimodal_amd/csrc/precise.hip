@@ -87,38 +87,6 @@ __global__ void k_split_x3(const float* __restrict__ in, int64_t ld_in, int rows
   }
 }
 
-// Many splits as one launch (dfu_split_x3_batch: the bf16x3 weight operands of every weight an
-// encoder uses, re-derived once per optimizer step).  Jobs in a device table; job j owns the
-// 8-column vectors [v0_j, v0_j + rows_j * seg_j / 8) of the launch, found by binary search.
-struct SplitJob {
-  const float* in;
-  bf16_t* out;
-  int64_t ld_in;
-  int64_t v0;
-  int32_t rows, cols, seg, pattern;
-};
-static_assert(sizeof(SplitJob) == 48, "dfu_split_job layout (include/dfu_hip.h)");
-
-__global__ void k_split_x3_batch(const SplitJob* __restrict__ jobs, int njobs, int64_t nvec) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    int lo = 0, hi = njobs - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (jobs[mid].v0 <= i) lo = mid; else hi = mid - 1;
-    }
-    const SplitJob& j = jobs[lo];
-    const int cv = j.seg / 8;
-    const int64_t li = i - j.v0;
-    const int64_t r = li / cv;
-    const int c = (int)(li - r * cv) * 8;
-    float f[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = c + e < j.cols ? j.in[r * j.ld_in + c + e] : 0.f;
-    st_triple8(j.out + r * 3 * j.seg, j.seg, c, f, j.pattern);
-  }
-}
-
 // fp32 OIHW conv weight -> bf16 KRSC' (C' = 3C, pattern B: [hi | hi | lo] along channels).
 __global__ void k_pack_conv_weight_x3(const float* __restrict__ w, bf16_t* __restrict__ out, int K,
                                       int C, int R, int S) {
@@ -334,14 +302,6 @@ extern "C" int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_
   if (n == 0) return DFU_OK;
   hipLaunchKernelGGL(k_split_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, in, ld_in,
                      rows, cols, seg, (bf16_t*)out, pattern, (bf16_t*)hi_out, ld_hi);
-  DFU_LAUNCH_CHECK();
-  return DFU_OK;
-}
-
-extern "C" int dfu_split_x3_batch(const void* jobs, int32_t njobs, int64_t nvec, void* stream) {
-  DFU_CHECK_ARG(jobs && njobs > 0 && nvec > 0, "dfu_split_x3_batch: bad args");
-  hipLaunchKernelGGL(k_split_x3_batch, dim3(nblocks(nvec)), dim3(TPB), 0, (hipStream_t)stream,
-                     (const SplitJob*)jobs, njobs, nvec);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

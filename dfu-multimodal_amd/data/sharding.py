@@ -11,7 +11,8 @@ same number of batches (the gradient all-reduce pairs collectives across ranks),
     seed + epoch, so it changes per epoch as the reference's global-RNG draw does), pads it
     by wrapping to a multiple of world_size, and keeps positions rank, rank + world, ...  The
     union of the shards is the single-rank draw (plus the wrapped padding).
-  * ShardedSequentialSampler: the val / test order (0 .. n-1) split the same way.
+  * ShardedSequentialSampler: the val / test order (0 .. n-1) split by whole batches, no
+    padding (every sample once; evaluate() restores the reference's order).
 
 `set_epoch(e)` mirrors torch.utils.data.DistributedSampler.
 """
@@ -57,21 +58,40 @@ class ShardedWeightedSampler(torch.utils.data.Sampler):
 
 
 class ShardedSequentialSampler(torch.utils.data.Sampler):
-    """0 .. n-1 sharded over ranks (wrap-padded to equal length): the val / test loaders."""
+    """0 .. n-1 sharded over ranks by whole batches, without padding: the val / test loaders.
 
-    def __init__(self, n, rank=0, world_size=1):
+    The single-process loader walks batches [0, B), [B, 2B), ... (the last one possibly short);
+    rank r takes batches r, r + world, ...  So every sample is evaluated exactly once, every
+    rank's batches are batches of the single-process run (the union of the ranks' batch losses
+    and confusion counts is the single-process one, with batch_size = the loader's), and
+    ``global_indices()`` tells evaluate() how to put the gathered per-rank rows back in the
+    reference's order.  Ranks may run different numbers of batches (eval has no per-batch
+    collective)."""
+
+    def __init__(self, n, rank=0, world_size=1, batch_size=1):
         if world_size < 1 or not 0 <= rank < world_size:
             raise ValueError(f"rank {rank} of world {world_size}")
-        self.n, self.rank, self.world = int(n), rank, world_size
+        if batch_size < 1:
+            raise ValueError(f"batch_size {batch_size}")
+        self.n, self.rank, self.world, self.batch_size = int(n), rank, world_size, int(batch_size)
 
     def set_epoch(self, epoch):
         pass
 
+    def indices_of(self, rank):
+        B = self.batch_size
+        nb = (self.n + B - 1) // B
+        return [i for j in range(rank, nb, self.world) for i in range(j * B, min(self.n, (j + 1) * B))]
+
+    def global_indices(self):
+        """The sample index of every row of the rank-order concatenation of all shards."""
+        return [i for r in range(self.world) for i in self.indices_of(r)]
+
     def __iter__(self):
-        return iter(_shard(list(range(self.n)), self.rank, self.world))
+        return iter(self.indices_of(self.rank))
 
     def __len__(self):
-        return math.ceil(self.n / self.world)
+        return len(self.indices_of(self.rank))
 
 
 def dp_rank_world(group=None):

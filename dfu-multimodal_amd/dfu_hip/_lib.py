@@ -52,7 +52,7 @@ class GemmDesc(ctypes.Structure):
         ("tile", c_int32),
         ("workspace", c_void_p), ("workspace_bytes", c_int64),
         ("tile_counters", c_void_p), ("tile_counters_len", c_int32),
-        ("bn_coef", c_void_p),
+        ("operand_type", c_int32),
     ]
 
 
@@ -142,7 +142,6 @@ PROTOTYPES = {
     "dfu_softmax_rows": [P, I32, I32, P, P],
     "dfu_metrics_accumulate": [P, P, I32, I32, P, P, P, P, P],
     "dfu_split_x3": [P, I64, I32, I32, I32, P, I32, P, I64, P],
-    "dfu_split_x3_batch": [P, I32, I64, P],
     "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, P],
     "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],
     "dfu_patchify_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],

@@ -39,12 +39,17 @@ F32 = torch.float32
 #   stay fp32 between kernels and attention runs in fp32, so the fusion logits meet north_star's
 #   "within 1e-3 abs of the reference CPU path" against the fp32 oracle.  The backward pass is
 #   the bf16 one (it reads the plain bf16 tensors the split kernels also write).
-PRECISIONS = ("bf16", "bf16x3")
+# "mixed": per stage -- a ResNet Bottleneck / ViT Block (or the ResNet module itself, for the
+#   stem) whose ``dfu_precision`` attribute is "bf16" runs the bf16 forward, every other stage
+#   the bf16x3 one (models.precision.apply_policy sets the attributes; a bf16 stage's output
+#   enters the next bf16x3 stage as an exact bf16 value, a bf16x3 stage's output reaches a bf16
+#   stage as the bf16 copy it also writes).
+PRECISIONS = ("bf16", "bf16x3", "mixed")
 _precision = ["bf16"]
 
 
 def set_precision(mode):
-    """Select the forward precision ("bf16" or "bf16x3"); returns the previous mode."""
+    """Select the forward precision ("bf16", "bf16x3" or "mixed"); returns the previous mode."""
     if mode not in PRECISIONS:
         raise ValueError(f"precision must be one of {PRECISIONS}, got {mode!r}")
     old = _precision[0]
@@ -72,8 +77,12 @@ class precision:
         return False
 
 
-def _x3():
-    return _precision[0] == "bf16x3"
+def _x3(mod=None):
+    """Does the stage `mod` (None: a stage without a policy of its own) run bf16x3?"""
+    p = _precision[0]
+    if p == "mixed":
+        return getattr(mod, "dfu_precision", None) != "bf16"
+    return p == "bf16x3"
 
 # ------------------------------------------------------------------------- grad plumbing
 _grad_ready_hooks = []
@@ -156,6 +165,19 @@ def join_grad_streams(stream=None, clear=True):
 # enqueued.  Optimizers joined through join_grad_streams anyway (FusedAdamW, GradAllReducer)
 # see no extra wait; any other torch.optim optimizer also joins in a step pre-hook.
 _join_armed = [False]
+_backward_end_hooks = []
+
+
+def register_backward_end_hook(fn):
+    """fn() is called when a backward pass through the HIP encoders has ended (the engine's
+    final callback, after every node ran)."""
+    _backward_end_hooks.append(fn)
+    return fn
+
+
+def remove_backward_end_hook(fn):
+    if fn in _backward_end_hooks:
+        _backward_end_hooks.remove(fn)
 
 
 def arm_backward_join():
@@ -167,6 +189,8 @@ def arm_backward_join():
     def _join():
         _join_armed[0] = False
         join_grad_streams(target, clear=False)
+        for fn in list(_backward_end_hooks):
+            fn()
     try:
         torch.autograd.Variable._execution_engine.queue_callback(_join)
     except RuntimeError:  # not inside a backward pass (a direct .backward() call of a Function)
@@ -186,15 +210,9 @@ except ImportError:  # torch without global optimizer hooks
 
 
 _side_streams = {}
-# HIP stream priorities of the side streams (torch: lower = higher priority).  Default 0 (the
-# streams' default).  DFU_SIDE_STREAM_PRIORITY=-1 runs the concurrent ViT branch at high
-# priority: in the eager fusion step that measured 18.57-18.61 vs 18.64-18.66 ms per step (within
-# 0.3%), but a C5 Grad-CAM step whose warm-up ran with the priority -1 side stream replayed from
-# a HIP graph at 49.6-54.4 ms against 22.9 ms with priority 0 everywhere -- even with the capture
-# itself on priority-0 streams -- so the default keeps one priority for every stream.
-# DFU_WGRAD_STREAM_PRIORITY: the ViT weight-gradient stream (default 0).
-_SIDE_PRIO = int(os.environ.get("DFU_SIDE_STREAM_PRIORITY", "0"))
-_WGRAD_PRIO = int(os.environ.get("DFU_WGRAD_STREAM_PRIORITY", "0"))
+# Every library stream runs at the default HIP priority: a high-priority ViT side stream gained
+# 0.3% in the eager fusion step, but a C5 Grad-CAM step whose warm-up ran with it replayed from
+# a HIP graph at 49.6-54.4 ms against 22.9 ms (round 3).
 
 
 def new_stream(idx, priority=0):
@@ -209,15 +227,13 @@ def new_stream(idx, priority=0):
 
 
 def side_stream(device):
-    """One persistent side stream per device for the concurrent encoder branch (at
-    DFU_SIDE_STREAM_PRIORITY; under HIP graph capture always at the default priority)."""
+    """One persistent side stream per device for the concurrent encoder branch."""
     idx = torch.device(device).index
     if idx is None:
         idx = torch.cuda.current_device()
-    prio = 0 if torch.cuda.is_current_stream_capturing() else _SIDE_PRIO
-    st = _side_streams.get((idx, prio))
+    st = _side_streams.get(idx)
     if st is None:
-        st = _side_streams[(idx, prio)] = new_stream(idx, prio)
+        st = _side_streams[idx] = new_stream(idx)
     return st
 
 
@@ -234,22 +250,13 @@ def wgrad_stream(device):
     idx = torch.device(device).index
     if idx is None:
         idx = torch.cuda.current_device()
-    prio = 0 if torch.cuda.is_current_stream_capturing() else _WGRAD_PRIO  # see side_stream
-    st = _wgrad_streams.get((idx, prio))
+    st = _wgrad_streams.get(idx)
     if st is None:
-        st = _wgrad_streams[(idx, prio)] = new_stream(idx, prio)
+        st = _wgrad_streams[idx] = new_stream(idx)
     return st
 
 
-# DFU_RESNET_WGRAD_STREAM=1: the bottleneck weight-gradient GEMMs run on the wgrad stream when
-# the ResNet runs alone (A/B; off: RGB-only 10.0-11.9 vs 9.1-10.2 ms per step, same box -- the
-# conv wgrads are not small gap-fillers, they compete with the input-gradient chain)
-_RESNET_WGRAD_STREAM = os.environ.get("DFU_RESNET_WGRAD_STREAM", "0") != "0"
-
 _concurrent_encoders = [0]
-# DFU_VIT_WGRAD_BESIDE_FUSED=1: the ViT weight gradients run on the wgrad stream also while the
-# ResNet branch runs concurrently (A/B; default: inline on the ViT's own stream there)
-_WGRAD_BESIDE_FUSED = os.environ.get("DFU_VIT_WGRAD_BESIDE_FUSED", "0") != "0"
 
 
 class concurrent_encoders:
@@ -417,67 +424,9 @@ def conv_weight_bf16(w):
     return ops.pack_conv_weight(w.detach())
 
 
-# bf16x3 weight operands ([hi | hi | lo] rows) are cached per parameter and re-derived, after
-# the weights change, for every weight of a stream's group in ONE launch (ops.SplitJobs): the
-# group is the set of weights first split on that stream (an encoder's), so the first stale
-# weight an encoder asks for in a step refreshes all of its weights at once instead of one
-# launch per layer.  Off by default (DFU_X3_WEIGHT_CACHE=1 enables it): the bf16x3 fusion step
-# measured 26.87-26.94 ms with it against 26.76-26.85 ms without (same box) -- the one batched
-# refresh sits at the head of each encoder stream, while the per-layer splits overlap the other
-# stream's work.
-_X3_CACHE = os.environ.get("DFU_X3_WEIGHT_CACHE", "0") != "0"
-_x3_groups = {}  # raw stream -> _X3Group
-
-
-def _x3_key(w):
-    """Changes whenever w's values may have: an in-place edit (version counter) or a FusedAdamW
-    step or refresh (its FlatParams generation: kernel writes do not bump the version)."""
-    flat = getattr(w, "_dfu_flat", None)
-    return (w._version, flat.gen if flat is not None else None)
-
-
-class _X3Group:
-    def __init__(self, stream):
-        self.stream = stream
-        self.params = []
-        self.jobs = None
-
-    def add(self, w):
-        # (the table is rebuilt here, on first use -- the first step -- not in a refresh, which
-        # may run under a graph capture)
-        self.params.append(w)
-        self.jobs = ops.SplitJobs([(p.detach().reshape(p.shape[0], -1), p._dfu_x3w[0], ops.X3_B)
-                                   for p in self.params])
-
-    def refresh(self):
-        self.jobs.launch()
-        for w in self.params:
-            w._dfu_x3w[2] = _x3_key(w)
-
-
 def weight_x3_rows(w, seg=None):
     """fp32 [N, K...] parameter -> bf16x3 GEMM B operand [N, 3 seg] = [hi | hi | lo]."""
-    w2 = w.detach().reshape(w.shape[0], -1)
-    if not (_X3_CACHE and w.is_cuda and w2.stride(1) == 1):
-        return ops.split_x3(w2, ops.X3_B, seg=seg)
-    seg = (w2.shape[1] + 7) // 8 * 8 if seg is None else int(seg)
-    ent = getattr(w, "_dfu_x3w", None)
-    st = ops.stream_ptr().value
-    if ent is None:
-        grp = _x3_groups.get(st)
-        if grp is None:
-            grp = _x3_groups[st] = _X3Group(st)
-        buf = ops.split_x3(w2, ops.X3_B, seg=seg)
-        w._dfu_x3w = [buf, seg, _x3_key(w), grp]
-        grp.add(w)
-        return buf
-    if ent[1] != seg or ent[3].stream != st:
-        # another padding, or another stream than its group's (whose refreshes would race with
-        # this use): a split of its own
-        return ops.split_x3(w2, ops.X3_B, seg=seg)
-    if ent[2] != _x3_key(w):
-        ent[3].refresh()
-    return ent[0]
+    return ops.split_x3(w.detach().reshape(w.shape[0], -1), ops.X3_B, seg=seg)
 
 
 def conv_weight_x3(w):
@@ -510,8 +459,7 @@ class _BN:
         self.bn = bn
         self.M, self.C = M, C
         self.training = bn.training or not bn.track_running_stats
-        # one [4][C] block (rows scale, shift, mean, invstd): the DSTATS dgrad epilogue's
-        # bn_coef operand (include/dfu_hip.h DFU_EPI_BF16_DSTATS)
+        # one [4][C] block: rows scale, shift, mean, invstd
         self.coef4 = _empty((4, C), F32, device)
         self.scale, self.shift, self.mean, self.invstd = self.coef4.unbind(0)
 
@@ -544,17 +492,6 @@ class _BN:
                    shift=self.shift)
         grads_done(bn.weight, bn.bias)
 
-    def backward_from_dstats(self, dstats, dout, y, dy):
-        """BN + ReLU (no residual) backward whose reduction already ran in the epilogue of the
-        dgrad that produced `dout` (conv_dgrad(..., bn=self)): finalize + apply only."""
-        bn = self.bn
-        dgamma = grad_buffer(bn.weight) if _wants(bn.weight) else None
-        dbeta = grad_buffer(bn.bias) if _wants(bn.bias) else None
-        ops.bn_bwd_finish(dstats, dstats.shape[0], dout, y, None, 2, self.mean, self.invstd,
-                          bn.weight, self.M, self.C, dy, None, dgamma, dbeta,
-                          batch_stats=self.training, scale=self.scale, shift=self.shift)
-        grads_done(bn.weight, bn.bias)
-
 
 # --------------------------------------------------------------------------- conv helpers
 def conv_fwd(x_rows, geom, w_krsc, y, stats):
@@ -585,44 +522,34 @@ def conv_fwd_x3(x3_rows, geom, w3, y, stats):
                  epilogue=L.EPI_F32_STATS, stats=stats, conv=g3)
 
 
-def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, bn=None, y=None, w_flip=None, w_t=None):
-    """dx[N*H*W, C] = dgrad(dy) (+ add, bf16).  With bn (a _BN whose input y is this conv's
-    input, BN + ReLU without residual; stride 1): the epilogue also reduces that BN's
-    backward sums over dx (DFU_EPI_BF16_DSTATS); returns the [tiles][2][C] records for
-    _BN.backward_from_dstats.  With w_flip (conv_weight_flipped; stride 1, no add, no bn): dx
-    is the forward convolution of dy (K input channels, pad R-1-pad) with the flipped weight.
-    With w_t (conv1x1_weight_T; a 1x1 stride-1 conv, no bn): dx = dy W as a K-contiguous GEMM
+def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, w_flip=None, w_t=None):
+    """dx[N*H*W, C] = dgrad(dy) (+ add, bf16).  With w_flip (conv_weight_flipped; stride 1, no
+    add): dx is the forward convolution of dy (K input channels, pad R-1-pad) with the flipped
+    weight.  With w_t (conv1x1_weight_T; a 1x1 stride-1 conv): dx = dy W as a K-contiguous GEMM
     on the transposed [C][K] weight."""
     g = geom
     Mx = g.n * g.h * g.w
-    if (w_t is not None and bn is None and g.r == 1 and g.s == 1 and g.stride == 1
-            and g.pad == 0):
+    if w_t is not None and g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
         ops.gemm(Mx, g.c, g.k, dy_rows, g.k, w_t, g.k, dx, g.c,
                  epilogue=L.EPI_BF16_ADD if add is not None else L.EPI_BF16, aux=add,
                  ldaux=g.c if add is not None else 0)
-        return None
-    if w_flip is not None and add is None and bn is None and g.stride == 1:
+        return
+    if w_flip is not None and add is None and g.stride == 1:
         gd = ops.ConvGeom(g.n, g.p, g.q, g.k, g.c, g.r, g.s, 1, g.r - 1 - g.pad)
         if (gd.p, gd.q) == (g.h, g.w) and g.r - 1 - g.pad >= 0:
             K = g.r * g.s * g.k
             ops.gemm(Mx, g.c, K, dy_rows, 0, w_flip, K, dx, g.c, a_mode=L.OPND_CONV_FWD,
                      epilogue=L.EPI_BF16, conv=gd)
-            return None
+            return
     epi = L.EPI_BF16_ADD if add is not None else L.EPI_BF16
-    aux, ld_aux, stats = add, (g.c if add is not None else 0), None
-    if bn is not None:
-        assert add is None and g.stride == 1 and y is not None and y.shape == (Mx, g.c)
-        epi, aux, ld_aux = L.EPI_BF16_DSTATS, y, g.c
-        stats = _empty((ops.stats_tiles(Mx), 2, g.c), F32, dx.device)
-    coef = bn.coef4 if bn is not None else None
+    aux, ld_aux = add, (g.c if add is not None else 0)
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
         ops.gemm(Mx, g.c, g.k, dy_rows, g.k, w_krsc, g.c, dx, g.c, b_mode=L.OPND_MNMAJOR,
-                 epilogue=epi, aux=aux, ldaux=ld_aux, stats=stats, bn_coef=coef)
+                 epilogue=epi, aux=aux, ldaux=ld_aux)
     else:
         ops.gemm(Mx, g.c, g.r * g.s * g.k, dy_rows, 0, w_krsc, g.r * g.s * g.c, dx, g.c,
                  a_mode=L.OPND_CONV_DGRAD, b_mode=L.OPND_CONV_DGRAD_W, epilogue=epi, aux=aux,
-                 ldaux=ld_aux, conv=g, stats=stats, bn_coef=coef)
-    return stats
+                 ldaux=ld_aux, conv=g)
 
 
 def conv_wgrad(dy_rows, x_rows, geom, dw):
@@ -670,7 +597,7 @@ class StemFn(torch.autograd.Function):
         xf = x.detach().float() if x.dtype != F32 else x.detach()
         wb = weight_bf16_rows(w, ld=Kp)
         Cout = w.shape[0]
-        x3 = _x3()
+        x3 = _x3(mod)
         if x3:
             col, P, Q = ops.im2col_f32_x3(xf, R, S, st, pad, Kp)  # [M][3 Kp] triple
         else:
@@ -750,25 +677,13 @@ def _fire_grad_hooks(probe, grad):
         hook(grad)
 
 
-# BN + ReLU backward sums of bn1 / bn2 in the epilogue of the dgrad producing their output
-# gradient (DFU_EPI_BF16_DSTATS) instead of a separate dfu_bn_bwd_reduce pass, for BNs of at
-# least FUSE_BN_DSTATS_MIN_C channels (tools/dstats_time.py on MI355X: layer3's 12544 x 256
-# dgrads gain ~4 us net, layer1's 200704 x 64 ones lose ~5 us: their many small-N tiles pay
-# the epilogue's VALU work more than the separate 13 us pass costs).  Off by default: in the
-# two-stream fusion step every threshold measured slower (20.70-20.76 ms vs 20.62 ms per step,
-# same box), the longer dgrads delaying the ResNet stream more than the small reduce passes
-# that overlap the ViT stream.  DFU_FUSE_BN_DSTATS=1 enables it.
-FUSE_BN_DSTATS = os.environ.get("DFU_FUSE_BN_DSTATS", "0") != "0"
-FUSE_BN_DSTATS_MIN_C = int(os.environ.get("DFU_FUSE_BN_DSTATS_MIN_C", "128"))
-
-
 class BottleneckFn(torch.autograd.Function):
     """torchvision Bottleneck: relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1 x))))))) + id)."""
 
     @staticmethod
     def forward(ctx, x, *params_and_mod):
         mod = params_and_mod[-1]
-        x3mode = _x3()
+        x3mode = _x3(mod)
         xin3 = _take_x3(x) if x3mode else None
         x = nhwc_bf16(x.detach())
         B, Cin, H, W = x.shape
@@ -849,9 +764,6 @@ class BottleneckFn(torch.autograd.Function):
             y3, out, s3 = conv_bn(a2, g3, w3, mod.bn3, True, residual=idn, mask=mask3)
         ctx.x3 = x3mode
         ctx.mod = mod
-        # weight gradients beside the input-gradient chain when the ResNet runs alone (as the ViT
-        # blocks'; inside the two-stream fusion step the other encoder fills the idle CUs)
-        ctx.beside = _RESNET_WGRAD_STREAM and _concurrent_encoders[0] == 0
         ctx.geo = (g1, g2, g3, gd)
         ctx.bns = (s1, s2, s3, sd)
         ctx.shape = (B, Cin, H, W)
@@ -883,18 +795,11 @@ class BottleneckFn(torch.autograd.Function):
         dev = xr.device
         g = rows_view(nhwc_bf16(gout))
         M1, M2 = y1.shape[0], y3.shape[0]
-        convs = (mod.conv1, mod.conv2, mod.conv3) + (
-            (mod.downsample[0],) if mod.downsample is not None else ())
-        # (no fork without work: a graph capture rejects an unjoined side stream)
-        bw = _Beside(wgrad_stream(dev) if ctx.beside and g.is_cuda and
-                     any(_wants(c.weight) for c in convs) else None)
 
         def wgrad(conv, dy, x, geom):
             if _wants(conv.weight):
-                def fn():
-                    conv_wgrad(dy, x, geom, grad_buffer(conv.weight))
-                    grads_done(conv.weight)
-                bw.run(fn, dy, x)
+                conv_wgrad(dy, x, geom, grad_buffer(conv.weight))
+                grads_done(conv.weight)
 
         # bn3 (+ residual) + relu: the mask from the forward's bitmask (bf16) or its output (x3)
         dy3 = torch.empty_like(y3)
@@ -906,11 +811,9 @@ class BottleneckFn(torch.autograd.Function):
             dyd = torch.empty_like(yd)
             sd.backward(dres, yd, None, False, dyd, None)
             wgrad(mod.downsample[0], dyd, xr, gd)
-        # conv3 (bf16 mode: bn2's backward sums reduced in its dgrad epilogue)
-        fuse = not ctx.x3 and FUSE_BN_DSTATS and g2.k >= FUSE_BN_DSTATS_MIN_C
+        # conv3
         da2 = torch.empty_like(a2)
-        st2 = conv_dgrad(dy3, g3, w3, da2, bn=s2 if fuse else None, y=y2,
-                         w_t=None if fuse else conv1x1_weight_T(mod.conv3, g3))
+        conv_dgrad(dy3, g3, w3, da2, w_t=conv1x1_weight_T(mod.conv3, g3))
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[1], from_rows(da2, B, g2.p, g2.q, g2.k))
         wgrad(mod.conv3, dy3, a2, g3)
@@ -918,24 +821,16 @@ class BottleneckFn(torch.autograd.Function):
         # BN + ReLU masks: recomputed from y (bf16), or in bf16x3 mode (fp32 pre-activations)
         # read from the forward's outputs
         dy2 = torch.empty_like(y2)
-        if st2 is not None:
-            s2.backward_from_dstats(st2, da2, y2, dy2)
-        else:
-            s2.backward(da2, y2, a2 if ctx.x3 else None, 1 if ctx.x3 else 2, dy2, None)
+        s2.backward(da2, y2, a2 if ctx.x3 else None, 1 if ctx.x3 else 2, dy2, None)
         da1 = torch.empty_like(a1)
-        fuse1 = fuse and g2.stride == 1
-        st1 = conv_dgrad(dy2, g2, w2, da1, bn=s1 if fuse1 else None, y=y1,
-                         w_flip=None if fuse1 or g2.stride != 1 else
-                         conv_weight_flipped(mod.conv2.weight))
+        conv_dgrad(dy2, g2, w2, da1, w_flip=None if g2.stride != 1 else
+                   conv_weight_flipped(mod.conv2.weight))
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[0], from_rows(da1, B, g1.p, g1.q, g1.k))
         wgrad(mod.conv2, dy2, a1, g2)
         # bn1 + relu, conv1 (+ identity gradient fused in the dgrad epilogue)
         dy1 = torch.empty_like(y1)
-        if st1 is not None:
-            s1.backward_from_dstats(st1, da1, y1, dy1)
-        else:
-            s1.backward(da1, y1, a1 if ctx.x3 else None, 1 if ctx.x3 else 2, dy1, None)
+        s1.backward(da1, y1, a1 if ctx.x3 else None, 1 if ctx.x3 else 2, dy1, None)
         dx = None
         if ctx.x_requires_grad:
             dxr = _empty((M1, Cin), BF16, dev)
@@ -956,7 +851,10 @@ class BottleneckFn(torch.autograd.Function):
 class AvgPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
-        x3 = _take_x3(x) if _x3() else None
+        # bf16x3: the triple the producer attached; "mixed": that triple if the last block ran
+        # bf16x3 (a bf16 block's output is pooled in bf16)
+        x3 = _take_x3(x) if _x3() and (get_precision() != "mixed" or hasattr(x, "_dfu_x3")) \
+            else None
         x = nhwc_bf16(x.detach())
         B, C, H, W = x.shape
         ctx.shape = (B, C, H, W)
@@ -1138,7 +1036,7 @@ class ViTBlockFn(torch.autograd.Function):
         wfc2 = weight_bf16_rows(mlp.fc2.weight)
         Dh = wfc1.shape[0]
         bias = lambda lin: lin.bias.detach() if lin.bias is not None else None  # noqa: E731
-        if _x3():
+        if _x3(blk):
             return ViTBlockFn._forward_x3(ctx, blk, x2, B, T, D, H, dh, rows, wqkv, wproj, wfc1,
                                           wfc2, bias)
         # attention branch
@@ -1166,7 +1064,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
-        ctx.beside = _VIT_WGRAD_STREAM and (_concurrent_encoders[0] == 0 or _WGRAD_BESIDE_FUSED)
+        ctx.beside = _VIT_WGRAD_STREAM and _concurrent_encoders[0] == 0
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo
@@ -1231,7 +1129,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)
-        ctx.beside = _VIT_WGRAD_STREAM and (_concurrent_encoders[0] == 0 or _WGRAD_BESIDE_FUSED)
+        ctx.beside = _VIT_WGRAD_STREAM and _concurrent_encoders[0] == 0
         ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
                               wproj, wfc1, wfc2)
         return xo

@@ -99,13 +99,21 @@ def reset_after_failed_capture(extra=()):
     return n, len(stuck)
 
 
+_capture_streams = {}
+
+
 def try_capture(step, log=None, pool=None):
     """Capture `step()` into a torch.cuda.CUDAGraph on a fresh capture stream; returns the graph,
     or None after a failed capture (streams recovered, the failure reported through `log`,
     default stderr).  Work the step left on a forked stream is joined into the capture
     (join_forked).  The caller warms `step` up eagerly first, as graph capture requires."""
     prev = torch.cuda.current_stream()
-    cap = Fn.new_stream(prev.device_index)  # library-owned: retired, not reused, if it sticks
+    # one library-owned capture stream per device, reused by every capture (a graph does not
+    # need its origin stream after the capture ends); retired, never reused, if a failure leaves
+    # it capturing
+    cap = _capture_streams.get(prev.device_index)
+    if cap is None:
+        cap = _capture_streams[prev.device_index] = Fn.new_stream(prev.device_index)
     cap.wait_stream(prev)
     g = torch.cuda.CUDAGraph()
     try:
@@ -117,6 +125,8 @@ def try_capture(step, log=None, pool=None):
         # torch.cuda.graph.__exit__ leaves its capture stream current when capture_end raises
         torch.cuda.set_stream(prev)
         n, stuck = reset_after_failed_capture(extra=(cap,))
+        if capture_status(cap) != 0:
+            _capture_streams.pop(prev.device_index, None)  # leaked on purpose (see above)
         msg = (f"[dfu] graph capture failed ({type(e).__name__}: {str(e).splitlines()[0]}); "
                f"{n} stream(s) were left capturing, {stuck} retired; running eager")
         if log is None:

@@ -92,7 +92,7 @@ def gemm_replay(records, stream=None):
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
          epilogue=L.EPI_BF16, alpha=1.0, bias=None, aux=None, ldaux=0, aux_out=None,
          ldaux_out=0, stats=None, split_k=0, ep_tokens=0, conv=None, tile=0, workspace=None,
-         bn_coef=None):
+         operand_type=0):
     """C = epilogue(A @ B^T).  `split_k` (F32_ACC only): 0 = library cost model, 1 = none.
     `tile`: 0 = library cost model, else a TILES id.  Split-K partials go to fp32 slabs in
     `workspace` (allocated here from the stream-ordered caching allocator when None) and are
@@ -113,7 +113,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
     d.aux_out = aux_out.data_ptr() if aux_out is not None else None
     d.ldaux_out = int(ldaux_out)
     d.stats = stats.data_ptr() if stats is not None else None
-    d.bn_coef = bn_coef.data_ptr() if bn_coef is not None else None
+    d.operand_type = int(operand_type)
     d.split_k = int(split_k)
     d.ep_tokens = int(ep_tokens)
     d.tile = int(tile)
@@ -135,7 +135,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
         if a_mode == L.OPND_CONV_DGRAD and conv is not None:
             flops /= conv.stride * conv.stride  # algorithmic: only the 1/stride^2 live taps
         gemm_record.append((d, flops, _algorithmic_bytes(d, conv),
-                            (A, B, C, bias, aux, aux_out, stats, workspace, bn_coef)))
+                            (A, B, C, bias, aux, aux_out, stats, workspace)))
 
 
 _COUNTERS = {}
@@ -727,33 +727,6 @@ def split_x3(x, pattern, seg=None, hi_out=None):
                              ptr(hi_out), seg if hi_out is None else hi_out.stride(0),
                              stream_ptr()), "dfu_split_x3")
     return out
-
-
-class SplitJobs:
-    """A device table of bf16x3 splits (dfu_split_x3_batch) launched as ONE kernel: jobs
-    (src fp32 [rows, cols] with unit column stride, out bf16 [rows, 3 seg], pattern)."""
-
-    def __init__(self, jobs):
-        import struct
-        raw, v0 = bytearray(), 0
-        for src, out, pattern in jobs:
-            _req(src, F32, "split_x3_batch")
-            _req(out, BF16, "split_x3_batch")
-            rows, cols = src.shape
-            seg = out.shape[1] // 3
-            if (src.stride(1) != 1 or out.shape != (rows, 3 * seg) or not out.is_contiguous()
-                    or seg % 8 or seg < cols or out.data_ptr() % 16):
-                raise ValueError(f"split_x3_batch: [{rows}, {cols}] -> {tuple(out.shape)}")
-            raw += struct.pack("<QQqqiiii", src.data_ptr(), out.data_ptr(), src.stride(0), v0,
-                               rows, cols, seg, int(pattern))
-            v0 += rows * (seg // 8)
-        self.jobs = list(jobs)  # keep the buffers alive as long as the table
-        self.njobs, self.nvec = len(self.jobs), v0
-        self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.jobs[0][0].device)
-
-    def launch(self):
-        check(lib().dfu_split_x3_batch(ptr(self.table), self.njobs, self.nvec, stream_ptr()),
-              "dfu_split_x3_batch")
 
 
 def pack_conv_weight_x3(w):

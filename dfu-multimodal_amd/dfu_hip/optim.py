@@ -198,23 +198,13 @@ class FlatParams:
 _EARLY_T = os.environ.get("DFU_EARLY_TRANSPOSE", "1") != "0"
 
 
-def _order_hook(wref):
-    """Grad-ready hook of one FusedAdamW (weakly referenced): notes the completion order of its
-    parameters' gradients and records the early main block's trigger event."""
-    def hook(p):
+def _version_snapshot(wref):
+    """Backward-end hook of one FusedAdamW (weakly referenced): the gradient buffer's version
+    as the backward left it (see FusedAdamW._grad_version)."""
+    def hook():
         o = wref()
-        if o is None or not o.early_main:
-            return
-        i = o._pidx.get(id(p))
-        if i is None or i in o._seen:
-            return
-        o._seen.add(i)
-        o._order.append(i)
-        t = o._trigger
-        if t is not None and i == t[0]:
-            ev = torch.cuda.Event()
-            ev.record()  # on the stream that produced the gradient (the current one)
-            o._trig_ev = ev
+        if o is not None:
+            o._grad_version = o.flat.grad._version
     return hook
 
 
@@ -236,32 +226,16 @@ class FusedAdamW(torch.optim.Optimizer):
         self.check_grads = True  # set False inside captured graphs (pointers are static)
         # update a side stream's parameter block on that stream (step); DFU_EARLY_ADAMW=0: off
         self.early_update = os.environ.get("DFU_EARLY_ADAMW", "1") != "0"
-        # the main stream's early block (DFU_EARLY_ADAMW_MAIN=1: on): the parameters whose
-        # gradients the backward's own stream finishes first (the ResNet's deep stages: its
-        # backward runs layer4 -> stem) are updated on an optimizer stream as soon as the last
-        # of them is done (an event recorded by a grad-ready hook), beside the rest of that
-        # backward instead of in the step's serial tail; learned from the previous step's
-        # completion order.  Its AdamW reads its own step counter (step_dev_b, kept equal).
-        # Off by default: the fusion step measured 18.40-18.46 vs 18.30-18.35 ms with it (the
-        # pass competes for HBM with the BatchNorm passes it runs beside).
-        self.early_main = os.environ.get("DFU_EARLY_ADAMW_MAIN", "0") != "0"
-        self.step_dev_b = torch.zeros((), dtype=torch.int64, device=dev)
-        self._b_valid = True  # step_dev_b == step_dev (not kept while the block is off)
-        self._pidx = {id(p): i for i, p in enumerate(self.flat.params)}
-        self._order, self._seen = [], set()
-        self._trigger = None   # (param index, lo, hi) learned from a step's completion order
-        self._learned_n = -1
-        self._trig_ev = None   # recorded this step when the trigger parameter completed
-        self._ost = None
-        self.last_early_main = None
-        if dev.type == "cuda":
-            hook = Fn.register_grad_ready_hook(_order_hook(weakref.ref(self)))
-            weakref.finalize(self, Fn.remove_grad_ready_hook, hook)
         self._dfu_joins_itself = True  # step() joins the gradient streams (functional)
-        # the flat gradient buffer's autograd version at the last zero_grad / step: the kernels
-        # write gradients through raw pointers (no bump), so a change means user code edited
-        # p.grad in place (clip_grad_norm_, unscaling, a manual reduction) on its own stream
+        # the flat gradient buffer's autograd version at the last zero_grad / step / end of a
+        # backward pass: the kernels write gradients through raw pointers (no bump), so a change
+        # since means user code edited p.grad in place (clip_grad_norm_, unscaling, a manual
+        # reduction) on its own stream.  Snapshotted again when a backward ends, so autograd's
+        # own AccumulateGrad into a torch.nn head's gradient (the drop-in path) does not count.
         self._grad_version = self.flat.grad._version
+        if dev.type == "cuda":
+            hook = Fn.register_backward_end_hook(_version_snapshot(weakref.ref(self)))
+            weakref.finalize(self, Fn.remove_backward_end_hook, hook)
 
     def zero_grad(self, set_to_none=True):
         # gradients stay bound to the flat buffer (stable addresses); one memset clears them
@@ -286,45 +260,14 @@ class FusedAdamW(torch.optim.Optimizer):
                 best = run
         return best if best is not None and best[1] - best[0] >= (1 << 20) else None
 
-    def _adamw(self, lo, hi, step_dev=None):
+    def _adamw(self, lo, hi):
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         fp = self.flat
         ops.adamw_flat(fp.data[lo:hi], fp.grad[lo:hi], self.exp_avg[lo:hi],
                        self.exp_avg_sq[lo:hi], g["lr"], b1, b2, g["eps"], g["weight_decay"],
-                       self.step_dev if step_dev is None else step_dev,
+                       self.step_dev,
                        shadow=None if fp.shadow is None else fp.shadow[lo:hi])
-
-    def _learn_trigger(self, cur):
-        """From this step's completion order: the largest run of parameters, contiguous in the
-        flat buffers, all produced on `cur` and complete while at most 90% of that stream's
-        gradient elements are -> (index of the parameter whose completion closes the run, lo,
-        hi), or None (runs are merged as their parameters complete: interval union)."""
-        fp = self.flat
-        main = [i for i in self._order if fp.params[i]._dfu_grad_stream == cur]
-        n = len(fp.params)
-        size = [_aligned(p.numel()) for p in fp.params]
-        total = sum(size[i] for i in main)
-        pre = [0]
-        for z in size:
-            pre.append(pre[-1] + z)
-        left, right = {}, {}
-        best, acc = None, 0
-        for i in main:
-            acc += size[i]
-            if acc > 0.9 * total:
-                break
-            lo_i = left[i - 1] if i - 1 in right else i
-            hi_i = right[i + 1] if i + 1 in left else i
-            right[lo_i], left[hi_i] = hi_i, lo_i
-            left.setdefault(i, lo_i)
-            right.setdefault(i, hi_i)
-            run = pre[hi_i + 1] - pre[lo_i]
-            if best is None or run > best[2] - best[1]:
-                best = (i, fp.offsets[lo_i], fp.offsets[hi_i] + size[hi_i])
-        if best is None or best[2] - best[1] < (1 << 20) or n == 0:
-            return None
-        return best
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -346,13 +289,6 @@ class FusedAdamW(torch.optim.Optimizer):
                 and not touched):
             early = self._early_range(torch.cuda.current_stream(fp.data.device))
         cur = torch.cuda.current_stream(fp.data.device) if fp.data.is_cuda else None
-        early_main = None
-        if (self.early_main and fp.data.is_cuda and not _dp_world() and not rebind and not touched
-                and self._trigger is not None and self._trig_ev is not None):
-            tr = self._trigger
-            if fp.params[tr[0]]._dfu_grad_stream == cur and (
-                    early is None or tr[2] <= early[0] or tr[1] >= early[1]):
-                early_main = tr[1:] if self._b_valid else None
         if early is not None:
             lo, hi, st = early
             with torch.cuda.stream(st):
@@ -364,37 +300,20 @@ class FusedAdamW(torch.optim.Optimizer):
                 if inside is not None:
                     inside.launch()
             cur.wait_stream(st)  # the rest, the step counter and the shadow transposes after it
-        if early_main is not None:
-            if self._ost is None:
-                self._ost = Fn.new_stream(fp.data.device.index)
-            self._ost.wait_event(self._trig_ev)
-            with torch.cuda.stream(self._ost):
-                ops.step_increment(self.step_dev_b)
-                self._adamw(early_main[0], early_main[1], self.step_dev_b)
-            cur.wait_stream(self._ost)
-        elif self.early_main and self._b_valid:
-            ops.step_increment(self.step_dev_b)
         Fn.join_grad_streams()
         if rebind:
             fp.rebind_grads()
         if early is None:
             ops.step_increment(self.step_dev)
-        done = sorted(r for r in (None if early is None else early[:2], early_main) if r)
-        a = 0
-        for r in done + [(fp.numel, fp.numel)]:
-            if r[0] > a:
-                self._adamw(a, r[0])
-            a = max(a, r[1])
-        if self.early_main and cur is not None and len(self._order) != self._learned_n:
-            self._trigger = self._learn_trigger(cur)  # (the order is the same every step)
-            self._learned_n = len(self._order)
-        self._order, self._seen, self._trig_ev = [], set(), None
+        if early is None:
+            self._adamw(0, fp.numel)
+        else:  # the rest: both sides of the early block
+            if early[0] > 0:
+                self._adamw(0, early[0])
+            if early[1] < fp.numel:
+                self._adamw(early[1], fp.numel)
         for p in fp.params:
             p._dfu_grad_stream = None
-        if self.early_main and not self._b_valid:  # (re-)enabled: resync its step counter
-            self.step_dev_b.copy_(self.step_dev)
-        self._b_valid = self.early_main
-        self.last_early_main = early_main
         self.last_early = None if early is None else early[:2]
         fp.shadows_rewritten(None if early is None or fp.t_jobs is None or not _EARLY_T
                              else early[:2])
@@ -436,5 +355,3 @@ class FusedAdamW(torch.optim.Optimizer):
         if steps:
             n = steps.pop()
             self.step_dev.fill_(n)
-            self.step_dev_b.fill_(n)
-            self._b_valid = self.early_main

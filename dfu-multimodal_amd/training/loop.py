@@ -219,6 +219,23 @@ def _gather_rows(t, group=None):
     return torch.cat([p[:k] for p, k in zip(parts, ns)])
 
 
+def gather_in_order(tensors, loader, group=None):
+    """Every rank's per-sample rows of each tensor, concatenated over the ranks; when the
+    loader's sampler knows the shards' sample indices (data.sharding.ShardedSequentialSampler
+    .global_indices), the rows are put back at their sample index (the reference's sequential
+    order, every sample exactly once)."""
+    out = [_gather_rows(t, group) for t in tensors]
+    order = getattr(getattr(loader, "sampler", None), "global_indices", None)
+    if order is None or _dp_group_size(group) <= 1:
+        return out
+    idx = torch.tensor(order(), dtype=torch.int64, device=out[0].device)
+    if idx.numel() != out[0].shape[0]:
+        raise RuntimeError(f"gather_in_order: {out[0].shape[0]} rows for {idx.numel()} samples")
+    inv = torch.empty_like(idx)
+    inv[idx] = torch.arange(idx.numel(), device=idx.device)
+    return [t[inv] for t in out]
+
+
 def evaluate(model, loader, criterion, forward=None, num_classes=2, device="cuda",
              results_path=None, group=None, log=print):
     """The reference's test phase (train_multimodal_fusion.py:457-504): eval mode, no_grad;
@@ -227,7 +244,8 @@ def evaluate(model, loader, criterion, forward=None, num_classes=2, device="cuda
     (dfu_argmax_rows, torch.max's first maximum).  Returns the reference's result dict; with
     `results_path`, rank 0 also saves it there (torch.save, as :497-504: lists of numpy scalars
     for preds / labels / probs).  Under data parallelism each rank evaluates its shard and the
-    dict holds every rank's samples in rank order."""
+    dict holds every sample once, in the reference's order when the loader's sampler is a
+    data.sharding.ShardedSequentialSampler (its global_indices)."""
     collect = []
     broadcast_buffers(model, group=group)
     r = run_epoch(model, loader, criterion, None, False, None, forward, num_classes, device,
@@ -241,7 +259,7 @@ def evaluate(model, loader, criterion, forward=None, num_classes=2, device="cuda
         logits = torch.zeros((0, num_classes), dtype=torch.float32, device=device)
         probs = torch.zeros((0,), dtype=torch.float32, device=device)
         preds = labels = torch.zeros((0,), dtype=torch.int64, device=device)
-    preds, labels, probs = (_gather_rows(t, group) for t in (preds, labels, probs))
+    preds, labels, probs = gather_in_order((preds, labels, probs), loader, group)
     res = {"test_preds": list(preds.cpu().numpy()), "test_labels": list(labels.cpu().numpy()),
            "test_probs": list(probs.cpu().numpy()), "test_acc": r["acc"], "test_f1": r["f1"],
            "test_loss": r["loss"]}

@@ -79,14 +79,9 @@ enum dfu_epilogue {
   DFU_EPI_PATCH = 10,        /* ViT patch-embed: C f32 [B][T+1][N] row 1+p = acc+bias+pos   */
   DFU_EPI_F32_STATS = 11,    /* C f32 = acc; per-column (sum, M2) of each 128-row tile (the
                                 split-bf16 "bf16x3" forward: BN statistics of unrounded y)  */
-  DFU_EPI_BF16_DSTATS = 12,  /* BatchNorm backward statistics in the dgrad that produces the
-                                BN output's gradient: C bf16 = g = alpha*acc; per column of
-                                each 128-row tile, stats[tile][0] = sum g', stats[tile][1] =
-                                sum g' (y - mean) invstd over g' = g masked by the forward's
-                                ReLU (fma(y, scale, shift) > 0), y = aux bf16 (the BN input),
-                                bn_coef = fp32 [4][N] rows scale, shift, mean, invstd.  The
-                                records feed dfu_bn_bwd_finalize (blocks = ceil(M/128)) in
-                                place of dfu_bn_bwd_reduce.  Stride-1 launches only.         */
+  DFU_EPI_BF16_DSTATS = 12,  /* retired (round 4: BN backward sums in the dgrad epilogue
+                                measured slower than the separate reduce); reserved, returns
+                                DFU_E_UNSUPPORTED                                            */
   DFU_EPI_X3_GELU = 13       /* bf16x3 forward of timm Mlp.fc1 + GELU: pre = acc + bias (fp32),
                                 C = the A-operand triple [hi | lo | hi] of gelu(pre), bf16
                                 [M][3N] (ldc >= 3N; segments at columns 0, N, 2N), aux_out
@@ -132,7 +127,9 @@ typedef struct dfu_gemm_desc {
    * buffer per stream (launches on one stream never overlap). */
   int32_t* tile_counters;
   int32_t tile_counters_len;
-  const float* bn_coef; /* DFU_EPI_BF16_DSTATS: fp32 [4][N] scale, shift, mean, invstd      */
+  int32_t operand_type; /* 0 = bf16 A and B; 1 = fp16 A and B (the "parity" precision
+                           mode's ViT forward: persistent tiles 8 / 9, K-contiguous A and B,
+                           epilogues F32, F32_RESID, F16_DUAL, F16_GELU)                   */
 } dfu_gemm_desc;
 
 int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
@@ -433,12 +430,6 @@ int dfu_metrics_accumulate(const float* logits, const int64_t* labels, int32_t r
  * columns past cols zero); optional plain bf16 copy hi_out [rows][ld_hi >= seg]. */
 int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_t cols, int32_t seg,
                  void* out, int32_t pattern, void* hi_out, int64_t ld_hi, void* stream);
-/* Many dfu_split_x3 (pattern and seg per job) as ONE launch.  jobs: a DEVICE array of njobs
- * records {const float* in; void* out; int64_t ld_in; int64_t v0; int32_t rows, cols, seg,
- * pattern;} (48 bytes each), v0 = the job's first 8-column vector = the sum of rows * seg / 8
- * over the jobs before it (ascending); nvec = that sum over all jobs.  The bf16x3 weight
- * operands of an encoder, re-derived once per optimizer step (dfu_hip.functional). */
-int dfu_split_x3_batch(const void* jobs, int32_t njobs, int64_t nvec, void* stream);
 /* fp32 OIHW conv weight -> bf16 KRSC' with C' = 3C, pattern 1 along the channels. */
 int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int32_t C, int32_t R, int32_t S,
                             void* stream);

@@ -39,16 +39,18 @@ import torch.nn.functional as F
 # §7 (hard parts: report both the fp32-oracle and the bf16-rounded-oracle deltas).
 _EMU = False
 _EXACT_SITES = set()  # rounding sites left in fp32 (precision studies, tools/precision_study.py)
+_EMU_DTYPE = [torch.bfloat16]  # the storage type emulated (fp16: tools/fp16_study.py)
 
 
-def set_bf16_emulation(on, exact_sites=()):
+def set_bf16_emulation(on, exact_sites=(), dtype=torch.bfloat16):
     global _EMU, _EXACT_SITES
     _EMU = bool(on)
     _EXACT_SITES = set(exact_sites)
+    _EMU_DTYPE[0] = dtype
 
 
 def rb(x, site=None):
-    return x.to(torch.bfloat16).float() if _EMU and site not in _EXACT_SITES else x
+    return x.to(_EMU_DTYPE[0]).float() if _EMU and site not in _EXACT_SITES else x
 
 
 def conv(x, w, stride=1, padding=0):
@@ -173,7 +175,7 @@ class _EmuAttention(torch.autograd.Function):
 
         def r(x, site):
             exact = ctx.exact == "all" or site in _EXACT_SITES
-            return x if exact else x.to(torch.bfloat16).float()
+            return x if exact else x.to(_EMU_DTYPE[0]).float()
         p = torch.exp(q @ k.transpose(-1, -2) * scale - lse)
         delta = (do * o).sum(-1, keepdim=True)
         dv = r(p, "p").transpose(-1, -2) @ do

@@ -29,9 +29,18 @@ def test_sharded_samplers_cover_one_draw(n, world):
     g = torch.Generator().manual_seed(5 + 2)
     assert shards[0].full_draw() == torch.multinomial(torch.tensor(w, dtype=torch.double), n, True,
                                                       generator=g).tolist()
-    seq = [list(ShardedSequentialSampler(n, r, world)) for r in range(world)]
-    assert sorted(set(sum(seq, []))) == list(range(n))
-    assert len({len(s) for s in seq}) == 1
+    for B in (1, 3, 4):
+        seq = [ShardedSequentialSampler(n, r, world, batch_size=B) for r in range(world)]
+        parts = [list(s) for s in seq]
+        # every sample exactly once (no wrap padding), batches of the single-process walk
+        assert sorted(sum(parts, [])) == list(range(n))
+        assert seq[0].global_indices() == sum(parts, [])
+        assert [len(p) for p in parts] == [len(s) for s in seq]
+        for r, p in enumerate(parts):
+            for k in range(0, len(p), B):
+                blk = p[k:k + B]
+                j = blk[0] // B
+                assert j % world == r and blk == list(range(j * B, min(n, (j + 1) * B)))
 
 
 def test_metrics_from_confusion_matches_sklearn():
@@ -63,6 +72,49 @@ def _reduce_worker(rank, port, q):
         q.put((rank, met.result()))
     finally:
         dist.destroy_process_group()
+
+
+def _order_worker(rank, port, q):
+    import torch.distributed as dist
+
+    from training.loop import gather_in_order
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        n, B = 11, 3  # 4 batches, the last short: rank 0 runs batches 0, 2; rank 1 runs 1, 3
+
+        class _L:
+            sampler = ShardedSequentialSampler(n, rank, 2, batch_size=B)
+        mine = torch.tensor(list(_L.sampler), dtype=torch.int64)
+        got, sq = gather_in_order((mine, (mine * mine).float()), _L)
+        q.put((rank, got.tolist(), sq.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_in_order_world2_ragged():
+    """val / test under DP with n % world != 0 -- every sample once, in order."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_order_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, got, sq = q.get(timeout=120)
+        res[r] = (got, sq)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert res[r][0] == list(range(11))
+        assert res[r][1] == [float(i * i) for i in range(11)]
 
 
 def test_device_metrics_all_reduce_world2():

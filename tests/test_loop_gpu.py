@@ -143,7 +143,7 @@ def _fit_worker(rank, port, ckdir, q):
         wsamp = ShardedWeightedSampler(sample_weights(y[:NT].tolist()), rank=rank, world_size=2,
                                        seed=42)
         train_loader = _TensorLoader(tr, B, wsamp)
-        val_loader = _TensorLoader(va, B, ShardedSequentialSampler(NV, rank, 2))
+        val_loader = _TensorLoader(va, B, ShardedSequentialSampler(NV, rank, 2, batch_size=B))
         recs = []
 
         class _Rec(hnn.CrossEntropyLoss):

@@ -58,9 +58,8 @@ def test_adamw_matches_torch_and_shadow_tracks():
 
 def test_early_adamw_on_side_stream_is_bitwise_equal():
     """In the two-stream fusion step the ViT branch's parameters get their AdamW update on the
-    ViT side stream as soon as its backward is done (FusedAdamW.step early block), the ResNet's
-    deep stages on an optimizer stream as soon as their gradients are (the main stream's early
-    block), the rest after the join: parameters, moments, bf16 shadows and the ViT transposed
+    ViT side stream as soon as its backward is done (FusedAdamW.step early block), the rest
+    after the join: parameters, moments, bf16 shadows and the ViT transposed
     shadows after three steps equal the single-launch update bit for bit."""
     import bench
     from dfu_hip import nn as hnn
@@ -74,7 +73,6 @@ def test_early_adamw_on_side_stream_is_bitwise_equal():
         fwd = lambda m, r, t: m(r, t)  # noqa: E731
         opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
         opt.early_update = early
-        opt.early_main = early  # (default off: DFU_EARLY_ADAMW_MAIN)
         crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
         rgb, th, y = bench.synthetic(4, dev, seed=3)
         for _ in range(3):
@@ -87,16 +85,9 @@ def test_early_adamw_on_side_stream_is_bitwise_equal():
             vit = [i for i, p in enumerate(opt.flat.params)
                    if any(p is q for q in model.vit.parameters())]
             assert opt.flat.offsets[vit[0]] == lo and hi - lo >= 85_000_000
-            # the main stream's early block: the ResNet's deep stages (their gradients complete
-            # first in its backward), learned from step 1 and used from step 2
-            mlo, mhi = opt.last_early_main
-            rn = [i for i, p in enumerate(opt.flat.params)
-                  if any(p is q for q in model.resnet.parameters())]
-            assert opt.flat.offsets[rn[0]] < mlo < mhi <= opt.flat.offsets[rn[-1] + 1]
-            assert mhi - mlo >= 15_000_000
-            assert int(opt.step_dev_b) == int(opt.step_dev) == 3
+            assert int(opt.step_dev) == 3
         else:
-            assert opt.last_early is None and opt.last_early_main is None
+            assert opt.last_early is None
         tq = model.vit.blocks[0].mlp.fc1.weight
         res.append([opt.flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(),
                     opt.flat.shadow.clone(), getattr(tq, "_dfu_shadow_T").clone(),

@@ -238,49 +238,3 @@ def test_attention_fwd_f32_matches_sdpa(N):
     assert torch.equal(qb, qkv.to(torch.bfloat16))  # the backward's bf16 qkv, written in passing
     lref = torch.logsumexp(s, -1).reshape(B * H, N)
     assert torch.allclose(lse[:, :N].double(), lref, rtol=2.0 ** -14, atol=1e-5)
-
-
-def test_split_x3_batch_equals_single_splits():
-    L, ops = _ops()
-    torch.manual_seed(3)
-    srcs = [torch.randn(r, c, device=DEV) for r, c in ((64, 147), (768, 768), (5, 8), (33, 100))]
-    segs = [160, 768, 8, 104]
-    outs = [torch.empty(s.shape[0], 3 * g, dtype=torch.bfloat16, device=DEV) for s, g in zip(srcs, segs)]
-    ops.SplitJobs([(s, o, ops.X3_B) for s, o in zip(srcs, outs)]).launch()
-    for s, o, g in zip(srcs, outs, segs):
-        assert torch.equal(o, ops.split_x3(s, ops.X3_B, seg=g))
-
-
-def test_x3_weight_cache_refreshes_after_optimizer_steps(monkeypatch):
-    """The cached bf16x3 weight operands (functional.weight_x3_rows: one batched re-split per
-    encoder stream after the weights change) give the logits of uncached per-use splits,
-    bitwise, across FusedAdamW steps and an in-place weight edit."""
-    from models.fusion import MultimodalFusionModel
-    from dfu_hip import functional as Fn
-    from dfu_hip import nn as hnn
-    from dfu_hip.optim import FusedAdamW
-    torch.manual_seed(0)
-    model = MultimodalFusionModel(num_classes=2).to(DEV).train()
-    for m in model.modules():
-        if isinstance(m, torch.nn.Dropout):
-            m.p = 0.0
-    opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
-    crit = hnn.CrossEntropyLoss(weight=torch.tensor([1.0, 2.0], device=DEV))
-    g = torch.Generator(device=DEV).manual_seed(1)
-    rgb = torch.randn(2, 3, 224, 224, device=DEV, generator=g)
-    th = torch.randn(2, 3, 224, 224, device=DEV, generator=g)
-    y = torch.tensor([0, 1], device=DEV)
-    for step in range(3):
-        outs = []
-        for cache in (False, True):
-            monkeypatch.setattr(Fn, "_X3_CACHE", cache)
-            with torch.no_grad(), Fn.precision("bf16x3"):
-                outs.append(model(rgb, th).float())
-        torch.cuda.synchronize()
-        assert torch.equal(outs[0], outs[1]), step
-        opt.zero_grad()
-        crit(model(rgb, th), y).backward()
-        opt.step()
-        if step == 1:
-            with torch.no_grad():
-                model.vit.blocks[0].attn.qkv.weight.mul_(1.01)
