@@ -46,13 +46,30 @@ DFU_DEV bf16x8 tr_frag_asm(const char* lds, int u, int d0, int lane) {
   bf16x4 x1 = lds_tr16_b64(lds + r128_off(r0 + 16, chunk) + half * 8);
   return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+template <bool H16 = false>
 DFU_DEV bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
   u32x4 w;
-  w[0] = pack2(a[0], a[1]);
-  w[1] = pack2(a[2], a[3]);
-  w[2] = pack2(b[0], b[1]);
-  w[3] = pack2(b[2], b[3]);
+  if constexpr (H16) {
+    w[0] = pack2h(a[0], a[1]);
+    w[1] = pack2h(a[2], a[3]);
+    w[2] = pack2h(b[0], b[1]);
+    w[3] = pack2h(b[2], b[3]);
+  } else {
+    w[0] = pack2(a[0], a[1]);
+    w[1] = pack2(a[2], a[3]);
+    w[2] = pack2(b[0], b[1]);
+    w[3] = pack2(b[2], b[3]);
+  }
   return __builtin_bit_cast(bf16x8, w);
+}
+// One 16x16x32 MFMA on 16-bit operands held as bf16x8 bits: bf16, or fp16 (H16).
+template <bool H16>
+DFU_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (H16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 // Copy rows [0, NPAD) of one (b, h) slice of qkv (which = 0 q, 1 k, 2 v) or of a [B*N][H][64]
@@ -137,11 +154,14 @@ DFU_DEV void stage_kv_dma(char* img, const bf16_t* kbase, const bf16_t* vbase,
 // DMA'd (global_load_lds, no register round trip) while this one is computed, so the staging
 // latency that a one-slice-per-workgroup launch exposed (216 VGPRs: one workgroup per CU)
 // overlaps the math.  13 query tiles of 16 at N = 197: at most 2 per wave.
-template <int KT, int NW = 8>
+// H16: fp16 qkv and P (the "parity" precision mode's ViT forward): o is written in fp16 (the
+// proj GEMM's operand) and in bf16 to o_bf (what the bf16 backward reads).
+template <int KT, int NW = 8, bool H16 = false>
 __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__ qkv, int N, int H,
                                                       int BH, float scale,
                                                       bf16_t* __restrict__ o,
-                                                      float* __restrict__ lse) {
+                                                      float* __restrict__ lse,
+                                                      bf16_t* __restrict__ o_bf = nullptr) {
   constexpr int NPAD = KT * 16;
   constexpr int IMG2 = 2 * NPAD * 128;  // K + V images of one slice
   constexpr int QPW = 2;                // query tiles per wave and slice (QT <= 2 * NW)
@@ -212,7 +232,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
         s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ks, 16 * t, ks, lane), qf[ks], s[t], 0, 0, 0);
+          s[t] = mfma16<H16>(row_frag(Ks, 16 * t, ks, lane), qf[ks], s[t]);
       }
       // lane holds S[q][key = 16t + 4g + r]; padding keys: NPAD rounds N up to a multiple of
       // 32, so only the last two key tiles (a compile-time set) can hold them
@@ -255,7 +275,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
       for (int dt = 0; dt < 4; ++dt) vf[dt] = tr_frag_asm(Vs, 0, 16 * dt, lane);
 #pragma unroll
       for (int u = 0; u < KT / 2; ++u) {
-        const bf16x8 pb = pack_frag(s[2 * u], s[2 * u + 1]);
+        const bf16x8 pb = pack_frag<H16>(s[2 * u], s[2 * u + 1]);
         lds_reads_retired();
         bf16x8 cur[4];
 #pragma unroll
@@ -268,16 +288,23 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
           for (int dt = 0; dt < 4; ++dt) vf[dt] = tr_frag_asm(Vs, u + 1, 16 * dt, lane);
         }
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[dt], pb, acc[dt], 0, 0, 0);
+        for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma16<H16>(cur[dt], pb, acc[dt]);
       }
       if (q < N) {
         const float inv = 1.0f / l;
-        bf16_t* orow = o + ((int64_t)b * N + q) * H * 64 + h * 64 + 4 * g;
+        const int64_t oe = ((int64_t)b * N + q) * H * 64 + h * 64 + 4 * g;
+        bf16_t* orow = o + oe;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          *(u32x2*)(orow + 16 * dt) = (u32x2){pack2(acc[dt][0] * inv, acc[dt][1] * inv),
-                                              pack2(acc[dt][2] * inv, acc[dt][3] * inv)};
+        for (int dt = 0; dt < 4; ++dt) {
+          const float o0 = acc[dt][0] * inv, o1 = acc[dt][1] * inv;
+          const float o2 = acc[dt][2] * inv, o3 = acc[dt][3] * inv;
+          if constexpr (H16) {
+            *(u32x2*)(orow + 16 * dt) = (u32x2){pack2h(o0, o1), pack2h(o2, o3)};
+            *(u32x2*)(o_bf + oe + 16 * dt) = (u32x2){pack2(o0, o1), pack2(o2, o3)};
+          } else {
+            *(u32x2*)(orow + 16 * dt) = (u32x2){pack2(o0, o1), pack2(o2, o3)};
+          }
+        }
         if (g == 0) lse[(int64_t)bh * NPAD + q] = mx * scale + logf(l);
       }
     }
@@ -675,6 +702,23 @@ extern "C" int dfu_attention_fwd(const void* qkv, int32_t B, int32_t N, int32_t 
   const int BH = B * H;
   const int grid = BH < attn_cus() ? BH : attn_cus();  // persistent: one workgroup per CU
 #define CALL(K) hipLaunchKernelGGL(k_attn_fwd<K>, dim3(grid), dim3(512), 0, s, (const bf16_t*)qkv, N, H, BH, scale, (bf16_t*)o, lse)
+  DISPATCH_KT(KT, CALL)
+#undef CALL
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_attention_fwd_f16(const void* qkv, int32_t B, int32_t N, int32_t H, int32_t dh,
+                                     float scale, void* o, void* o_bf16, float* lse,
+                                     void* stream) {
+  DFU_CHECK_ARG(qkv && o && o_bf16 && lse && B > 0 && H > 0, "dfu_attention_fwd_f16: bad args");
+  DFU_CHECK_ARG(dh == 64, "dfu_attention_fwd_f16: head dim %d unsupported (64 only)", dh);
+  DFU_CHECK_ARG(N > 0 && N <= 256, "dfu_attention_fwd_f16: N=%d unsupported (<= 256)", N);
+  const int KT = dfu_attention_npad(N) / 16;
+  hipStream_t s = (hipStream_t)stream;
+  const int BH = B * H;
+  const int grid = BH < attn_cus() ? BH : attn_cus();
+#define CALL(K) hipLaunchKernelGGL((k_attn_fwd<K, 8, true>), dim3(grid), dim3(512), 0, s, (const bf16_t*)qkv, N, H, BH, scale, (bf16_t*)o, lse, (bf16_t*)o_bf16)
   DISPATCH_KT(KT, CALL)
 #undef CALL
   DFU_LAUNCH_CHECK();

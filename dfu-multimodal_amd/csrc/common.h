@@ -31,6 +31,12 @@ typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 DFU_DEV uint32_t pack2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2_t));
 }
+// fp16 (IEEE binary16, RNE) forms: the "parity" precision mode's ViT forward operands
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+DFU_DEV uint32_t pack2h(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, f16x2_t));
+}
 DFU_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 DFU_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
@@ -46,6 +52,12 @@ DFU_DEV u32x4 pack8(const float* f) {
   u32x4 r;
 #pragma unroll
   for (int i = 0; i < 4; ++i) r[i] = pack2(f[2 * i], f[2 * i + 1]);
+  return r;
+}
+DFU_DEV u32x4 pack8h(const float* f) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = pack2h(f[2 * i], f[2 * i + 1]);
   return r;
 }
 

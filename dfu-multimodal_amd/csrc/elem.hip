@@ -56,6 +56,17 @@ __global__ void k_cast_rows_bf16(const float* __restrict__ in, int64_t ld_in,
   }
 }
 
+__global__ void k_cast_rows_f16(const float* __restrict__ in, int64_t ld_in,
+                                bf16_t* __restrict__ out, int64_t ld_out, int rows, int cols) {
+  const int64_t n = (int64_t)rows * ld_out;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / ld_out;
+    const int c = (int)(i - r * ld_out);
+    out[i] = c < cols ? (bf16_t)(pack2h(in[r * ld_in + c], 0.f) & 0xffffu) : (bf16_t)0;
+  }
+}
+
 __global__ void k_cast_rows_f32(const bf16_t* __restrict__ in, int64_t ld_in,
                                 float* __restrict__ out, int64_t ld_out, int rows, int cols) {
   const int64_t n = (int64_t)rows * cols;
@@ -854,6 +865,15 @@ extern "C" int dfu_cast_rows_bf16(const float* in, int64_t ld_in, void* out, int
   DFU_CHECK_ARG(in && out && rows > 0 && cols > 0 && ld_out >= cols && ld_in >= cols,
                 "dfu_cast_rows_bf16: bad args");
   LAUNCH(k_cast_rows_bf16, (int64_t)rows * ld_out, stream, in, ld_in, (bf16_t*)out, ld_out, rows,
+         cols);
+  return DFU_OK;
+}
+
+extern "C" int dfu_cast_rows_f16(const float* in, int64_t ld_in, void* out, int64_t ld_out,
+                                 int32_t rows, int32_t cols, void* stream) {
+  DFU_CHECK_ARG(in && out && rows > 0 && cols > 0 && ld_out >= cols && ld_in >= cols,
+                "dfu_cast_rows_f16: bad args");
+  LAUNCH(k_cast_rows_f16, (int64_t)rows * ld_out, stream, in, ld_in, (bf16_t*)out, ld_out, rows,
          cols);
   return DFU_OK;
 }

@@ -77,6 +77,11 @@ const TunedPlan kTuned[] = {
 #include "gemm_tuned.inc"
     {-1, -1, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
 
+// the dispatch key of a descriptor's kernel: its epilogue, | kF16Key for fp16 operands
+inline int epi_key(const dfu_gemm_desc* d) {
+  return d->epilogue | (d->operand_type == 1 ? kF16Key : 0);
+}
+
 const TunedPlan* find_tuned(const dfu_gemm_desc* d) {
   const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
   const int epi = d->epilogue;
@@ -99,7 +104,7 @@ Plan plan_gemm(const dfu_gemm_desc* d) {
     if (const TunedPlan* tp = find_tuned(d)) {
       Plan pl;
       pl.tile = tp->tile - 1;
-      pl.entry = find_entry(d->a_mode, d->b_mode, d->epilogue, pl.tile);
+      pl.entry = find_entry(d->a_mode, d->b_mode, epi_key(d), pl.tile);
       pl.split = acc_epi ? tp->split : 1;
       pl.cost = 0.0;
       if (pl.entry) return pl;
@@ -109,7 +114,7 @@ Plan plan_gemm(const dfu_gemm_desc* d) {
   Plan best;
   for (int t = 0; t < NTILES; ++t) {
     if (d->tile > 0 && d->tile - 1 != t) continue;
-    const Entry* en = find_entry(d->a_mode, d->b_mode, d->epilogue, t);
+    const Entry* en = find_entry(d->a_mode, d->b_mode, epi_key(d), t);
     if (!en) continue;
     const int tiles = cdiv(d->M, kTM[t]) * cdiv(d->N, kTN[t]);
     int s_lo = 1, s_hi = 1;
@@ -284,6 +289,15 @@ extern "C" int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* d) {
 
 extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* split_k) {
   DFU_CHECK_ARG(d != nullptr && tile != nullptr && split_k != nullptr, "dfu_gemm_plan: null");
+  DFU_CHECK_ARG(d->operand_type == 0 || d->operand_type == 1, "dfu_gemm: bad operand_type %d",
+                d->operand_type);
+  if (d->epilogue == DFU_EPI_F16_DUAL || d->epilogue == DFU_EPI_F16_GELU) {
+    DFU_CHECK_ARG(d->operand_type == 1, "dfu_gemm: the F16 epilogues need operand_type 1");
+    DFU_CHECK_ARG(d->aux_out != nullptr && d->ldaux_out >= d->N,
+                  "dfu_gemm: F16_DUAL / F16_GELU need aux_out (ldaux_out >= N)");
+    DFU_CHECK_ARG(d->epilogue != DFU_EPI_F16_GELU || d->ldc >= 2LL * d->N,
+                  "dfu_gemm: F16_GELU needs ldc >= 2N");
+  }
   const Plan pl = plan_gemm(d);
   if (!pl.entry) {
     dfu_set_error("dfu_gemm_plan: unsupported combination");
@@ -372,10 +386,20 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
   const bool acc_epi = d->epilogue == DFU_EPI_F32_ACC;
   DFU_CHECK_ARG(d->split_k >= 0, "dfu_gemm: split_k must be >= 0 (0 = auto)");
   DFU_CHECK_ARG(d->split_k <= 1 || acc_epi, "dfu_gemm: split_k > 1 needs the F32_ACC epilogue");
+  DFU_CHECK_ARG(d->operand_type == 0 || d->operand_type == 1, "dfu_gemm: bad operand_type %d",
+                d->operand_type);
+  if (d->epilogue == DFU_EPI_F16_DUAL || d->epilogue == DFU_EPI_F16_GELU) {
+    DFU_CHECK_ARG(d->operand_type == 1, "dfu_gemm: the F16 epilogues need operand_type 1");
+    DFU_CHECK_ARG(d->aux_out != nullptr && d->ldaux_out >= d->N,
+                  "dfu_gemm: F16_DUAL / F16_GELU need aux_out (ldaux_out >= N)");
+    DFU_CHECK_ARG(d->epilogue != DFU_EPI_F16_GELU || d->ldc >= 2LL * d->N,
+                  "dfu_gemm: F16_GELU needs ldc >= 2N");
+  }
   const Plan pl = plan_gemm(d);
   if (!pl.entry) {
-    dfu_set_error("dfu_gemm: unsupported combination a_mode=%d b_mode=%d epilogue=%d tile=%d",
-                  d->a_mode, d->b_mode, d->epilogue, d->tile);
+    dfu_set_error("dfu_gemm: unsupported combination a_mode=%d b_mode=%d epilogue=%d tile=%d "
+                  "operand_type=%d", d->a_mode, d->b_mode, d->epilogue, d->tile,
+                  d->operand_type);
     return DFU_E_UNSUPPORTED;
   }
   if (d->epilogue == DFU_EPI_BF16_DGELU && d->stats != nullptr && pl.tile != T256x256ps) {

@@ -392,15 +392,18 @@ DFU_DEV void st4_f32(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, const
                                             boff(okr && n + q < N, (e + q) * 4), 0, AUX);
   }
 }
+template <bool H16 = false>
 DFU_DEV void st4_bf16(rsrc_t r, int64_t e, bool okr, int n, int N, bool n4, const float* v) {
   if (n4) {
-    const u32x2 x = {pack2(v[0], v[1]), pack2(v[2], v[3])};
+    const u32x2 x = H16 ? (u32x2){pack2h(v[0], v[1]), pack2h(v[2], v[3])}
+                        : (u32x2){pack2(v[0], v[1]), pack2(v[2], v[3])};
     __builtin_amdgcn_raw_buffer_store_b64(x, r, boff(okr && n < N, e * 2), 0, 0);
   } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_raw_buffer_store_b16(f2bf(v[q]), r, boff(okr && n + q < N, (e + q) * 2),
-                                            0, 0);
+    for (int q = 0; q < 4; ++q) {
+      const uint16_t h = H16 ? (uint16_t)(pack2h(v[q], 0.f) & 0xffffu) : f2bf(v[q]);
+      __builtin_amdgcn_raw_buffer_store_b16(h, r, boff(okr && n + q < N, (e + q) * 2), 0, 0);
+    }
   }
 }
 template <int AUX = 0>
@@ -502,17 +505,19 @@ DFU_DEV void load_bias(const float* bias, int n0w, int N, int lane, float (&b)[F
 // v_permlane16_swap per dword so every lane stores 8 consecutive columns (16 B): lane group g
 // takes columns 16j + 16(g&1) + 8(g>>1) .. +7, the 4 lanes of a row cover 64 contiguous bytes,
 // and one dwordx4 replaces two dwordx2 (HIP guide T21, for the 16x16 accumulator layout).
-template <int FN, int AUX = 0>
+// H16: fp16 outputs instead of bf16 (the same 16-bit layout).
+template <int FN, int AUX = 0, bool H16 = false>
 DFU_DEV void st_row_bf16(rsrc_t r, int64_t rowe, bool okm, int n0w, int N, bool n8, bool n4,
                          int lane, const float (&v)[FN][4]) {
   static_assert(FN % 2 == 0, "fragment pairs");
+  auto pk = [](float a, float b) { return H16 ? pack2h(a, b) : pack2(a, b); };
   if (n8) {
     const int g = lane >> 4;
     const int cofs = ((g & 1) << 4) + ((g >> 1) << 3);
 #pragma unroll
     for (int j = 0; j < FN; j += 2) {
-      const uint32_t a0 = pack2(v[j][0], v[j][1]), a1 = pack2(v[j][2], v[j][3]);
-      const uint32_t b0 = pack2(v[j + 1][0], v[j + 1][1]), b1 = pack2(v[j + 1][2], v[j + 1][3]);
+      const uint32_t a0 = pk(v[j][0], v[j][1]), a1 = pk(v[j][2], v[j][3]);
+      const uint32_t b0 = pk(v[j + 1][0], v[j + 1][1]), b1 = pk(v[j + 1][2], v[j + 1][3]);
       const auto rx = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
       const auto ry = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
       const u32x4 q = {rx[0], ry[0], rx[1], ry[1]};
@@ -524,7 +529,7 @@ DFU_DEV void st_row_bf16(rsrc_t r, int64_t rowe, bool okm, int n0w, int N, bool 
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0w + 16 * j + lcol;
-      st4_bf16(r, rowe + n, okm, n, N, n4, v[j]);
+      st4_bf16<H16>(r, rowe + n, okm, n, N, n4, v[j]);
     }
   }
 }

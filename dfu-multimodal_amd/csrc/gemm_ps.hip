@@ -121,7 +121,10 @@ DFU_DEV int ps_epi_stores(const GemmArgs& p) {
   const int per = bf16_out && p.n8 ? 2 * NI : 4 * NI * (p.n4 ? 1 : 4);
   // dGELU with column sums (p.stats): four more 16-B stores per wave (scalar: sixteen)
   const int cs = EPI == DFU_EPI_BF16_DGELU && p.stats ? (p.n4 ? 4 : 16) : 0;
-  if constexpr (EPI == DFU_EPI_X3_GELU) return 4 * (p.n8 ? 2 * NI : 4 * NI * (p.n4 ? 1 : 4));
+  const int per16 = p.n8 ? 2 * NI : 4 * NI * (p.n4 ? 1 : 4);  // one 16-bit output
+  if constexpr (EPI == DFU_EPI_X3_GELU) return 4 * per16;
+  if constexpr (EPI == DFU_EPI_F16_DUAL) return 2 * per16;
+  if constexpr (EPI == DFU_EPI_F16_GELU) return 3 * per16;
   return (EPI == DFU_EPI_BF16_GELU ? 2 * per : per) + cs;
 }
 
@@ -154,7 +157,8 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
     for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
   constexpr bool kBias = EPI == DFU_EPI_BF16 || EPI == DFU_EPI_BF16_GELU ||
                          EPI == DFU_EPI_F32_RESID || EPI == DFU_EPI_F32 ||
-                         EPI == DFU_EPI_X3_GELU;
+                         EPI == DFU_EPI_X3_GELU || EPI == DFU_EPI_F16_DUAL ||
+                         EPI == DFU_EPI_F16_GELU;
   if (kBias && p.bias) {
     float b2[2][4];
 #pragma unroll
@@ -241,6 +245,20 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
         st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
         st_row_bf16<2, kStAux>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, lo);
         st_row_bf16<2, kStAux>(rc, mc * p.ldc + 2 * N, okm, n0w, N, p.n8, n4, lane, g);
+      } else if constexpr (EPI == DFU_EPI_F16_DUAL) {
+        // fp16 operand of the next fp16 step, bf16 copy for the backward
+        st_row_bf16<2, kStAux, true>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+        st_row_bf16<2, kStAux>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, v);
+      } else if constexpr (EPI == DFU_EPI_F16_GELU) {
+        // gelu(pre) as fp16 (fc2's operand, column 0) and bf16 (the backward's h, column N)
+        float g[2][4], d[2][4];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
+        st_row_bf16<2, kStAux>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
+        st_row_bf16<2, kStAux, true>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, kStAux>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, g);
       } else if constexpr (EPI == DFU_EPI_F32) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
@@ -317,7 +335,9 @@ DFU_DEV void ps_epilogue(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, in
 
 // TMH: rows per tile half (128: the 256 x 256 tile; 96: 192 x 256, K-contiguous A only -- for
 // N = 768 outputs, whose 256-row tiling leaves 41 % of the CUs idle: 150 tiles at M = 12608).
-template <int AMODE, int BMODE, int EPI, int TMH = 128>
+// H16: fp16 A and B (v_mfma_f32_16x16x32_f16, the same fragment layout and rate as bf16): the
+// "parity" precision mode's ViT forward (dfu_gemm_desc.operand_type 1).
+template <int AMODE, int BMODE, int EPI, int TMH = 128, bool H16 = false>
 __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   constexpr bool AK_ = AMODE == DFU_OPND_KMAJOR;  // A K-contiguous (else MN-major: wgrad)
   constexpr bool BK_ = BMODE == DFU_OPND_KMAJOR;  // B K-contiguous (else MN-major)
@@ -484,8 +504,13 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     for (int i = 0; i < FMH; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[ha * FMH + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            fbh[kB2 ? hb : 0][j][ks], fa[i][ks], acc[ha * FMH + i][hb * 2 + j], 0, 0, 0);
+        if constexpr (H16)
+          acc[ha * FMH + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+              __builtin_bit_cast(f16x8, fbh[kB2 ? hb : 0][j][ks]),
+              __builtin_bit_cast(f16x8, fa[i][ks]), acc[ha * FMH + i][hb * 2 + j], 0, 0, 0);
+        else
+          acc[ha * FMH + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              fbh[kB2 ? hb : 0][j][ks], fa[i][ks], acc[ha * FMH + i][hb * 2 + j], 0, 0, 0);
     if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -607,6 +632,9 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
 }  // namespace
 
 #define PS(A, B, E) {A, B, E, T256x256ps, &gemm_ps<A, B, E>, PS_LDS, 512}
+#define PSH(E)                                                                            \
+  {DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, (E) | kF16Key, T256x256ps,                           \
+   &gemm_ps<DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, E, 128, true>, PS_LDS, 512}
 const Entry kTable256x256ps[] = {
     PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
     PS(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16_GELU),
@@ -618,8 +646,14 @@ const Entry kTable256x256ps[] = {
     PS(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_DGELU),
     PS(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_ADD),
     PS(DFU_OPND_MNMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_F32_ACC),  // weight gradients (split-K slabs)
+    // fp16 operands (epilogue key | kF16Key): the "parity" mode's ViT forward
+    PSH(DFU_EPI_F32),        // qkv (fp32 out: unused by the product path, tests)
+    PSH(DFU_EPI_F32_RESID),  // proj / fc2 with the fp32 residual
+    PSH(DFU_EPI_F16_DUAL),   // qkv: fp16 for the attention, bf16 for the backward
+    PSH(DFU_EPI_F16_GELU),   // fc1 + GELU
 };
 #undef PS
+#undef PSH
 const int kTable256x256psN = sizeof(kTable256x256ps) / sizeof(Entry);
 
 // 192 x 256 (K-contiguous A): the N = 768 ViT GEMMs (forward proj / fc2 with the fp32 residual,
@@ -631,6 +665,8 @@ const Entry kTable192x256ps[] = {
     PS192(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32),
     PS192(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16),
     PS192(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_BF16_ADD),
+    {DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_RESID | kF16Key, T192x256ps,
+     &gemm_ps<DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_RESID, 96, true>, PS_LDS, 512},
 };
 #undef PS192
 const int kTable192x256psN = sizeof(kTable192x256ps) / sizeof(Entry);

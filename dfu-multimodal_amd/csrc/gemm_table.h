@@ -4,6 +4,8 @@
 
 namespace dfu {
 typedef void (*gemm_fn)(const GemmArgs);
+// Entry.e of an fp16-operand kernel (dfu_gemm_desc.operand_type 1): the epilogue | kF16Key
+constexpr int kF16Key = 64;
 struct Entry {
   int a, b, e, tile;
   gemm_fn fn;

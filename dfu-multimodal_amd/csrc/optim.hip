@@ -83,10 +83,12 @@ DFU_DEV void adam_update(float& p, float g, float& m, float& v, const AdamCoef& 
 }
 
 // Optionally also writes the bf16 shadow of the updated parameters (the GEMM operand copy),
-// so no per-step cast kernels are needed.
+// so no per-step cast kernels are needed, and an fp16 shadow (the "parity" precision mode's
+// ViT forward operands).
 __device__ __forceinline__ void adamw_vec4(float* __restrict__ p, const float* __restrict__ g,
                                            float* __restrict__ m, float* __restrict__ v,
-                                           bf16_t* __restrict__ shadow, int64_t i, f32x4 pp,
+                                           bf16_t* __restrict__ shadow,
+                                           bf16_t* __restrict__ shadow16, int64_t i, f32x4 pp,
                                            f32x4 gg, f32x4 mm, f32x4 vv, const AdamCoef& a,
                                            float b1, float b2, float eps) {
 #pragma unroll
@@ -99,6 +101,7 @@ __device__ __forceinline__ void adamw_vec4(float* __restrict__ p, const float* _
   ((f32x4*)m)[i] = mm;
   ((f32x4*)v)[i] = vv;
   if (shadow) ((u32x2*)shadow)[i] = (u32x2){pack2(pp[0], pp[1]), pack2(pp[2], pp[3])};
+  if (shadow16) ((u32x2*)shadow16)[i] = (u32x2){pack2h(pp[0], pp[1]), pack2h(pp[2], pp[3])};
 }
 
 // Each thread handles ADAM_UNROLL float4 groups per grid-stride pass, spaced one grid apart so
@@ -114,7 +117,8 @@ __global__ void __launch_bounds__(256) k_adamw_flat(float* __restrict__ p,
                                                     int64_t n, float lr, float b1, float b2,
                                                     float eps, float wd,
                                                     const int64_t* __restrict__ step_dev,
-                                                    bf16_t* __restrict__ shadow) {
+                                                    bf16_t* __restrict__ shadow,
+                                                    bf16_t* __restrict__ shadow16) {
   const AdamCoef a = adam_coef(*step_dev, lr, b1, b2, wd);
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -131,10 +135,12 @@ __global__ void __launch_bounds__(256) k_adamw_flat(float* __restrict__ p,
     }
 #pragma unroll
     for (int u = 0; u < ADAM_UNROLL; ++u)
-      adamw_vec4(p, g, m, v, shadow, i + u * stride, pp[u], gg[u], mm[u], vv[u], a, b1, b2, eps);
+      adamw_vec4(p, g, m, v, shadow, shadow16, i + u * stride, pp[u], gg[u], mm[u], vv[u], a, b1,
+                 b2, eps);
   }
   for (; i < n4; i += stride)
-    adamw_vec4(p, g, m, v, shadow, i, ((f32x4*)p)[i], ((const f32x4*)g)[i], ((f32x4*)m)[i],
+    adamw_vec4(p, g, m, v, shadow, shadow16, i, ((f32x4*)p)[i], ((const f32x4*)g)[i],
+               ((f32x4*)m)[i],
                ((f32x4*)v)[i], a, b1, b2, eps);
   for (int64_t k = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
        k += stride) {
@@ -142,6 +148,7 @@ __global__ void __launch_bounds__(256) k_adamw_flat(float* __restrict__ p,
     adam_update(pe, g[k], me, ve, a, b1, b2, eps);
     p[k] = pe; m[k] = me; v[k] = ve;
     if (shadow) shadow[k] = f2bf(pe);
+    if (shadow16) shadow16[k] = (bf16_t)(pack2h(pe, 0.f) & 0xffffu);
   }
 }
 
@@ -202,13 +209,13 @@ extern "C" int dfu_ce_weighted_bwd(const float* saved, const float* grad_loss, i
 extern "C" int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                               int64_t n, float lr, float beta1, float beta2, float eps,
                               float weight_decay, const int64_t* step_dev, void* shadow_bf16,
-                              void* stream) {
+                              void* shadow_f16, void* stream) {
   DFU_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step_dev && n > 0,
                 "dfu_adamw_flat: bad args");
   DFU_CHECK_ARG(((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 &&
                     ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0 &&
-                    ((uintptr_t)shadow_bf16 & 7) == 0,
-                "dfu_adamw_flat: buffers must be 16-byte aligned (shadow 8-byte)");
+                    ((uintptr_t)shadow_bf16 & 7) == 0 && ((uintptr_t)shadow_f16 & 7) == 0,
+                "dfu_adamw_flat: buffers must be 16-byte aligned (shadows 8-byte)");
   int64_t blocks = (n / 4 + 255) / 256;
   static const int64_t cap = [] {  // one block per CU (see k_adamw_flat)
     int dev = 0, cus = 256;
@@ -221,7 +228,7 @@ extern "C" int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, f
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_adamw_flat<1>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param,
                      grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step_dev,
-                     (bf16_t*)shadow_bf16);
+                     (bf16_t*)shadow_bf16, (bf16_t*)shadow_f16);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -212,7 +212,9 @@ __global__ void k_avgpool_fwd_x3(const bf16_t* __restrict__ x3, int B, int HW, i
 
 // ---------------------------------------------------------------- LayerNorm
 // timm LayerNorm over fp32 rows of D (one wave per row, as k_ln_fwd) -> triple [rows][3D]
-// and plain bf16 [rows][D]; mean / rstd saved for the backward.
+// (H16: fp16 [rows][D], the fp16 forward's GEMM operand) and plain bf16 [rows][D]; mean / rstd
+// saved for the backward.
+template <bool H16>
 __global__ void k_ln_fwd_x3(const float* __restrict__ x, int64_t ldx, int rows, int D,
                             const float* __restrict__ gamma, const float* __restrict__ beta,
                             float eps, bf16_t* __restrict__ out3, bf16_t* __restrict__ out_bf,
@@ -258,7 +260,10 @@ __global__ void k_ln_fwd_x3(const float* __restrict__ x, int64_t ldx, int rows, 
     ld8_f32(beta + 8 * j, b);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
-    st_triple8(out3 + (int64_t)row * 3 * D, D, 8 * j, o, 0);
+    if constexpr (H16)
+      *(u32x4*)(out3 + (int64_t)row * D + 8 * j) = pack8h(o);
+    else
+      st_triple8(out3 + (int64_t)row * 3 * D, D, 8 * j, o, 0);
     *(u32x4*)(out_bf + (int64_t)row * D + 8 * j) = pack8(o);
   }
 }
@@ -361,8 +366,24 @@ extern "C" int dfu_layernorm_fwd_x3(const float* x, int64_t ldx, int32_t rows, i
                 "dfu_layernorm_fwd_x3: bad args (D %% 8 == 0, D <= 1024)");
   if (rows == 0) return DFU_OK;
   const int wpb = 4;
-  hipLaunchKernelGGL(k_ln_fwd_x3, dim3((rows + wpb - 1) / wpb), dim3(64 * wpb), 0,
+  hipLaunchKernelGGL(k_ln_fwd_x3<false>, dim3((rows + wpb - 1) / wpb), dim3(64 * wpb), 0,
                      (hipStream_t)stream, x, ldx, rows, D, gamma, beta, eps, (bf16_t*)out3,
+                     (bf16_t*)out_bf16, mean, rstd);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_layernorm_fwd_h16(const float* x, int64_t ldx, int32_t rows, int32_t D,
+                                     const float* gamma, const float* beta, float eps,
+                                     void* out_f16, void* out_bf16, float* mean, float* rstd,
+                                     void* stream) {
+  DFU_CHECK_ARG(x && gamma && beta && out_f16 && out_bf16 && mean && rstd && D % 8 == 0 &&
+                    D <= 1024 && ldx % 4 == 0,
+                "dfu_layernorm_fwd_h16: bad args (D %% 8 == 0, D <= 1024)");
+  if (rows == 0) return DFU_OK;
+  const int wpb = 4;
+  hipLaunchKernelGGL(k_ln_fwd_x3<true>, dim3((rows + wpb - 1) / wpb), dim3(64 * wpb), 0,
+                     (hipStream_t)stream, x, ldx, rows, D, gamma, beta, eps, (bf16_t*)out_f16,
                      (bf16_t*)out_bf16, mean, rstd);
   DFU_LAUNCH_CHECK();
   return DFU_OK;

@@ -24,7 +24,9 @@ OPND_KMAJOR, OPND_MNMAJOR, OPND_CONV_FWD, OPND_CONV_DGRAD, OPND_CONV_DGRAD_W, OP
 # enum dfu_epilogue
 (EPI_BF16, EPI_BF16_RELU, EPI_BF16_GELU, EPI_F32, EPI_F32_RESID, EPI_BF16_DGELU, EPI_BF16_ADD,
  EPI_F32_ACC, EPI_F32_ACC_CONVW, EPI_BF16_STATS, EPI_PATCH, EPI_F32_STATS,
- EPI_BF16_DSTATS, EPI_X3_GELU) = range(14)
+ EPI_BF16_DSTATS, EPI_X3_GELU, EPI_F16_DUAL, EPI_F16_GELU) = range(16)
+# dfu_gemm_desc.operand_type
+OPERAND_BF16, OPERAND_F16 = 0, 1
 
 DFU_E_INVALID = 1001
 DFU_E_UNSUPPORTED = 1002
@@ -91,6 +93,7 @@ PROTOTYPES = {
     "dfu_cast_rows_bf16": [P, I64, P, I64, I32, I32, P],
     "dfu_transpose_bf16": [P, I32, I32, P],
     "dfu_cast_rows_f32": [P, I64, P, I64, I32, I32, P],
+    "dfu_cast_rows_f16": [P, I64, P, I64, I32, I32, P],
     "dfu_im2col_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],
     "dfu_patchify_f32": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
     "dfu_col2im_f32": [P, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P],
@@ -119,6 +122,7 @@ PROTOTYPES = {
     "dfu_reduce_partials": [P, I32, I32, I32, P, P, P],
     "dfu_reduce_partials_batch": [ctypes.POINTER(ReduceEntry), I32, P],
     "dfu_attention_fwd": [P, I32, I32, I32, I32, F, P, P, P],
+    "dfu_attention_fwd_f16": [P, I32, I32, I32, I32, F, P, P, P, P],
     "dfu_attention_bwd": [P, P, P, P, I32, I32, I32, I32, F, P, P, P],
     "dfu_attention_npad": [I32],
     "dfu_vit_cls_rows": [P, P, P, I32, I32, I32, P],
@@ -136,7 +140,7 @@ PROTOTYPES = {
     "dfu_ce_weighted_fwd": [P, P, P, I32, I32, P, P, P],
     "dfu_ce_weighted_bwd": [P, P, I32, I32, P, P],
     "dfu_adamw": [P, P, P, P, P, I32, P, I32, F, F, F, F, F, P, P],
-    "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P],
+    "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P, P],
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
     "dfu_softmax_rows": [P, I32, I32, P, P],
@@ -149,6 +153,7 @@ PROTOTYPES = {
     "dfu_maxpool_fwd_x3": [P, I32, I32, I32, I32, P, P, P, I32, I32, P],
     "dfu_avgpool_fwd_x3": [P, I32, I32, I32, P, P],
     "dfu_layernorm_fwd_x3": [P, I64, I32, I32, P, P, F, P, P, P, P, P],
+    "dfu_layernorm_fwd_h16": [P, I64, I32, I32, P, P, F, P, P, P, P, P],
     "dfu_gelu_x3": [P, I64, I32, P, P, P, P],
     "dfu_attention_fwd_f32": [P, I32, I32, I32, I32, F, I32, P, P, P, P, P],
     "dfu_resize_ksize": [I32, I32],

@@ -39,17 +39,26 @@ F32 = torch.float32
 #   stay fp32 between kernels and attention runs in fp32, so the fusion logits meet north_star's
 #   "within 1e-3 abs of the reference CPU path" against the fp32 oracle.  The backward pass is
 #   the bf16 one (it reads the plain bf16 tensors the split kernels also write).
+# "fp16" (a ViT Block stage only): the block's four Linears and its attention on fp16 MFMA
+#   operands (11-bit significands, fp32 accumulate; fp32 residual stream, LayerNorm statistics
+#   and softmax), writing the same bf16 tensors for the bf16 backward.
+# "parity": the headline mode -- per stage the precision its module class names in
+#   ``dfu_parity_precision``: every ResNet stage bf16x3, every ViT Block fp16 (the cheapest
+#   assignment measured to keep the fusion logits within north_star's 1e-3 of the fp32 oracle
+#   with margin: profiles/r16_precision_study.md).
 # "mixed": per stage -- a ResNet Bottleneck / ViT Block (or the ResNet module itself, for the
-#   stem) whose ``dfu_precision`` attribute is "bf16" runs the bf16 forward, every other stage
-#   the bf16x3 one (models.precision.apply_policy sets the attributes; a bf16 stage's output
-#   enters the next bf16x3 stage as an exact bf16 value, a bf16x3 stage's output reaches a bf16
-#   stage as the bf16 copy it also writes).
-PRECISIONS = ("bf16", "bf16x3", "mixed")
+#   stem) runs its ``dfu_precision`` attribute's mode ("bf16", "bf16x3", ViT Blocks also
+#   "fp16"), bf16x3 where unset (models.precision.apply_policy sets the attributes).  A bf16 or
+#   fp16 stage's output enters the next bf16x3 stage as its exact bf16 / fp32 value; a bf16x3
+#   stage's output reaches a bf16 stage as the bf16 copy it also writes.
+PRECISIONS = ("bf16", "bf16x3", "mixed", "parity")
+STAGE_MODES = ("bf16", "bf16x3", "fp16")
 _precision = ["bf16"]
 
 
 def set_precision(mode):
-    """Select the forward precision ("bf16", "bf16x3" or "mixed"); returns the previous mode."""
+    """Select the forward precision ("bf16", "bf16x3", "mixed" or "parity"); returns the
+    previous mode."""
     if mode not in PRECISIONS:
         raise ValueError(f"precision must be one of {PRECISIONS}, got {mode!r}")
     old = _precision[0]
@@ -77,12 +86,28 @@ class precision:
         return False
 
 
-def _x3(mod=None):
-    """Does the stage `mod` (None: a stage without a policy of its own) run bf16x3?"""
+def stage_mode(mod=None):
+    """The forward precision of stage `mod` (None: a stage without a policy of its own) under
+    the current mode: "bf16", "bf16x3" or "fp16"."""
     p = _precision[0]
     if p == "mixed":
-        return getattr(mod, "dfu_precision", None) != "bf16"
-    return p == "bf16x3"
+        m = getattr(mod, "dfu_precision", None) or "bf16x3"
+    elif p == "parity":
+        m = getattr(mod, "dfu_parity_precision", None) or "bf16x3"
+    else:
+        return p
+    if m not in STAGE_MODES:
+        raise ValueError(f"stage precision must be one of {STAGE_MODES}, got {m!r}")
+    return m
+
+
+def _x3(mod=None):
+    """Does the stage `mod` run bf16x3?"""
+    return stage_mode(mod) == "bf16x3"
+
+
+def _per_stage():
+    return _precision[0] in ("mixed", "parity")
 
 # ------------------------------------------------------------------------- grad plumbing
 _grad_ready_hooks = []
@@ -353,6 +378,23 @@ def weight_bf16_rows(w, ld=None):
             w._dfu_sgen = getattr(w, "_dfu_sgen", 0) - 1  # any transposed copy is now stale
         return sh
     return ops.cast_rows_bf16(w2, ld_out=ld)
+
+
+def weight_f16_rows(w):
+    """fp32 [N, K...] parameter -> fp16 [N, K] GEMM operand (the "fp16" stage precision).
+    FusedAdamW-managed parameters get an fp16 shadow the optimizer kernel keeps current from the
+    first use on (optim.FlatParams.enable_f16; re-cast only after an outside edit); others are
+    cast per call."""
+    flat = getattr(w, "_dfu_flat", None)
+    if flat is not None and flat.shadow is not None:
+        if flat.shadow16 is None:
+            flat.enable_f16()
+        sh = w._dfu_shadow16
+        if w._version != getattr(w, "_dfu_shadow16_version", -1):
+            ops.cast_rows_f16(_rows2d(w.detach()), out=sh)
+            w._dfu_shadow16_version = w._version
+        return sh
+    return ops.cast_rows_f16(_rows2d(w.detach()))
 
 
 def weight_bf16_T(w):
@@ -851,10 +893,9 @@ class BottleneckFn(torch.autograd.Function):
 class AvgPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
-        # bf16x3: the triple the producer attached; "mixed": that triple if the last block ran
-        # bf16x3 (a bf16 block's output is pooled in bf16)
-        x3 = _take_x3(x) if _x3() and (get_precision() != "mixed" or hasattr(x, "_dfu_x3")) \
-            else None
+        # bf16x3: the triple the producer attached; per-stage modes: that triple if the last block
+        # ran bf16x3 (a bf16 block's output is pooled in bf16)
+        x3 = _take_x3(x) if _x3() and (not _per_stage() or hasattr(x, "_dfu_x3")) else None
         x = nhwc_bf16(x.detach())
         B, C, H, W = x.shape
         ctx.shape = (B, C, H, W)
@@ -1036,9 +1077,13 @@ class ViTBlockFn(torch.autograd.Function):
         wfc2 = weight_bf16_rows(mlp.fc2.weight)
         Dh = wfc1.shape[0]
         bias = lambda lin: lin.bias.detach() if lin.bias is not None else None  # noqa: E731
-        if _x3(blk):
+        mode = stage_mode(blk)
+        if mode == "bf16x3":
             return ViTBlockFn._forward_x3(ctx, blk, x2, B, T, D, H, dh, rows, wqkv, wproj, wfc1,
                                           wfc2, bias)
+        if mode == "fp16":
+            return ViTBlockFn._forward_h16(ctx, blk, x2, B, T, D, H, dh, rows, wqkv, wproj, wfc1,
+                                           wfc2, bias)
         # attention branch
         xn1 = _empty((rows, D), BF16, dev)
         m1, r1 = _ln_fwd(x2, blk.norm1, rows, D, xn1)
@@ -1126,6 +1171,64 @@ class ViTBlockFn(torch.autograd.Function):
         ops.gemm(rows, D, 3 * Dh, h3, 3 * Dh, weight_x3_rows(mlp.fc2.weight), 3 * Dh,
                  xo.view(rows, D), D, epilogue=L.EPI_F32_RESID, bias=bias(mlp.fc2), aux=xm,
                  ldaux=D, tile=tl_d)
+        ctx.blk = blk
+        ctx.dims = (B, T, D, H, dh, Dh)
+        ctx.out_ref = weakref.ref(xo)
+        ctx.beside = _VIT_WGRAD_STREAM and _concurrent_encoders[0] == 0
+        ctx.save_for_backward(x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv,
+                              wproj, wfc1, wfc2)
+        return xo
+
+    @staticmethod
+    def _forward_h16(ctx, blk, x2, B, T, D, H, dh, rows, wqkv, wproj, wfc1, wfc2, bias):
+        """fp16 forward: the four Linears on fp16 operands (fp32 accumulate; persistent
+        256 x 256 tile, 192 x 256 for the N = 768 GEMMs when the ViT runs alone), the fp16
+        attention, fp32 residual stream; saves the same bf16 tensors as the bf16 forward (every
+        fp16 producer also writes the bf16 copy)."""
+        attn, mlp = blk.attn, blk.mlp
+        dev = x2.device
+        Dh = wfc1.shape[0]
+        F16 = torch.float16
+
+        def ln(xsrc, norm):
+            t16 = _empty((rows, D), F16, dev)
+            tb = _empty((rows, D), BF16, dev)
+            mean = _empty((rows,), F32, dev)
+            rstd = _empty((rows,), F32, dev)
+            ops.layernorm_fwd_h16(xsrc, D, rows, D, norm.weight, norm.bias, norm.eps, t16, tb,
+                                  mean, rstd)
+            return t16, tb, mean, rstd
+
+        h16 = L.OPERAND_F16
+        ctx.t768 = _t768()
+        tl_d = ctx.t768 or 8
+        xn1_16, xn1, m1, r1 = ln(x2, blk.norm1)
+        qkv16 = _empty((rows, 3 * D), F16, dev)
+        qkv = _empty((rows, 3 * D), BF16, dev)  # the backward's operand
+        ops.gemm(rows, 3 * D, D, xn1_16, D, weight_f16_rows(attn.qkv.weight), D, qkv16, 3 * D,
+                 epilogue=L.EPI_F16_DUAL, bias=bias(attn.qkv), aux_out=qkv, ldaux_out=3 * D,
+                 tile=8, operand_type=h16)
+        del xn1_16
+        o16, o, lse = ops.attention_fwd_f16(qkv16, B, T, H, dh, attn.scale)
+        del qkv16
+        xm = _empty((rows, D), F32, dev)
+        ops.gemm(rows, D, D, o16, D, weight_f16_rows(attn.proj.weight), D, xm, D,
+                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D, tile=tl_d,
+                 operand_type=h16)
+        del o16
+        xn2_16, xn2, m2, r2 = ln(xm, blk.norm2)
+        # fc1 + GELU: [fp16 gelu | bf16 gelu] (fc2's operand, the backward's h) + bf16 gelu'
+        h2 = _empty((rows, 2 * Dh), BF16, dev)
+        dgl = _empty((rows, Dh), BF16, dev)
+        ops.gemm(rows, Dh, D, xn2_16, D, weight_f16_rows(mlp.fc1.weight), D, h2, 2 * Dh,
+                 epilogue=L.EPI_F16_GELU, bias=bias(mlp.fc1), aux_out=dgl, ldaux_out=Dh, tile=8,
+                 operand_type=h16)
+        del xn2_16
+        h = h2[:, Dh:]
+        xo = _empty((B, T, D), F32, dev)
+        ops.gemm(rows, D, Dh, h2, 2 * Dh, weight_f16_rows(mlp.fc2.weight), Dh, xo.view(rows, D),
+                 D, epilogue=L.EPI_F32_RESID, bias=bias(mlp.fc2), aux=xm, ldaux=D, tile=tl_d,
+                 operand_type=h16)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)

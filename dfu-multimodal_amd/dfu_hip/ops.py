@@ -13,6 +13,7 @@ from ._lib import check
 
 BF16 = torch.bfloat16
 F32 = torch.float32
+F16 = torch.float16
 
 
 def lib():
@@ -232,6 +233,21 @@ def cast_rows_bf16(x, ld_out=None, out=None):
         out = torch.empty((rows, ld_out), dtype=BF16, device=x.device)
     check(lib().dfu_cast_rows_bf16(ptr(x2), x2.stride(0), ptr(out), ld_out, rows, cols,
                                    stream_ptr()), "dfu_cast_rows_bf16")
+    return out
+
+
+def cast_rows_f16(x, ld_out=None, out=None):
+    """fp32 [rows, cols] -> fp16 [rows, ld_out] (RNE, zero-padded columns)."""
+    _req(x, F32, "cast_rows_f16")
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(1) != 1:
+        x2 = x2.contiguous()
+    rows, cols = x2.shape
+    ld_out = cols if ld_out is None else ld_out
+    if out is None:
+        out = torch.empty((rows, ld_out), dtype=F16, device=x.device)
+    check(lib().dfu_cast_rows_f16(ptr(x2), x2.stride(0), ptr(out), ld_out, rows, cols,
+                                  stream_ptr()), "dfu_cast_rows_f16")
     return out
 
 
@@ -567,6 +583,18 @@ def attention_fwd(qkv, B, N, H, dh, scale):
     return o, lse
 
 
+def attention_fwd_f16(qkv16, B, N, H, dh, scale):
+    """The fp16 forward ("parity" mode): qkv fp16 [B*N][3*H*dh] -> (o fp16, o bf16, lse)."""
+    _req(qkv16, F16, "attention_fwd_f16")
+    assert qkv16.is_contiguous() and qkv16.shape == (B * N, 3 * H * dh)
+    o16 = torch.empty((B * N, H * dh), dtype=F16, device=qkv16.device)
+    o = torch.empty((B * N, H * dh), dtype=BF16, device=qkv16.device)
+    lse = torch.empty((B * H, attention_npad(N)), dtype=F32, device=qkv16.device)
+    check(lib().dfu_attention_fwd_f16(ptr(qkv16), B, N, H, dh, scale, ptr(o16), ptr(o), ptr(lse),
+                                      stream_ptr()), "dfu_attention_fwd_f16")
+    return o16, o, lse
+
+
 def attention_bwd(qkv, o, dout, lse, B, N, H, dh, scale, dqkv=None):
     delta = torch.empty((B * H, attention_npad(N)), dtype=F32, device=qkv.device)
     if dqkv is None:
@@ -681,9 +709,10 @@ def ce_weighted_bwd(saved, grad_loss):
     return out
 
 
-def adamw_flat(p, g, m, v, lr, b1, b2, eps, wd, step_dev, shadow=None):
+def adamw_flat(p, g, m, v, lr, b1, b2, eps, wd, step_dev, shadow=None, shadow16=None):
     check(lib().dfu_adamw_flat(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd,
-                               ptr(step_dev), ptr(shadow), stream_ptr()), "dfu_adamw_flat")
+                               ptr(step_dev), ptr(shadow), ptr(shadow16), stream_ptr()),
+          "dfu_adamw_flat")
 
 
 def step_increment(step_dev):
@@ -791,6 +820,13 @@ def layernorm_fwd_x3(x, ldx, rows, D, gamma, beta, eps, out3, out_bf16, mean, rs
     check(lib().dfu_layernorm_fwd_x3(ptr(x), ldx, rows, D, ptr(gamma), ptr(beta), eps, ptr(out3),
                                      ptr(out_bf16), ptr(mean), ptr(rstd), stream_ptr()),
           "dfu_layernorm_fwd_x3")
+
+
+def layernorm_fwd_h16(x, ldx, rows, D, gamma, beta, eps, out16, out_bf16, mean, rstd):
+    _req(out16, F16, "layernorm_fwd_h16")
+    check(lib().dfu_layernorm_fwd_h16(ptr(x), ldx, rows, D, ptr(gamma), ptr(beta), eps,
+                                      ptr(out16), ptr(out_bf16), ptr(mean), ptr(rstd),
+                                      stream_ptr()), "dfu_layernorm_fwd_h16")
 
 
 def gelu_x3(hpre):

@@ -80,6 +80,7 @@ class FlatParams:
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
         self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=dev) if dev.type == "cuda" \
             else None
+        self.shadow16 = None  # fp16 shadow, from the first fp16-stage forward on (enable_f16)
         self.gen = 0         # bumped whenever every shadow is rewritten (step, refresh)
         self.t_params = []   # parameters with a transposed (p._dfu_shadow_T) or flipped
         self.t_pairs = []    # (p._dfu_shadow_F) shadow, and their (src, dst) transpose jobs
@@ -99,13 +100,31 @@ class FlatParams:
         self.refresh_shadow()
 
     def refresh_shadow(self):
-        """Re-cast every parameter into the bf16 shadow and mark it current."""
+        """Re-cast every parameter into the bf16 (and fp16) shadow and mark it current."""
         if self.shadow is None:
             return
         ops.cast_rows_bf16(self.data.view(1, -1), out=self.shadow.view(1, -1))
         for p in self.params:
             p._dfu_shadow_version = p._version
+        if self.shadow16 is not None:
+            self._cast_f16()
         self.shadows_rewritten()
+
+    def _cast_f16(self):
+        ops.cast_rows_f16(self.data.view(1, -1), out=self.shadow16.view(1, -1))
+        for p in self.params:
+            p._dfu_shadow16_version = p._version
+
+    def enable_f16(self):
+        """Keep an fp16 shadow of every parameter from now on (the "fp16" stage precision's
+        GEMM operands, functional.weight_f16_rows): cast once here, then written by every AdamW
+        step beside the bf16 shadow (2 B per parameter)."""
+        if self.shadow16 is not None or self.shadow is None:
+            return
+        self.shadow16 = torch.empty(self.numel, dtype=torch.float16, device=self.data.device)
+        for p, o in zip(self.params, self.offsets):
+            p._dfu_shadow16 = self.shadow16[o:o + p.numel()].view(p.shape[0], -1)
+        self._cast_f16()
 
     def add_transposed(self, p):
         """Give parameter p a transposed bf16 shadow, kept current from now on."""
@@ -267,7 +286,8 @@ class FusedAdamW(torch.optim.Optimizer):
         ops.adamw_flat(fp.data[lo:hi], fp.grad[lo:hi], self.exp_avg[lo:hi],
                        self.exp_avg_sq[lo:hi], g["lr"], b1, b2, g["eps"], g["weight_decay"],
                        self.step_dev,
-                       shadow=None if fp.shadow is None else fp.shadow[lo:hi])
+                       shadow=None if fp.shadow is None else fp.shadow[lo:hi],
+                       shadow16=None if fp.shadow16 is None else fp.shadow16[lo:hi])
 
     @torch.no_grad()
     def step(self, closure=None):

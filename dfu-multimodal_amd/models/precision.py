@@ -1,16 +1,21 @@
-"""Per-stage forward precision of the HIP encoders (functional.set_precision("mixed")).
+"""Per-stage forward precision of the HIP encoders.
 
 A stage is the ResNet stem ("resnet.stem"), a ResNet Bottleneck ("resnet.layer<i>.<j>") or a
-ViT Block ("vit.blocks.<k>").  A *policy* names the stages whose forward runs in plain bf16;
-every other stage runs bf16x3 (fp32-accurate).  Rounding introduced late in an encoder is
-amplified by fewer layers than rounding introduced early, so the cheapest policy that keeps the
-fusion logits within north_star's 1e-3 of the fp32 oracle runs a suffix of each encoder in bf16.
-The shipped policy (PARITY_POLICY) and the study it comes from are in DESIGN.md §4 and
-profiles/r16_precision_study.{json,md} (tools/precision_policy_study.py).
+ViT Block ("vit.blocks.<k>").  Its forward runs in one of functional.STAGE_MODES: "bf16" (bf16
+operands and activations), "bf16x3" (fp32-accurate split-bf16 operands) or, for a ViT Block,
+"fp16" (fp16 operands, fp32 accumulation and residual stream).  The backward is bf16 in every
+mode.
+
+  * functional.precision("parity") -- the headline mode -- runs each stage at its module
+    class's ``dfu_parity_precision``: ResNet stages bf16x3, ViT Blocks fp16.  It is the cheapest
+    assignment the per-stage study found to keep the fusion logits within half of north_star's
+    1e-3 of the fp32 oracle on every seed (profiles/r16_precision_study.md,
+    tools/precision_policy_study.py): the random-init ResNet amplifies rounding ~30x more than
+    the ViT, so its forward needs ~2^-17 products while the ViT's holds the bar with fp16's
+    2^-11 -- and bf16 anywhere, even in the last ResNet block or ViT Block alone, costs 4-7e-4.
+  * functional.precision("mixed") runs each stage at its ``dfu_precision`` attribute (bf16x3
+    where unset), which apply_policy sets -- the study's tool.
 """
-# The policy the bench's headline mode runs ("parity": the cheapest stage assignment measured to
-# hold max |logits - fp32 oracle| <= 5e-4 at C3 B = 64 on every seed of the study).
-PARITY_POLICY = ()
 
 
 def encoders(model):
@@ -27,7 +32,7 @@ def encoders(model):
 
 
 def stages(model):
-    """Ordered {name: module} of every stage the policy can name."""
+    """Ordered {name: module} of every stage a policy can name."""
     r, v = encoders(model)
     out = {}
     if r is not None:
@@ -41,27 +46,39 @@ def stages(model):
     return out
 
 
-def apply_policy(model, bf16_stages):
-    """Mark the named stages bf16 and every other stage bf16x3 (effective under
-    functional.precision("mixed")).  Unknown names raise; returns the model."""
+def apply_policy(model, policy):
+    """Set every stage's ``dfu_precision`` (effective under functional.precision("mixed")):
+    `policy` maps stage names to modes (every other stage bf16x3), or is an iterable of stage
+    names that run bf16.  Unknown names or modes raise; returns the model."""
+    from dfu_hip.functional import STAGE_MODES
     st = stages(model)
-    names = set(bf16_stages)
-    bad = names - set(st)
+    pol = dict(policy) if isinstance(policy, dict) else {n: "bf16" for n in policy}
+    bad = set(pol) - set(st)
     if bad:
         raise ValueError(f"unknown stages {sorted(bad)}; known: {list(st)}")
+    for name, mode in pol.items():
+        if mode not in STAGE_MODES or (mode == "fp16" and not name.startswith("vit.")):
+            raise ValueError(f"stage {name}: unsupported precision {mode!r}")
     for name, m in st.items():
-        m.dfu_precision = "bf16" if name in names else "bf16x3"
+        m.dfu_precision = pol.get(name, "bf16x3")
     return model
 
 
 def suffix(model, resnet_blocks=0, vit_blocks=0):
-    """The policy that runs the last `resnet_blocks` Bottlenecks and the last `vit_blocks` ViT
-    Blocks in bf16."""
+    """The bf16 policy that runs the last `resnet_blocks` Bottlenecks and the last `vit_blocks`
+    ViT Blocks in bf16."""
     names = list(stages(model))
     rn = [n for n in names if n.startswith("resnet.layer")]
     vn = [n for n in names if n.startswith("vit.")]
     return tuple((rn[len(rn) - resnet_blocks:] if resnet_blocks else []) +
                  (vn[len(vn) - vit_blocks:] if vit_blocks else []))
+
+
+def parity_policy(model, vit_x3_blocks=0):
+    """The "parity" assignment as an explicit policy (ViT Blocks fp16, ResNet bf16x3), with the
+    first `vit_x3_blocks` ViT Blocks bf16x3 instead (the study's variants)."""
+    names = [n for n in stages(model) if n.startswith("vit.")]
+    return {n: ("bf16x3" if k < vit_x3_blocks else "fp16") for k, n in enumerate(names)}
 
 
 def clear_policy(model):
@@ -71,4 +88,4 @@ def clear_policy(model):
     return model
 
 
-__all__ = ["PARITY_POLICY", "apply_policy", "clear_policy", "encoders", "stages", "suffix"]
+__all__ = ["apply_policy", "clear_policy", "encoders", "parity_policy", "stages", "suffix"]

@@ -26,6 +26,8 @@ class Bottleneck(tnn.Module):
     """torchvision Bottleneck (ResNet v1.5: stride on the 3x3 conv)."""
 
     expansion = 4
+    # forward precision under functional.precision("parity") (models/precision.py)
+    dfu_parity_precision = "bf16x3"
 
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()

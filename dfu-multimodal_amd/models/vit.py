@@ -63,6 +63,9 @@ class Mlp(tnn.Module):
 
 
 class Block(tnn.Module):
+    # forward precision under functional.precision("parity") (models/precision.py)
+    dfu_parity_precision = "fp16"
+
     def __init__(self, dim, num_heads, mlp_ratio=4.0, qkv_bias=True):
         super().__init__()
         self.norm1 = hnn.LayerNorm(dim, eps=1e-6)

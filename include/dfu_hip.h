@@ -82,10 +82,17 @@ enum dfu_epilogue {
   DFU_EPI_BF16_DSTATS = 12,  /* retired (round 4: BN backward sums in the dgrad epilogue
                                 measured slower than the separate reduce); reserved, returns
                                 DFU_E_UNSUPPORTED                                            */
-  DFU_EPI_X3_GELU = 13       /* bf16x3 forward of timm Mlp.fc1 + GELU: pre = acc + bias (fp32),
+  DFU_EPI_X3_GELU = 13,      /* bf16x3 forward of timm Mlp.fc1 + GELU: pre = acc + bias (fp32),
                                 C = the A-operand triple [hi | lo | hi] of gelu(pre), bf16
                                 [M][3N] (ldc >= 3N; segments at columns 0, N, 2N), aux_out
                                 bf16 = gelu'(pre).  Persistent 256x256 tile only.            */
+  DFU_EPI_F16_DUAL = 14,     /* v = alpha*acc + bias: C fp16 = v (the next fp16 GEMM's or the
+                                fp16 attention's operand), aux_out bf16 = v (what the bf16
+                                backward saves; may be NULL).  operand_type 1 only.           */
+  DFU_EPI_F16_GELU = 15      /* fp16 forward of timm Mlp.fc1 + GELU: pre = acc + bias: C =
+                                [fp16 gelu(pre) | bf16 gelu(pre)], 16-bit [M][2N] (ldc >= 2N;
+                                fc2's fp16 operand at column 0, the backward's bf16 h at
+                                column N), aux_out bf16 = gelu'(pre).  operand_type 1 only.  */
 };
 
 typedef struct dfu_gemm_desc {
@@ -195,6 +202,10 @@ typedef struct dfu_transpose_job {
 } dfu_transpose_job;
 int dfu_transpose_bf16(const dfu_transpose_job* jobs, int32_t njobs, int32_t ntiles,
                        void* stream);
+/* fp32 [rows][cols] -> fp16 [rows][ld_out] (RNE; cols..ld_out-1 zero-filled): the fp16
+ * operands of the "parity" precision mode's ViT forward. */
+int dfu_cast_rows_f16(const float* in, int64_t ld_in, void* out, int64_t ld_out, int32_t rows,
+                      int32_t cols, void* stream);
 /* bf16 [rows][cols] (ld_in) -> fp32 [rows][cols] (ld_out). */
 int dfu_cast_rows_f32(const void* in, int64_t ld_in, float* out, int64_t ld_out, int32_t rows,
                       int32_t cols, void* stream);
@@ -338,6 +349,11 @@ int dfu_reduce_partials_batch(const dfu_reduce_entry* entries, int32_t n, void* 
  * Linear output), o bf16 [B*N][H][dh], lse fp32 [B*H][Npad]. dh == 64, N <= 256. */
 int dfu_attention_fwd(const void* qkv, int32_t B, int32_t N, int32_t H, int32_t dh, float scale,
                       void* o, float* lse, void* stream);
+/* The "parity" precision mode's fp16 forward: qkv fp16 (the DFU_EPI_F16_DUAL output), the same
+ * kernel on v_mfma_f32_16x16x32_f16 with fp16 probabilities; o fp16 (the proj GEMM's operand)
+ * and o_bf16 (what the bf16 backward reads), lse as dfu_attention_fwd. */
+int dfu_attention_fwd_f16(const void* qkv, int32_t B, int32_t N, int32_t H, int32_t dh,
+                          float scale, void* o, void* o_bf16, float* lse, void* stream);
 /* Backward: writes dq, dk, dv into dqkv (same layout as qkv); delta scratch [B*H][Npad]. */
 int dfu_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse,
                       int32_t B, int32_t N, int32_t H, int32_t dh, float scale, float* delta,
@@ -400,10 +416,11 @@ int dfu_adamw(float* const* params, float* const* grads, float* const* exp_avg,
               float beta2, float eps, float weight_decay, int64_t* step_dev, void* stream);
 /* Flat form: one contiguous buffer of n parameters (the fused flat-parameter layout).
  * shadow_bf16 (optional, n bf16): also receives bf16(updated param) — the GEMM operand copy
- * of every weight, so the forward pass needs no cast kernels. */
+ * of every weight, so the forward pass needs no cast kernels; shadow_f16 (optional, n fp16):
+ * fp16(updated param), the operands of the "parity" precision mode's fp16 ViT forward. */
 int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float lr, float beta1, float beta2, float eps, float weight_decay,
-                   const int64_t* step_dev, void* shadow_bf16, void* stream);
+                   const int64_t* step_dev, void* shadow_bf16, void* shadow_f16, void* stream);
 int dfu_step_increment(int64_t* step_dev, void* stream);
 /* argmax over C for each row (torch.max(outputs, 1), :384) -> int64. */
 int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t* out, void* stream);
@@ -454,6 +471,11 @@ int dfu_avgpool_fwd_x3(const void* x3, int32_t B, int32_t HW, int32_t C, float* 
 int dfu_layernorm_fwd_x3(const float* x, int64_t ldx, int32_t rows, int32_t D,
                          const float* gamma, const float* beta, float eps, void* out3,
                          void* out_bf16, float* mean, float* rstd, void* stream);
+/* timm LayerNorm -> fp16 [rows][D] (the fp16 forward's GEMM operand) + plain bf16 [rows][D];
+ * mean / rstd per row. */
+int dfu_layernorm_fwd_h16(const float* x, int64_t ldx, int32_t rows, int32_t D,
+                          const float* gamma, const float* beta, float eps, void* out_f16,
+                          void* out_bf16, float* mean, float* rstd, void* stream);
 /* exact GELU of the fp32 fc1 output -> triple [rows][3N], bf16 h and bf16 gelu'(pre) (the
  * DFU_EPI_BF16_DGELU operand, as DFU_EPI_BF16_GELU's aux_out). */
 int dfu_gelu_x3(const float* hpre, int64_t rows, int32_t N, void* h3, void* h_bf16,
