@@ -289,11 +289,15 @@ def gemm_roofline(fwd_bwd, tail, replays=3):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / replays  # per step
     flops = sum(r[1] for r in rec)
+    # MFMA work executed: a bf16x3 GEMM runs its K three times (the record counts it once)
+    executed = sum(2.0 * r[0].M * r[0].N * r[0].K for r in rec)
     nbytes = sum(r[2] for r in rec)
     n = len(rec)
     return {"launches_per_step": n, "avg_launch_us": us / n, "flops_per_launch": flops / n,
             "bytes_per_launch": nbytes / n, "gemm_ms_per_step": us / 1e3,
-            "achieved": flops / (us * 1e-6) / 1e12}
+            "achieved": flops / (us * 1e-6) / 1e12,
+            "mfma_executed": executed / (us * 1e-6) / 1e12,
+            "x3_launches": sum(1 for r in rec if 2.0 * r[0].M * r[0].N * r[0].K != r[1])}
 
 
 def main_gradcam(args, rank, world, dev):
@@ -835,11 +839,17 @@ def main():
                          "traffic_unit": "bytes per launch (HBM, PMC)",
                          "algorithmic_bytes_per_launch": round(gr["bytes_per_launch"]),
                          "traffic_source": traffic_src,
-                         "kernel": "dfu gemm_kernel (MFMA bf16 GEMM template: all ViT linears "
+                         "kernel": "dfu gemm_kernel / gemm_ps (MFMA GEMM template, bf16 "
+                                   "operands; in the parity mode the ViT forward's on fp16 "
+                                   "MFMA and the ResNet forward's split-bf16: all ViT linears "
                                    "and implicit-GEMM convs, fwd/dgrad/wgrad)",
                          "launches_per_step": gr["launches_per_step"],
                          "avg_launch_us": round(gr["avg_launch_us"], 2),
                          "gflop_per_launch": round(gr["flops_per_launch"] / 1e9, 4),
+                         "flop_basis": "algorithmic 2MNK per GEMM (a bf16x3 GEMM's tripled K "
+                                       "counted once; strided dgrad / s^2)",
+                         "mfma_executed_tflops": round(gr["mfma_executed"], 1),
+                         "x3_launches_per_step": gr["x3_launches"],
                          "gemm_ms_per_step": round(gr["gemm_ms_per_step"], 3),
                          "step": {"achieved": round(achieved, 1),
                                   "frac": round(achieved / PEAK_BF16_TFLOPS, 4),

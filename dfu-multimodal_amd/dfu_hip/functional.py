@@ -556,12 +556,13 @@ def conv_fwd_x3(x3_rows, geom, w3, y, stats):
     M = g.n * g.p * g.q
     C3 = 3 * g.c
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
-        ops.gemm(M, g.k, C3, x3_rows, C3, w3, C3, y, g.k, epilogue=L.EPI_F32_STATS, stats=stats)
+        ops.gemm(M, g.k, C3, x3_rows, C3, w3, C3, y, g.k, epilogue=L.EPI_F32_STATS, stats=stats,
+                 x3=True)
     else:
         g3 = ops.ConvGeom(g.n, g.h, g.w, C3, g.k, g.r, g.s, g.stride, g.pad)
         K = g.r * g.s * C3
         ops.gemm(M, g.k, K, x3_rows, 0, w3, K, y, g.k, a_mode=L.OPND_CONV_FWD,
-                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3)
+                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3, x3=True)
 
 
 def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, w_flip=None, w_t=None):
@@ -652,7 +653,7 @@ class StemFn(torch.autograd.Function):
             a = _empty((M, Cout), BF16, x.device)
             yf = _empty((M, Cout), F32, x.device)
             ops.gemm(M, Cout, 3 * Kp, col, 3 * Kp, weight_x3_rows(w, seg=Kp), 3 * Kp, yf, Cout,
-                     epilogue=L.EPI_F32_STATS, stats=stats)
+                     epilogue=L.EPI_F32_STATS, stats=stats, x3=True)
             bns.forward_coeffs(stats)
             af = _empty((M, Cout), F32, x.device)
             ops.bn_apply_x3(yf, bns.scale, bns.shift, None, 0, True, M, Cout, out_bf16=a,
@@ -938,7 +939,7 @@ class PatchEmbedFn(torch.autograd.Function):
             A, Bop, Kg = patches, wb, K
         ops.gemm(B * T, D, Kg, A, Kg, Bop, Kg, X, D, epilogue=L.EPI_PATCH,
                  bias=b.detach() if b is not None else None, aux=pos.detach().reshape(T + 1, D),
-                 ldaux=D, ep_tokens=T)
+                 ldaux=D, ep_tokens=T, x3=Kg != K)
         ops.vit_cls_rows(cls.detach().reshape(D), pos.detach().reshape(T + 1, D), X, B, T + 1, D)
         ctx.params = (w, b, cls, pos)
         ctx.dims = (B, T, D, K, C, H, W, ps)
@@ -1141,14 +1142,15 @@ class ViTBlockFn(torch.autograd.Function):
         xn1_3, xn1, m1, r1 = ln_x3(x2, blk.norm1)
         qkvf = _empty((rows, 3 * D), F32, dev)
         ops.gemm(rows, 3 * D, 3 * D, xn1_3, 3 * D, weight_x3_rows(attn.qkv.weight), 3 * D, qkvf,
-                 3 * D, epilogue=L.EPI_F32, bias=bias(attn.qkv), tile=tl)
+                 3 * D, epilogue=L.EPI_F32, bias=bias(attn.qkv), tile=tl, x3=True)
         del xn1_3
         qkv = _empty((rows, 3 * D), BF16, dev)  # written by the attention kernel
         o3, o, lse = ops.attention_fwd_f32(qkvf, B, T, H, dh, attn.scale, qkv_bf16=qkv)
         del qkvf
         xm = _empty((rows, D), F32, dev)
         ops.gemm(rows, D, 3 * D, o3, 3 * D, weight_x3_rows(attn.proj.weight), 3 * D, xm, D,
-                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D, tile=tl_d)
+                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D, tile=tl_d,
+                 x3=True)
         del o3
         xn2_3, xn2, m2, r2 = ln_x3(xm, blk.norm2)
         dgl = _empty((rows, Dh), BF16, dev)  # bf16 gelu'(pre): the DGELU factor
@@ -1158,19 +1160,19 @@ class ViTBlockFn(torch.autograd.Function):
             h3 = _empty((rows, 3 * Dh), BF16, dev)
             ops.gemm(rows, Dh, 3 * D, xn2_3, 3 * D, weight_x3_rows(mlp.fc1.weight), 3 * D, h3,
                      3 * Dh, epilogue=L.EPI_X3_GELU, bias=bias(mlp.fc1), aux_out=dgl,
-                     ldaux_out=Dh, tile=tl)
+                     ldaux_out=Dh, tile=tl, x3=True)
             h = h3[:, :Dh]
         else:
             hf = _empty((rows, Dh), F32, dev)
             ops.gemm(rows, Dh, 3 * D, xn2_3, 3 * D, weight_x3_rows(mlp.fc1.weight), 3 * D, hf,
-                     Dh, epilogue=L.EPI_F32, bias=bias(mlp.fc1), tile=tl)
+                     Dh, epilogue=L.EPI_F32, bias=bias(mlp.fc1), tile=tl, x3=True)
             h3, h, dgl = ops.gelu_x3(hf)
             del hf
         del xn2_3
         xo = _empty((B, T, D), F32, dev)
         ops.gemm(rows, D, 3 * Dh, h3, 3 * Dh, weight_x3_rows(mlp.fc2.weight), 3 * Dh,
                  xo.view(rows, D), D, epilogue=L.EPI_F32_RESID, bias=bias(mlp.fc2), aux=xm,
-                 ldaux=D, tile=tl_d)
+                 ldaux=D, tile=tl_d, x3=True)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
         ctx.out_ref = weakref.ref(xo)

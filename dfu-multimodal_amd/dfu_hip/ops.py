@@ -93,8 +93,9 @@ def gemm_replay(records, stream=None):
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
          epilogue=L.EPI_BF16, alpha=1.0, bias=None, aux=None, ldaux=0, aux_out=None,
          ldaux_out=0, stats=None, split_k=0, ep_tokens=0, conv=None, tile=0, workspace=None,
-         operand_type=0):
+         operand_type=0, x3=False):
     """C = epilogue(A @ B^T).  `split_k` (F32_ACC only): 0 = library cost model, 1 = none.
+    `x3`: a bf16x3 product (K tripled): the recorded algorithmic FLOPs count K / 3.
     `tile`: 0 = library cost model, else a TILES id.  Split-K partials go to fp32 slabs in
     `workspace` (allocated here from the stream-ordered caching allocator when None) and are
     reduced deterministically by a second kernel."""
@@ -132,7 +133,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
         d.tile_counters, d.tile_counters_len = cnt.data_ptr(), cnt.numel()
     check(lib().dfu_gemm(ctypes.byref(d), stream_ptr()), "dfu_gemm")
     if gemm_record is not None:
-        flops = 2.0 * M * N * K
+        flops = 2.0 * M * N * (K // 3 if x3 else K)  # algorithmic (x3: the product, not its 3 passes)
         if a_mode == L.OPND_CONV_DGRAD and conv is not None:
             flops /= conv.stride * conv.stride  # algorithmic: only the 1/stride^2 live taps
         gemm_record.append((d, flops, _algorithmic_bytes(d, conv),

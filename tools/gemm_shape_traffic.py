@@ -20,7 +20,7 @@ import sys
 
 OPND = ["KM", "MN", "CFWD", "CDGD", "CDGW", "CWGX"]
 EPI = ["BF16", "RELU", "GELU", "F32", "RESID", "DGELU", "ADD", "ACC", "ACCW", "STATS", "PATCH",
-       "F32STATS"]
+       "F32STATS", "DSTATS", "X3GELU", "F16DUAL", "F16GELU"]
 TILE = ["auto", "128x128", "256x128", "128x256", "256x256", "128x128o2", "128x128w4", "256x256p8",
         "256x256ps", "192x256ps", "256x64", "128x64o2"]
 
@@ -78,6 +78,8 @@ def main():
         name = f"{OPND[k[0]]}x{OPND[k[1]]}->{EPI[k[2]]} {k[3]}x{k[4]}x{k[5]}"
         if k[6]:
             name += f" conv{k[7]}x{k[8]} c{k[9]} k{k[10]} r{k[11]} s{k[13]}"
+        if len(k) > 15 and k[15]:
+            name += " f16"
         if times:
             key = name
             if key not in times:

@@ -20,14 +20,14 @@ from dfu_hip import ops  # noqa: E402
 
 OPND = ["KM", "MN", "CFWD", "CDGD", "CDGW", "CWGX"]
 EPI = ["BF16", "RELU", "GELU", "F32", "RESID", "DGELU", "ADD", "ACC", "ACCW", "STATS", "PATCH", "F32STATS",
-       "DSTATS", "X3GELU"]
+       "DSTATS", "X3GELU", "F16DUAL", "F16GELU"]
 TILE = ["auto", "128x128", "256x128", "128x256", "256x256", "128x128o2", "128x128w4", "256x256p8",
         "256x256ps", "192x256ps", "256x64", "128x64o2"]
 
 
 def key(d):
     return (d.a_mode, d.b_mode, d.epilogue, d.M, d.N, d.K, d.conv_n, d.conv_h, d.conv_w, d.conv_c,
-            d.conv_k, d.conv_r, d.conv_s, d.conv_stride, d.conv_pad)
+            d.conv_k, d.conv_r, d.conv_s, d.conv_stride, d.conv_pad, d.operand_type)
 
 
 def time_desc(d, iters):
@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--config", default="fusion")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--precision", default="parity", help="record the step in this mode")
     ap.add_argument("--ab", action="store_true", help="also time the one-shot schedule")
     ap.add_argument("--tail-ab", action="store_true",
                     help="also time without the tail split (in the '1shot' column)")
@@ -65,9 +66,11 @@ def main():
     opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
     crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
     rgb, th, y = bench.synthetic(a.batch, dev, 42)
+    from dfu_hip import functional as Fn
     ops.gemm_record = []
     opt.zero_grad()
-    crit(fwd(model, rgb, th), y).backward()
+    with Fn.precision(a.precision):
+        crit(fwd(model, rgb, th), y).backward()
     opt.step()
     rec, ops.gemm_record = ops.gemm_record, None
     torch.cuda.synchronize()
@@ -117,7 +120,7 @@ def main():
     for tot_us, n, us, us1, flops, nbytes, d, t, sk in rows:
         name = (f"{OPND[d.a_mode]}x{OPND[d.b_mode]}->{EPI[d.epilogue]} {d.M}x{d.N}x{d.K}"
                 + (f" conv{d.conv_h}x{d.conv_w} c{d.conv_c} k{d.conv_k} r{d.conv_r} s{d.conv_stride}"
-                   if d.conv_n else ""))
+                   if d.conv_n else "") + (" f16" if d.operand_type else ""))
         print(f"{tot_us / 1e3:8.3f} {n:3d} {us:7.1f} {us1 if us1 is not None else 0:7.1f} "
               f"{flops / us / 1e6:5.0f} {nbytes / 6e6:6.1f}  {TILE[t]}/{sk}  {name}", flush=True)
 

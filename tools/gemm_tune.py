@@ -24,7 +24,7 @@ from dfu_hip import ops  # noqa: E402
 SPLITS = [1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256]
 OPND = ["KM", "MN", "CONV_FWD", "CONV_DGRAD", "CONV_DGRAD_W", "CONV_WGRAD_X"]
 EPI = ["BF16", "BF16_RELU", "BF16_GELU", "F32", "F32_RESID", "BF16_DGELU", "BF16_ADD", "F32_ACC",
-       "F32_ACC_CONVW", "BF16_STATS", "PATCH", "F32_STATS", "BF16_DSTATS", "X3_GELU"]
+       "F32_ACC_CONVW", "BF16_STATS", "PATCH", "F32_STATS", "BF16_DSTATS", "X3_GELU", "F16_DUAL", "F16_GELU"]
 CONV_FIELDS = ("conv_n", "conv_h", "conv_w", "conv_c", "conv_k", "conv_r", "conv_s",
                "conv_stride", "conv_pad")
 

@@ -54,16 +54,18 @@ def cat(name):
 
 OPND = ["KM", "MN", "CONV_FWD", "CONV_DGRAD", "CONV_DGRAD_W", "CONV_WGRAD_X"]
 EPI = ["BF16", "BF16_RELU", "BF16_GELU", "F32", "F32_RESID", "BF16_DGELU", "BF16_ADD", "F32_ACC",
-       "F32_ACC_CONVW", "BF16_STATS", "PATCH", "F32_STATS", "BF16_DSTATS", "X3_GELU"]
+       "F32_ACC_CONVW", "BF16_STATS", "PATCH", "F32_STATS", "BF16_DSTATS", "X3_GELU", "F16_DUAL",
+       "F16_GELU"]
 
 
 def gemm_label(name):
-    m8 = re.search(r"gemm_p(8|s)<(\d+), (\d+), (\d+)(?:, (\d+))?>", name)
+    m8 = re.search(r"gemm_p(8|s)<(\d+), (\d+), (\d+)(?:, (\d+))?(?:, (true|false))?>", name)
     if m8:
         kind = "phased" if m8.group(1) == "8" else "persistent phased"
         rows = 2 * int(m8.group(5)) if m8.group(5) else 256
+        f16 = " fp16" if m8.group(6) == "true" else ""
         return (f"gemm {OPND[int(m8.group(2))]} x {OPND[int(m8.group(3))]} -> "
-                f"{EPI[int(m8.group(4))]} {rows}x256 {kind}")
+                f"{EPI[int(m8.group(4))]} {rows}x256 {kind}{f16}")
     m = re.search(r"gemm_kernel<(\d+), (\d+), (\d+), (\d+), (\d+)(?:, (\d+))?(?:, \d+)?>", name)
     if not m:
         return short(name)
