@@ -174,13 +174,18 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
     const int b = bh / H, h = bh - b * H;
     return qkv + (int64_t)b * N * tok_stride + h * 64;
   };
+  // Query tile of slot j of this wave in the it-th slice: the QT <= 2 NW tiles sit in the
+  // slots wave + NW j rotated by it & 3, so the SIMD holding the surplus tile (13 tiles on 4
+  // SIMDs at N = 197) changes from slice to slice: 10 instead of 12 tiles on the busiest SIMD
+  // over a CU's three slices at B = 64.
+  auto qtile = [&](int j, int itv) { return (wave + NW * j + 2 * NW - (itv & 3)) % (2 * NW); };
   // this wave's query fragments of a slice (exactly 2 QPW loads per lane, branch-free: rows
   // past N re-read row N - 1, unused)
-  auto load_q = [&](int bh, u32x4 (&v)[QPW][2]) {
+  auto load_q = [&](int bh, int itv, u32x4 (&v)[QPW][2]) {
     const bf16_t* qbase = slice_base(bh);
 #pragma unroll
     for (int j = 0; j < QPW; ++j) {
-      const int q = (wave + NW * j) * 16 + (lane & 15);
+      const int q = qtile(j, itv) * 16 + (lane & 15);
       const int64_t qo = (int64_t)(q < N ? q : N - 1) * tok_stride + 8 * g;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) v[j][ks] = *(const u32x4*)(qbase + qo + 32 * ks);
@@ -190,7 +195,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
   {
     const bf16_t* qb = slice_base(blockIdx.x);
     stage_kv_dma<KT, NW>(smem, qb + H * 64, qb + 2 * H * 64, tok_stride, N, wave, lane);
-    load_q(blockIdx.x, qn);
+    load_q(blockIdx.x, 0, qn);
   }
   int it = 0;
   for (int bh = blockIdx.x; bh < BH; bh += gridDim.x, ++it) {
@@ -216,12 +221,12 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
       const bf16_t* nq = slice_base(nb);
       stage_kv_dma<KT, NW>(smem + ((it + 1) & 1) * IMG2, nq + H * 64, nq + 2 * H * 64,
                            tok_stride, N, wave, lane);
-      load_q(nb, qn);
+      load_q(nb, it + 1, qn);
     }
 #pragma unroll
     for (int j = 0; j < QPW; ++j) {
-      const int qt = wave + NW * j;
-      if (qt >= QT) break;
+      const int qt = qtile(j, it);
+      if (qt >= QT) continue;
       const int q = qt * 16 + (lane & 15);
       bf16x8 qf[2];
 #pragma unroll
@@ -446,24 +451,38 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
         dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
         dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
-#pragma unroll 1
-      for (int u = 0; u < KT / 2; ++u) {
-        f32x4 ph[2], dsh[2];
+      // software-pipelined over query-tile pairs: the S / dP MFMAs of pair u + 1 are issued
+      // before pair u's exponentials, so the MFMA -> exp -> pack -> MFMA chain of one pair runs
+      // under the next pair's products instead of stalling the wave
+      f32x4 st[2][2], dp[2][2];  // [buffer][hh]
+      auto products = [&](int u, f32x4* st_, f32x4* dp_) {
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const int qt = 2 * u + hh;
-          f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+          st_[hh] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          dp_[hh] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
-            st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * qt, ks, lane), kf[ks], st, 0, 0, 0);
-            dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * qt, ks, lane), vf[ks], dp, 0, 0, 0);
+            st_[hh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * qt, ks, lane), kf[ks], st_[hh], 0, 0, 0);
+            dp_[hh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * qt, ks, lane), vf[ks], dp_[hh], 0, 0, 0);
           }
+        }
+      };
+      products(0, st[0], dp[0]);
+#pragma unroll
+      for (int u = 0; u < KT / 2; ++u) {
+        const int cb = u & 1;
+        if (u + 1 < KT / 2) products(u + 1, st[cb ^ 1], dp[cb ^ 1]);
+        f32x4 ph[2], dsh[2];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int q0 = 16 * (2 * u + hh) + 4 * g;
+          const f32x4 l4 = *(const f32x4*)(Ls + q0), e4 = *(const f32x4*)(Es + q0);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int q = 16 * qt + 4 * g + r;
-            const float pv = fast_exp2(fmaf(st[r], c, -Ls[q]));
+            const float pv = fast_exp2(fmaf(st[cb][hh][r], c, -l4[r]));
             ph[hh][r] = pv;
-            dsh[hh][r] = pv * (dp[r] - Es[q]);
+            dsh[hh][r] = pv * (dp[cb][hh][r] - e4[r]);
           }
         }
         const bf16x8 pb = pack_frag(ph[0], ph[1]);

@@ -426,6 +426,20 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
     DFU_CHECK_ARG(d->ldb >= round8(d->N), "dfu_gemm: MN-major B needs ldb >= round8(N)");
   if (d->epilogue == DFU_EPI_BF16_STATS || d->epilogue == DFU_EPI_F32_STATS)
     DFU_CHECK_ARG(d->stats != nullptr, "dfu_gemm: STATS epilogue needs a stats slab");
+  if (d->a_seg) {
+    const bool conv_a = d->a_mode == DFU_OPND_CONV_FWD;
+    DFU_CHECK_ARG(d->a_lo != nullptr && d->a_seg > 0 && d->a_seg % 64 == 0 &&
+                      (d->a_mode == DFU_OPND_KMAJOR || conv_a) &&
+                      (conv_a ? d->conv_c == 3 * d->a_seg : (d->K == 3 * d->a_seg &&
+                                                             d->lda == d->a_seg)) &&
+                      ((uintptr_t)d->a_lo & 15) == 0 &&
+                      ((const char*)d->a_lo - (const char*)d->A) % 2 == 0,
+                  "dfu_gemm: split-pair A needs a_lo, a_seg %% 64 == 0, K-contiguous or conv-"
+                  "forward A with K (conv_c) = 3 a_seg and lda = a_seg");
+    DFU_CHECK_ARG(pl.tile != T256x256p8 && pl.tile != T256x256ps && pl.tile != T192x256ps,
+                  "dfu_gemm: split-pair A is not supported on the phased tiles (plan %d)",
+                  pl.tile + 1);
+  }
   if (d->epilogue == DFU_EPI_BF16_DSTATS) {  // retired in round 4 (measured slower); reserved
     dfu_set_error("dfu_gemm: the DSTATS epilogue is retired");
     return DFU_E_UNSUPPORTED;
@@ -542,6 +556,11 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   a.ck = d->conv_k; a.cr = d->conv_r; a.cs = d->conv_s;
   a.cstride = d->conv_stride; a.cpad = d->conv_pad; a.cp = d->conv_p; a.cq = d->conv_q;
   a.cpad_w = d->conv_pad;
+  // split-pair A (the bf16x3 ResNet forward's activations): hi at A, lo at a_lo, both with
+  // row / pixel stride a_seg; the tripled K reads segments hi | lo | hi
+  a.a_seg = d->a_seg;
+  a.a_pix = d->a_seg ? d->a_seg : d->conv_c;
+  a.a_lo_delta = d->a_seg ? ((const bf16_t*)d->a_lo - (const bf16_t*)d->A) : 0;
   a.ph_st = a.ph_h = a.ph_w = a.ph_r0 = a.ph_s0 = a.ph_H = a.ph_W = a.ph_S = 0;
   if (ph) {  // the phase's stride-1 equivalent geometry (GemmArgs::ph_*)
     a.ch = ph->Hs; a.cw = ph->Ws; a.cr = ph->nr; a.cs = ph->ns;

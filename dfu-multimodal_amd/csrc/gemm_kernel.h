@@ -81,6 +81,11 @@ struct GemmArgs {
   // counter sums the slabs in split order and runs the normal epilogue.
   int tail_full, tail_r, tail_s, tail_kps;
   float* tslab;  // [tail_s][tail_r][FM*FN][threads] f32x4, lane-linear
+  // Split-pair A (dfu_gemm_desc.a_seg > 0, the bf16x3 ResNet forward): the tripled K is read
+  // as segments [hi | lo | hi] of width a_seg from two buffers of row (pixel) stride a_seg,
+  // hi at A and lo at A + a_lo_delta (elements); a_pix = the conv gather's pixel stride.
+  int a_seg, a_pix;
+  int64_t a_lo_delta;
   int n4;       // N and every leading dimension % 4 == 0: one vector access per 4 columns
   int n8;       // N, ldc (, ldaux_out) % 8 == 0 and 16-B aligned bf16 outputs: paired stores
   int ep_tokens;
@@ -201,10 +206,12 @@ DFU_DEV void glds16(const void* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, 0);
 }
 
-// Issue this thread's NLD LDS-DMA instructions for K-step kt into `tile`.
-template <int MODE, int NLD, int NW>
+// Issue this thread's NLD LDS-DMA instructions for K-step kt into `tile` (IS_A: the A operand,
+// which may be in split-pair form, GemmArgs::a_seg).
+template <int MODE, int NLD, int NW, bool IS_A = false>
 DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_t* base,
                         int64_t ld, int MN_bound, int kt, int kend, int tid, char* tile) {
+  constexpr bool is_a = IS_A;
   constexpr int PPS = 16 / NW;  // MN-contiguous pieces per wave and 128-column sub-image
   constexpr int STEP = 1024 * NW;
   const int k0 = kt * BK;
@@ -212,15 +219,28 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
   const void* zero = (const void*)g_zero16;
   if constexpr (MODE == DFU_OPND_KMAJOR) {
     const bool kin = k0 + st.kc < kend;
+    // split-pair A: segment 1 of the tripled K from the lo buffer, segment 2 from hi again (the
+    // whole K-step lies in one segment: a_seg % 64 == 0, host-checked; a wave-uniform offset)
+    int64_t adj = 0;
+    if (is_a && p.a_seg)
+      adj = k0 >= 2 * p.a_seg ? -2 * (int64_t)p.a_seg
+                              : (k0 >= p.a_seg ? p.a_lo_delta - p.a_seg : 0);
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const bool ok = st.valid[i] && kin;
-      glds16(ok ? (const void*)(st.ptr[i] + k0) : zero, dst + STEP * i);
+      glds16(ok ? (const void*)(st.ptr[i] + k0 + adj) : zero, dst + STEP * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_FWD) {
     // whole K-step lies in one filter tap (C % 64 == 0, host-checked)
     const uint32_t rs = fdiv((uint32_t)k0, p.div_c);
-    const int c0 = k0 - (int)rs * p.cc + st.kc;
+    int c0 = k0 - (int)rs * p.cc;
+    int64_t adj = 0;
+    if (p.a_seg) {  // split-pair input: channel segment 1 from the lo buffer, 2 from hi again
+      const int seg = c0 >= 2 * p.a_seg ? 2 : (c0 >= p.a_seg ? 1 : 0);
+      c0 -= seg * p.a_seg;
+      adj = seg == 1 ? p.a_lo_delta : 0;
+    }
+    c0 += st.kc;
     const uint32_t r = fdiv(rs, p.div_s);
     const int sx = (int)(rs - r * p.cs);
     const bool kin = k0 < kend;
@@ -228,7 +248,7 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
     for (int i = 0; i < NLD; ++i) {
       const int ih = st.i0[i] + (int)r, iw = st.i1[i] + sx;
       const bool ok = kin && st.valid[i] && (unsigned)ih < (unsigned)p.ch && (unsigned)iw < (unsigned)p.cw;
-      const int64_t off = (((int64_t)st.bofs[i] * p.ch + ih) * p.cw + iw) * p.cc + c0;
+      const int64_t off = (((int64_t)st.bofs[i] * p.ch + ih) * p.cw + iw) * p.a_pix + c0 + adj;
       glds16(ok ? (const void*)(base + off) : zero, dst + STEP * i);
     }
   } else if constexpr (MODE == DFU_OPND_CONV_DGRAD) {
@@ -1014,7 +1034,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   load_init<BMODE, T::NLDB, NW>(p, sb, p.B, p.ldb, in0, p.N, tid);
   auto issue_next = [&](char* stage) {
     if (!(p.dbg & 4)) {
-    issue_tile<AMODE, T::NLDA, NW>(p, sa, p.A, p.lda, p.m_ld_bound, ikb + ik, p.K, tid, stage);
+    issue_tile<AMODE, T::NLDA, NW, true>(p, sa, p.A, p.lda, p.m_ld_bound, ikb + ik, p.K, tid,
+                                         stage);
     issue_tile<BMODE, T::NLDB, NW>(p, sb, p.B, p.ldb, p.n_ld_bound, ikb + ik, p.K, tid,
                                stage + T::A_BYTES);
     }

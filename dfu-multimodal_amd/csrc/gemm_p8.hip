@@ -266,32 +266,6 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
       };
-#if DFU_P8_FINE
-      // phase 1: A-top x B-left; next A-top
-      wait_vmcnt<4>();
-      __builtin_amdgcn_s_barrier();
-      read_a(0);
-      read_b(0);
-      if (nxt) issue_a(m0, k1, 0, na);
-      mfma(0, 0);
-      // phase 2: A-top x B-right; next B-left
-      if (nxt) wait_vmcnt<4>(); else wait_vmcnt<2>();
-      __builtin_amdgcn_s_barrier();
-      read_b(1);
-      if (nxt) issue_b(n0, k1, 0, nb);
-      mfma(0, 1);
-      // phase 3: A-bottom x B-right; next B-right
-      if (nxt) wait_vmcnt<4>(); else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      read_a(1);
-      if (nxt) issue_b(n0, k1, 1, nb);
-      mfma(1, 1);
-      // phase 4: A-bottom x B-left; next A-bottom
-      __builtin_amdgcn_s_barrier();
-      read_b(0);
-      if (nxt) issue_a(m0, k1, 1, na);
-      mfma(1, 0);
-#else
       // one barrier per K-step (all of this K-step's half-tiles landed and published); the next
       // K-step's DMA goes out in phases 1 and 2, leaving phases 3-4 of MFMAs to cover it; waves
       // drift freely through phases 2-4 (no LDS hazard inside a K-step)
@@ -314,7 +288,6 @@ __global__ __launch_bounds__(512) void gemm_p8(const GemmArgs p) {
       mfma(1, 1);
       read_b(0);
       mfma(1, 0);
-#endif
     }
     p8_epilogue<EPI>(p, acc, m0, n0, wr, wc, lane, sidx);
   }

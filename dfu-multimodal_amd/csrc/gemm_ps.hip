@@ -27,19 +27,6 @@ namespace {
 #define DFU_PS_ABLATE 0
 #endif
 constexpr int kAbl = DFU_PS_ABLATE;
-// Schedule experiments (same mechanism): bit 0 = the two wave rows issue their whole DMA share at
-// different points (wr 0 before the first MFMA group, wr 1 after the second), bit 1 =
-// s_setprio(1) around every MFMA group, bit 2 = both B halves kept in registers, bit 3 = the
-// partial last round of units in contiguous runs per XCD.
-#ifndef DFU_PS_SCHED
-#define DFU_PS_SCHED 0
-#endif
-constexpr int kSched = DFU_PS_SCHED;
-// Cache-policy bits of the epilogue's output stores (experiment builds: -DDFU_PS_STAUX=2 = nt)
-#ifndef DFU_PS_STAUX
-#define DFU_PS_STAUX 0
-#endif
-constexpr int kStAux = DFU_PS_STAUX;
 
 constexpr int PS_IMG = 256 * 128;   // one operand image: 256 rows x 64 k x 2 B
 constexpr int PS_BUF = 2 * PS_IMG;  // A + B
@@ -222,15 +209,15 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[jj][r] = acc[i][2 * hb + jj][r] * p.alpha + bias[2 * hb + jj][r];
       if constexpr (EPI == DFU_EPI_BF16) {
-        st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+        st_row_bf16<2, 0>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
       } else if constexpr (EPI == DFU_EPI_BF16_GELU) {
         float g[2][4], d[2][4];
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
           for (int r = 0; r < 4; ++r) gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
-        st_row_bf16<2, kStAux>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
-        st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, 0>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
+        st_row_bf16<2, 0>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
       } else if constexpr (EPI == DFU_EPI_X3_GELU) {
         // gelu(pre) as the split triple hi = bf16(g), lo = bf16(g - hi): segments hi | lo | hi
         float g[2][4], d[2][4], lo[2][4];
@@ -241,14 +228,14 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
             gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
             lo[jj][r] = g[jj][r] - bf2f(f2bf(g[jj][r]));
           }
-        st_row_bf16<2, kStAux>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
-        st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
-        st_row_bf16<2, kStAux>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, lo);
-        st_row_bf16<2, kStAux>(rc, mc * p.ldc + 2 * N, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, 0>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
+        st_row_bf16<2, 0>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, 0>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, lo);
+        st_row_bf16<2, 0>(rc, mc * p.ldc + 2 * N, okm, n0w, N, p.n8, n4, lane, g);
       } else if constexpr (EPI == DFU_EPI_F16_DUAL) {
         // fp16 operand of the next fp16 step, bf16 copy for the backward
-        st_row_bf16<2, kStAux, true>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
-        st_row_bf16<2, kStAux>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, v);
+        st_row_bf16<2, 0, true>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+        st_row_bf16<2, 0>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, v);
       } else if constexpr (EPI == DFU_EPI_F16_GELU) {
         // gelu(pre) as fp16 (fc2's operand, column 0) and bf16 (the backward's h, column N)
         float g[2][4], d[2][4];
@@ -256,14 +243,14 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
           for (int r = 0; r < 4; ++r) gelu_and_grad(v[jj][r], g[jj][r], d[jj][r]);
-        st_row_bf16<2, kStAux>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
-        st_row_bf16<2, kStAux, true>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
-        st_row_bf16<2, kStAux>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, 0>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, d);
+        st_row_bf16<2, 0, true>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, g);
+        st_row_bf16<2, 0>(rc, mc * p.ldc + N, okm, n0w, N, p.n8, n4, lane, g);
       } else if constexpr (EPI == DFU_EPI_F32) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const int n = n0w + jj * 16 + 4 * (lane >> 4);
-          st4_f32<kStAux>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+          st4_f32<0>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
         }
       } else if constexpr (EPI == DFU_EPI_BF16_DGELU || EPI == DFU_EPI_BF16_ADD) {
 #pragma unroll
@@ -281,7 +268,7 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) cs[hb][jj][r] += okm ? bf2f(f2bf(v[jj][r])) : 0.f;
         }
-        st_row_bf16<2, kStAux>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
+        st_row_bf16<2, 0>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
       } else if constexpr (EPI == DFU_EPI_F32_ACC) {  // split-K slab, or C += acc unsplit
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
@@ -291,7 +278,7 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
           } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[jj][r] += __uint_as_float(af[st][jj][r]);
-            st4_f32<kStAux>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+            st4_f32<0>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
           }
         }
       } else {  // DFU_EPI_F32_RESID
@@ -300,7 +287,7 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
           const int n = n0w + jj * 16 + 4 * (lane >> 4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[jj][r] += __uint_as_float(af[st][jj][r]);
-          st4_f32<kStAux>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
+          st4_f32<0>(rc, mc * p.ldc + n, okm, n, N, n4, v[jj]);
         }
       }
     }
@@ -358,21 +345,9 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   // rounds: in complete rounds workgroup b takes unit i*G + wg(b); in the last, partial round
   // unit i*G + b (spread over every XCD)
   const int full = units / nwg;
-  int rounds = full + (bid < units - full * nwg ? 1 : 0);
-  int tail_slot = bid;  // this workgroup's unit in the last, partial round (if any)
-  if constexpr ((kSched & 8) != 0) {
-    // the R units of the partial round in 8 contiguous runs, run x on XCD x (blocks b = x mod
-    // 8): neighbouring tiles of the grouped raster share their A / B panels in one L2
-    const int R = units - full * nwg;
-    if (nwg >= 16 && R > 0) {
-      const int x = bid & 7, j = bid >> 3;
-      const int r0 = (x * R) >> 3, r1 = ((x + 1) * R) >> 3;
-      rounds = full + (j < r1 - r0 ? 1 : 0);
-      tail_slot = r0 + j;
-    }
-  }
+  const int rounds = full + (bid < units - full * nwg ? 1 : 0);
   if (rounds == 0) return;
-  auto unit_at = [&](int i) { return i * nwg + (i < full ? wg : tail_slot); };
+  auto unit_at = [&](int i) { return i * nwg + (i < full ? wg : bid); };
   auto unit_geom = [&](int u, int& m0, int& n0, int& kb, int& nk) {
     constexpr int GROUP_M = 4;
     const int s = u / tiles, t = u - s * tiles;
@@ -449,24 +424,15 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   // wave's and its SIMD partner's) to land under instead of stalling the pipe (the compiler's
   // lgkmcnt waits are the exact ones for K-contiguous reads; MN-major ones are asm, retired by an
   // lgkmcnt(0) in front of each group).
-  // kSched bit 2: both B halves stay in registers (fbh[hb]), so phase 4 does not re-read B-left.
-  // kSched bit 4 (16): K-step g+1's DMA wait and barrier move in front of K-step g's last MFMA
-  // group, and K-step g+1's first fragment reads go out right behind that group (the reads'
-  // latency and the barrier's skew land under the group instead of idling the pipe at the top of
-  // every K-step).  RAW: each wave waits for its own DMA of K-step g+1 before the barrier.  WAR:
-  // every wave retires its LDS reads (lgkmcnt(0)) before that barrier, and the DMA that refills
-  // K-step g's buffer is issued after it.
-  // kSched bit 5 (32): the next K-step's DMA goes out two pieces behind each of the first four
-  // MFMA groups (after that group's fragment reads) instead of in two bursts beside the reads.
-  constexpr bool kB2 = (kSched & 4) != 0;
-  constexpr bool kEarly = (kSched & 16) != 0;
-  constexpr bool kSpread = (kSched & 32) != 0;
-  bf16x8 fa[FMH][2], fbh[2][2][2];
+  // (Measured and dropped, round 3: both B halves kept in registers, the next K-step's barrier
+  // moved in front of the last MFMA group, the DMA spread over all four groups, the two wave rows
+  // issuing their DMA at different points, s_setprio around the groups, per-XCD runs for the
+  // partial round -- all within noise.)
+  bf16x8 fa[FMH][2], fb[2][2];
   if constexpr ((kAbl & 8) != 0) {
 #pragma unroll
     for (int i = 0; i < FMH; ++i) fa[i][0] = fa[i][1] = (bf16x8){};
-    fbh[0][0][0] = fbh[0][0][1] = fbh[0][1][0] = fbh[0][1][1] = (bf16x8){};
-    fbh[1][0][0] = fbh[1][0][1] = fbh[1][1][0] = fbh[1][1][1] = (bf16x8){};
+    fb[0][0] = fb[0][1] = fb[1][0] = fb[1][1] = (bf16x8){};
   }
   auto rd_a = [&](const char* la, int h, int ks) {
     if constexpr ((kAbl & 8) != 0) return;
@@ -478,7 +444,7 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     if constexpr ((kAbl & 8) != 0) return;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      fbh[kB2 ? h : 0][j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
+      fb[j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
   };
   // the first group's reads of a K-step (A-top, B-left, both k-halves)
   auto rd_first = [&](const char* la) {
@@ -497,28 +463,21 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
 #pragma unroll
       for (int i = 0; i < FMH; ++i) pin(fa[i][ks]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) pin(fbh[kB2 ? hb : 0][j][ks]);
+      for (int j = 0; j < 2; ++j) pin(fb[j][ks]);
     }
-    if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FMH; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         if constexpr (H16)
           acc[ha * FMH + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-              __builtin_bit_cast(f16x8, fbh[kB2 ? hb : 0][j][ks]),
+              __builtin_bit_cast(f16x8, fb[j][ks]),
               __builtin_bit_cast(f16x8, fa[i][ks]), acc[ha * FMH + i][hb * 2 + j], 0, 0, 0);
         else
           acc[ha * FMH + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              fbh[kB2 ? hb : 0][j][ks], fa[i][ks], acc[ha * FMH + i][hb * 2 + j], 0, 0, 0);
-    if constexpr ((kSched & 2) != 0) __builtin_amdgcn_s_setprio(0);
+              fb[j][ks], fa[i][ks], acc[ha * FMH + i][hb * 2 + j], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   };
-  if constexpr (kEarly) {  // K-step 0: landed, published, first reads out
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    rd_first(smem);
-  }
   for (int g = 0; g < total; ++g) {
     const char* la = smem + (g & 1) * PS_BUF;
     const char* lb = la + PS_IMG;
@@ -526,48 +485,23 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     char* nb = na + PS_IMG;
     const bool nxt = g + 1 < total;
     const int k1 = (ikb + ik) * BK;  // the next K-step (issue cursor)
-    const bool row0 = __builtin_amdgcn_readfirstlane(wr) == 0;
-    if constexpr (!kEarly) {
-      // this K-step's DMA landed (younger: only the previous epilogue's stores), then published
-      if (epi_last)
-        wait_vm_le<63>(E);
-      else
-        wait_vmcnt<0>();
-      if constexpr (!(kAbl & 16)) __builtin_amdgcn_s_barrier();
-      rd_first(la);
-    }
-    if constexpr (kSched & 1) {
-      if (nxt && row0) {
-        issue_a(k1, 0, na);
-        issue_b(k1, 0, nb);
-        issue_b(k1, 1, nb);
-        issue_a(k1, 1, na);
-        advance_issue();
-      }
-    } else if (nxt && !kSpread) {
+    // this K-step's DMA landed (younger: only the previous epilogue's stores), then published
+    if (epi_last)
+      wait_vm_le<63>(E);
+    else
+      wait_vmcnt<0>();
+    if constexpr (!(kAbl & 16)) __builtin_amdgcn_s_barrier();
+    rd_first(la);
+    if (nxt) {
       issue_a(k1, 0, na);
       issue_b(k1, 0, nb);
     }
     __builtin_amdgcn_sched_barrier(0);
     mf(0, 0, 0);   // A-top x B-left
     rd_b(lb, 1, 0);
-    if constexpr (kSpread) {
-      if (nxt) issue_a(k1, 0, na);
-      __builtin_amdgcn_sched_barrier(0);
-    }
     mf(0, 0, 1);
     rd_b(lb, 1, 1);
-    if constexpr (kSched & 1) {
-      if (nxt && !row0) {
-        issue_a(k1, 0, na);
-        issue_b(k1, 0, nb);
-        issue_b(k1, 1, nb);
-        issue_a(k1, 1, na);
-        advance_issue();
-      }
-    } else if (kSpread) {
-      if (nxt) issue_b(k1, 0, nb);
-    } else if (nxt) {
+    if (nxt) {
       issue_b(k1, 1, nb);
       issue_a(k1, 1, na);
       advance_issue();
@@ -575,32 +509,13 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     __builtin_amdgcn_sched_barrier(0);
     mf(0, 1, 0);   // A-top x B-right
     rd_a(la, 1, 0);
-    if constexpr (kSpread) {
-      if (nxt) issue_b(k1, 1, nb);
-      __builtin_amdgcn_sched_barrier(0);
-    }
     mf(0, 1, 1);
     rd_a(la, 1, 1);
-    if constexpr (kSpread) {
-      if (nxt) {
-        issue_a(k1, 1, na);
-        advance_issue();
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
     mf(1, 1, 0);   // A-bottom x B-right
-    if constexpr (!kB2) rd_b(lb, 0, 0);
+    rd_b(lb, 0, 0);
     mf(1, 1, 1);
-    if constexpr (!kB2) rd_b(lb, 0, 1);
+    rd_b(lb, 0, 1);
     mf(1, 0, 0);   // A-bottom x B-left
-    if constexpr (kEarly) {
-      if (nxt) {  // K-step g+1: landed (older: at most an epilogue's stores), reads retired, published
-        wait_vmcnt<0>();
-        lds_reads_retired();
-        __builtin_amdgcn_s_barrier();
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
     mf(1, 0, 1);
     epi_last = false;
     if (++ck == cnk) {
@@ -622,9 +537,6 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
         cu = unit_at(ci);
         unit_geom(cu, cm0, cn0, ckb, cnk);
       }
-    }
-    if constexpr (kEarly) {
-      if (nxt) rd_first(na);
     }
   }
 }

@@ -14,7 +14,10 @@
 // PATCH epilogues), and the kernels below turn them into the next GEMM's triple while also
 // writing the plain bf16 tensors the (unchanged, bf16) backward pass saves.
 //
-// Layout of a triple: bf16 [rows][3C], segment s at columns [sC, (s+1)C).
+// Layout of a triple: bf16 [rows][3C], segment s at columns [sC, (s+1)C).  The ResNet's
+// activations use the split-pair form instead (round 4): the plain bf16 tensor IS the hi
+// buffer and a second [rows][C] buffer holds lo; the GEMM reads the tripled K from the two
+// (dfu_gemm_desc.a_seg), so each BN output is written as 2 + 2 bytes instead of 6 + 2.
 #include "common.h"
 
 namespace {
@@ -109,44 +112,63 @@ __global__ void k_pack_conv_weight_x3(const float* __restrict__ w, bf16_t* __res
   }
 }
 
+// hi = bf16(f), lo = bf16(f - hi) of 8 values into the pair buffers at element e
+DFU_DEV void st_pair8(bf16_t* hi, bf16_t* lo, int64_t e, const float* f) {
+  float h[8], l[8];
+  split8(f, h, l);
+  *(u32x4*)(hi + e) = pack8(h);
+  *(u32x4*)(lo + e) = pack8(l);
+}
+// hi + lo of 8 values of a pair at element e
+DFU_DEV void ld8_pair(const bf16_t* hi, const bf16_t* lo, int64_t e, float* f) {
+  float h[8], l[8];
+  unpack8(*(const u32x4*)(hi + e), h);
+  unpack8(*(const u32x4*)(lo + e), l);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = h[i] + l[i];
+}
+
 // ---------------------------------------------------------------- BatchNorm apply
 // out = act(y*scale + shift + res) from the fp32 conv output y (F32_STATS epilogue).
-// res_mode 0 none, 1 fp32 [M][C], 2 triple [M][3C].  Outputs (each optional): the triple
-// (the next convolution's operand), plain bf16 (what the backward saves), fp32 (a residual),
-// and y rounded to bf16 (the BN backward's input).
+// res_mode 0 none, 1 fp32 [M][C], 2 split pair (res = hi, res_lo = lo, [M][C] each).  Outputs
+// (each optional): the pair hi = out_bf (the plain bf16 tensor the backward saves and the next
+// convolution's hi operand) and out_lo, fp32 (a residual), and y rounded to bf16 (the BN
+// backward's input).
 __global__ void k_bn_apply_x3(const float* __restrict__ y, const float* __restrict__ scale,
                               const float* __restrict__ shift, const void* __restrict__ res,
-                              int res_mode, int relu, bf16_t* __restrict__ out3,
-                              bf16_t* __restrict__ out_bf, float* __restrict__ out_f32,
-                              bf16_t* __restrict__ y_bf, int64_t M, int C) {
+                              const bf16_t* __restrict__ res_lo, int res_mode, int relu,
+                              bf16_t* __restrict__ out_lo, bf16_t* __restrict__ out_bf,
+                              float* __restrict__ out_f32, bf16_t* __restrict__ y_bf, int64_t M,
+                              int C) {
   const int cv = C / 8;
   const int64_t n = M * cv;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t m = i / cv;
     const int c = (int)(i - m * cv) * 8;
+    const int64_t e = m * C + c;
     float f[8], r[8];
-    ld8_f32(y + m * C + c, f);
-    if (y_bf) *(u32x4*)(y_bf + m * C + c) = pack8(f);
-    if (res_mode == 1) ld8_f32((const float*)res + m * C + c, r);
-    else if (res_mode == 2) ld8_triple((const bf16_t*)res + m * 3 * C, C, c, r);
+    ld8_f32(y + e, f);
+    if (y_bf) *(u32x4*)(y_bf + e) = pack8(f);
+    if (res_mode == 1) ld8_f32((const float*)res + e, r);
+    else if (res_mode == 2) ld8_pair((const bf16_t*)res, res_lo, e, r);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float v = fmaf(f[e], scale[c + e], shift[c + e]);
-      if (res_mode) v += r[e];
-      f[e] = relu ? fmaxf(v, 0.f) : v;
+    for (int k = 0; k < 8; ++k) {
+      float v = fmaf(f[k], scale[c + k], shift[c + k]);
+      if (res_mode) v += r[k];
+      f[k] = relu ? fmaxf(v, 0.f) : v;
     }
-    if (out3) st_triple8(out3 + m * 3 * C, C, c, f, 0);
-    if (out_bf) *(u32x4*)(out_bf + m * C + c) = pack8(f);
-    if (out_f32) st8_f32(out_f32 + m * C + c, f);
+    if (out_lo) st_pair8(out_bf, out_lo, e, f);
+    else if (out_bf) *(u32x4*)(out_bf + e) = pack8(f);
+    if (out_f32) st8_f32(out_f32 + e, f);
   }
 }
 
 // ---------------------------------------------------------------- pooling
-// resnet maxpool 3x3/s2/p1 over fp32 NHWC -> triple + plain bf16 + argmax (first max in
-// row-major window order wins, as k_maxpool_fwd).
+// resnet maxpool 3x3/s2/p1 over fp32 NHWC -> split pair (plain bf16 = hi, y_lo) + argmax
+// (first max in row-major window order wins, as k_maxpool_fwd).
 __global__ void k_maxpool_fwd_x3(const float* __restrict__ x, int B, int H, int W, int C,
-                                 bf16_t* __restrict__ y3, bf16_t* __restrict__ y_bf,
+                                 bf16_t* __restrict__ y_lo, bf16_t* __restrict__ y_bf,
                                  uint8_t* __restrict__ am, int P, int Q) {
   const int cv = C / 8;
   const int64_t n = (int64_t)B * P * Q * cv;
@@ -178,8 +200,7 @@ __global__ void k_maxpool_fwd_x3(const float* __restrict__ x, int B, int H, int 
           }
       }
     }
-    st_triple8(y3 + pix * 3 * C, C, c8 * 8, best, 0);
-    *(u32x4*)(y_bf + pix * C + c8 * 8) = pack8(best);
+    st_pair8(y_bf, y_lo, pix * C + c8 * 8, best);
     uint64_t packed = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) packed |= (uint64_t)arg[e] << (8 * e);
@@ -187,9 +208,9 @@ __global__ void k_maxpool_fwd_x3(const float* __restrict__ x, int B, int H, int 
   }
 }
 
-// AdaptiveAvgPool2d(1) over a triple [B*HW][3C] -> fp32 [B][C].
-__global__ void k_avgpool_fwd_x3(const bf16_t* __restrict__ x3, int B, int HW, int C,
-                                 float* __restrict__ y) {
+// AdaptiveAvgPool2d(1) over a split pair (hi, lo: [B*HW][C] each) -> fp32 [B][C].
+__global__ void k_avgpool_fwd_x3(const bf16_t* __restrict__ hi, const bf16_t* __restrict__ lo,
+                                 int B, int HW, int C, float* __restrict__ y) {
   const int cv = C / 8;
   const int64_t n = (int64_t)B * cv;
   const float inv = 1.0f / (float)HW;
@@ -200,7 +221,7 @@ __global__ void k_avgpool_fwd_x3(const bf16_t* __restrict__ x3, int B, int HW, i
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int t = 0; t < HW; ++t) {
       float f[8];
-      ld8_triple(x3 + ((int64_t)b * HW + t) * 3 * C, C, c8 * 8, f);
+      ld8_pair(hi, lo, ((int64_t)b * HW + t) * C + c8 * 8, f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += f[e];
     }
@@ -322,38 +343,39 @@ extern "C" int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int
 }
 
 extern "C" int dfu_bn_apply_x3(const float* y, const float* scale, const float* shift,
-                               const void* residual, int32_t res_mode, int32_t relu, void* out3,
-                               void* out_bf16, float* out_f32, void* y_bf16, int64_t M, int32_t C,
-                               void* stream) {
+                               const void* residual, const void* residual_lo, int32_t res_mode,
+                               int32_t relu, void* out_lo, void* out_bf16, float* out_f32,
+                               void* y_bf16, int64_t M, int32_t C, void* stream) {
   DFU_CHECK_ARG(y && scale && shift && C % 8 == 0 && M >= 0 && res_mode >= 0 && res_mode <= 2 &&
-                    (res_mode == 0 || residual),
+                    (res_mode == 0 || residual) && (res_mode != 2 || residual_lo) &&
+                    (!out_lo || out_bf16),
                 "dfu_bn_apply_x3: bad args");
   const int64_t n = M * (C / 8);
   if (n == 0) return DFU_OK;
   hipLaunchKernelGGL(k_bn_apply_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, y, scale,
-                     shift, residual, res_mode, relu, (bf16_t*)out3, (bf16_t*)out_bf16, out_f32,
-                     (bf16_t*)y_bf16, M, C);
+                     shift, residual, (const bf16_t*)residual_lo, res_mode, relu, (bf16_t*)out_lo,
+                     (bf16_t*)out_bf16, out_f32, (bf16_t*)y_bf16, M, C);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
 
 extern "C" int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t W, int32_t C,
-                                  void* y3, void* y_bf16, uint8_t* argmax, int32_t P, int32_t Q,
+                                  void* y_lo, void* y_bf16, uint8_t* argmax, int32_t P, int32_t Q,
                                   void* stream) {
-  DFU_CHECK_ARG(x && y3 && y_bf16 && argmax && C % 8 == 0, "dfu_maxpool_fwd_x3: bad args");
+  DFU_CHECK_ARG(x && y_lo && y_bf16 && argmax && C % 8 == 0, "dfu_maxpool_fwd_x3: bad args");
   const int64_t n = (int64_t)B * P * Q * (C / 8);
   hipLaunchKernelGGL(k_maxpool_fwd_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, x, B,
-                     H, W, C, (bf16_t*)y3, (bf16_t*)y_bf16, argmax, P, Q);
+                     H, W, C, (bf16_t*)y_lo, (bf16_t*)y_bf16, argmax, P, Q);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
 
-extern "C" int dfu_avgpool_fwd_x3(const void* x3, int32_t B, int32_t HW, int32_t C, float* y,
-                                  void* stream) {
-  DFU_CHECK_ARG(x3 && y && C % 8 == 0, "dfu_avgpool_fwd_x3: bad args");
+extern "C" int dfu_avgpool_fwd_x3(const void* hi, const void* lo, int32_t B, int32_t HW,
+                                  int32_t C, float* y, void* stream) {
+  DFU_CHECK_ARG(hi && lo && y && C % 8 == 0, "dfu_avgpool_fwd_x3: bad args");
   const int64_t n = (int64_t)B * (C / 8);
   hipLaunchKernelGGL(k_avgpool_fwd_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream,
-                     (const bf16_t*)x3, B, HW, C, y);
+                     (const bf16_t*)hi, (const bf16_t*)lo, B, HW, C, y);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -55,6 +55,7 @@ class GemmDesc(ctypes.Structure):
         ("workspace", c_void_p), ("workspace_bytes", c_int64),
         ("tile_counters", c_void_p), ("tile_counters_len", c_int32),
         ("operand_type", c_int32),
+        ("a_seg", c_int32), ("a_lo", c_void_p),
     ]
 
 
@@ -149,9 +150,9 @@ PROTOTYPES = {
     "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, P],
     "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P],
     "dfu_patchify_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
-    "dfu_bn_apply_x3": [P, P, P, P, I32, I32, P, P, P, P, I64, I32, P],
+    "dfu_bn_apply_x3": [P, P, P, P, P, I32, I32, P, P, P, P, I64, I32, P],
     "dfu_maxpool_fwd_x3": [P, I32, I32, I32, I32, P, P, P, I32, I32, P],
-    "dfu_avgpool_fwd_x3": [P, I32, I32, I32, P, P],
+    "dfu_avgpool_fwd_x3": [P, P, I32, I32, I32, P, P],
     "dfu_layernorm_fwd_x3": [P, I64, I32, I32, P, P, F, P, P, P, P, P],
     "dfu_layernorm_fwd_h16": [P, I64, I32, I32, P, P, F, P, P, P, P, P],
     "dfu_gelu_x3": [P, I64, I32, P, P, P, P],

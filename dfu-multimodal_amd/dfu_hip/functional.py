@@ -479,18 +479,18 @@ def conv_weight_x3(w):
 
 
 def _take_x3(x):
-    """The fp32-accurate triple [rows][3C] a bf16x3 producer attached to activation x (and
-    detach it from x: each one has a single consumer); built from x itself (lo = 0) when x came
-    from elsewhere."""
-    t = getattr(x, "_dfu_x3", None)
-    if t is not None:
+    """The fp32-accurate split pair (hi, lo) of activation x, [rows][C] bf16 each: hi is x's own
+    bf16 rows, lo the residual a bf16x3 producer attached (detached from x here: each one has a
+    single consumer), or zeros when x came from elsewhere (a bf16 value is its own hi)."""
+    hi = rows_view(nhwc_bf16(x.detach()))
+    lo = getattr(x, "_dfu_lo", None)
+    if lo is not None:
         try:
-            del x._dfu_x3
+            del x._dfu_lo
         except AttributeError:
             pass
-        return t
-    xb = nhwc_bf16(x.detach())
-    return ops.split_x3(ops.cast_rows_f32(rows_view(xb).contiguous()), ops.X3_A)
+        return hi, lo
+    return hi, torch.zeros_like(hi)
 
 
 # ---------------------------------------------------------------------- BatchNorm helper
@@ -549,20 +549,22 @@ def conv_fwd(x_rows, geom, w_krsc, y, stats):
                  epilogue=L.EPI_BF16_STATS, stats=stats, conv=g)
 
 
-def conv_fwd_x3(x3_rows, geom, w3, y, stats):
-    """bf16x3: fp32 y[M, K] = conv(x) over the channel-tripled triple x3 [N*H*W, 3C] and KRSC'
-    weights; BN tile statistics of the unrounded outputs into stats."""
+def conv_fwd_x3(x_pair, geom, w3, y, stats):
+    """bf16x3: fp32 y[M, K] = conv(x) over the split pair x = (hi, lo) [N*H*W, C] (the GEMM
+    reads the channel-tripled hi | lo | hi) and KRSC' weights; BN tile statistics of the
+    unrounded outputs into stats."""
     g = geom
+    hi, lo = x_pair
     M = g.n * g.p * g.q
     C3 = 3 * g.c
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
-        ops.gemm(M, g.k, C3, x3_rows, C3, w3, C3, y, g.k, epilogue=L.EPI_F32_STATS, stats=stats,
-                 x3=True)
+        ops.gemm(M, g.k, C3, hi, g.c, w3, C3, y, g.k, epilogue=L.EPI_F32_STATS, stats=stats,
+                 x3=True, a_lo=lo)
     else:
         g3 = ops.ConvGeom(g.n, g.h, g.w, C3, g.k, g.r, g.s, g.stride, g.pad)
         K = g.r * g.s * C3
-        ops.gemm(M, g.k, K, x3_rows, 0, w3, K, y, g.k, a_mode=L.OPND_CONV_FWD,
-                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3, x3=True)
+        ops.gemm(M, g.k, K, hi, 0, w3, K, y, g.k, a_mode=L.OPND_CONV_FWD,
+                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3, x3=True, a_lo=lo)
 
 
 def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, w_flip=None, w_t=None):
@@ -658,7 +660,7 @@ class StemFn(torch.autograd.Function):
             af = _empty((M, Cout), F32, x.device)
             ops.bn_apply_x3(yf, bns.scale, bns.shift, None, 0, True, M, Cout, out_bf16=a,
                             out_f32=af, y_bf16=y)
-            out3, out, am, P2, Q2 = ops.maxpool_fwd_x3(af, B, P, Q, Cout)
+            out_lo, out, am, P2, Q2 = ops.maxpool_fwd_x3(af, B, P, Q, Cout)
         else:
             ops.gemm(M, Cout, Kp, col, Kp, wb, Kp, y, Cout, epilogue=L.EPI_BF16_STATS,
                      stats=stats)
@@ -676,7 +678,7 @@ class StemFn(torch.autograd.Function):
         ctx.save_for_backward(col, y, a, am, wb)
         res = out.permute(0, 3, 1, 2)
         if x3:
-            res._dfu_x3 = out3
+            res._dfu_lo = out_lo
         return res
 
     @staticmethod
@@ -753,31 +755,32 @@ class BottleneckFn(torch.autograd.Function):
             ops.bn_apply(y, st.scale, st.shift, residual, relu, out, M, geom.k, mask=mask)
             return y, out, st
 
-        def conv_bn_x3(x3rows, geom, w3x, bnmod, relu, res=None, res_mode=0, want3=True,
-                       want_bf=True, want_f32=False):
-            """bf16x3: fp32 conv + BN (+res) (+ReLU) -> (y bf16, out bf16, out triple, out
-            fp32, BN state)."""
+        def conv_bn_x3(xpair, geom, w3x, bnmod, relu, res=None, res_mode=0, want_pair=True,
+                       want_f32=False):
+            """bf16x3: fp32 conv + BN (+res) (+ReLU) -> (y bf16, out bf16 (hi), out lo, out
+            fp32, BN state); res_mode 2: res is a split pair."""
             M = geom.n * geom.p * geom.q
             yf = _empty((M, geom.k), F32, dev)
             stats = _empty((ops.stats_tiles(M), 2, geom.k), F32, dev)
-            conv_fwd_x3(x3rows, geom, w3x, yf, stats)
+            conv_fwd_x3(xpair, geom, w3x, yf, stats)
             st = _BN(bnmod, M, geom.k, dev)
             st.forward_coeffs(stats)
             y = _empty((M, geom.k), BF16, dev)
-            out = _empty((M, geom.k), BF16, dev) if want_bf else None
-            out3 = _empty((M, 3 * geom.k), BF16, dev) if want3 else None
+            out = _empty((M, geom.k), BF16, dev) if want_pair else None
+            lo = _empty((M, geom.k), BF16, dev) if want_pair else None
             of = _empty((M, geom.k), F32, dev) if want_f32 else None
-            ops.bn_apply_x3(yf, st.scale, st.shift, res, res_mode, relu, M, geom.k, out3=out3,
-                            out_bf16=out, out_f32=of, y_bf16=y)
-            return y, out, out3, of, st
+            rhi, rlo = res if res_mode == 2 else (res, None)
+            ops.bn_apply_x3(yf, st.scale, st.shift, rhi, res_mode, relu, M, geom.k, out_lo=lo,
+                            out_bf16=out, out_f32=of, y_bf16=y, residual_lo=rlo)
+            return y, out, lo, of, st
 
-        out3 = None
+        out_lo = None
         if x3mode:
-            y1, a1, a1_3, _, s1 = conv_bn_x3(xin3, g1, conv_weight_x3(mod.conv1.weight),
-                                              mod.bn1, True)
-            y2, a2, a2_3, _, s2 = conv_bn_x3(a1_3, g2, conv_weight_x3(mod.conv2.weight),
-                                              mod.bn2, True)
-            del a1_3
+            y1, a1, a1_lo, _, s1 = conv_bn_x3(xin3, g1, conv_weight_x3(mod.conv1.weight),
+                                               mod.bn1, True)
+            y2, a2, a2_lo, _, s2 = conv_bn_x3((a1, a1_lo), g2, conv_weight_x3(mod.conv2.weight),
+                                               mod.bn2, True)
+            del a1_lo
         else:
             y1, a1, s1 = conv_bn(xr, g1, w1, mod.bn1, True)
             y2, a2, s2 = conv_bn(a1, g2, w2, mod.bn2, True)
@@ -787,7 +790,7 @@ class BottleneckFn(torch.autograd.Function):
             wd = conv_weight_bf16(dconv.weight)
             if x3mode:
                 yd, _, _, idn, sd = conv_bn_x3(xin3, gd, conv_weight_x3(dconv.weight), dbn, False,
-                                               want3=False, want_bf=False, want_f32=True)
+                                               want_pair=False, want_f32=True)
                 res, res_mode = idn, 1
             else:
                 yd, idn, sd = conv_bn(xr, gd, wd, dbn, False)
@@ -796,9 +799,9 @@ class BottleneckFn(torch.autograd.Function):
             idn = xr
             res, res_mode = xin3, 2
         if x3mode:
-            y3, out, out3, _, s3 = conv_bn_x3(a2_3, g3, conv_weight_x3(mod.conv3.weight),
-                                              mod.bn3, True, res=res, res_mode=res_mode)
-            del a2_3, res, xin3
+            y3, out, out_lo, _, s3 = conv_bn_x3((a2, a2_lo), g3, conv_weight_x3(mod.conv3.weight),
+                                                 mod.bn3, True, res=res, res_mode=res_mode)
+            del a2_lo, res, xin3
             mask3 = None
         else:
             # bn3 + residual + ReLU also writes its ReLU bitmask: the backward reads M*C/8 bytes
@@ -822,8 +825,8 @@ class BottleneckFn(torch.autograd.Function):
         ctx.save_for_backward(xr, y1, a1, y2, a2, y3, out if mask3 is None else mask3, w1, w2,
                               w3, *( (yd, wd) if yd is not None else ()))
         res = from_rows(out, B, g3.p, g3.q, outc)
-        if out3 is not None:
-            res._dfu_x3 = out3
+        if out_lo is not None:
+            res._dfu_lo = out_lo
         return res
 
     @staticmethod
@@ -894,14 +897,14 @@ class BottleneckFn(torch.autograd.Function):
 class AvgPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
-        # bf16x3: the triple the producer attached; per-stage modes: that triple if the last block
+        # bf16x3: the split pair of the producer; per-stage modes: that pair if the last block
         # ran bf16x3 (a bf16 block's output is pooled in bf16)
-        x3 = _take_x3(x) if _x3() and (not _per_stage() or hasattr(x, "_dfu_x3")) else None
+        x3 = _take_x3(x) if _x3() and (not _per_stage() or hasattr(x, "_dfu_lo")) else None
         x = nhwc_bf16(x.detach())
         B, C, H, W = x.shape
         ctx.shape = (B, C, H, W)
         if x3 is not None:
-            y = ops.avgpool_fwd_x3(x3, B, H * W, C)
+            y = ops.avgpool_fwd_x3(x3[0], x3[1], B, H * W, C)
         else:
             y = ops.avgpool_fwd(rows_view(x), B, H * W, C)
         return y.view(B, C, 1, 1)

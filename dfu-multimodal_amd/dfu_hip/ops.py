@@ -93,9 +93,11 @@ def gemm_replay(records, stream=None):
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
          epilogue=L.EPI_BF16, alpha=1.0, bias=None, aux=None, ldaux=0, aux_out=None,
          ldaux_out=0, stats=None, split_k=0, ep_tokens=0, conv=None, tile=0, workspace=None,
-         operand_type=0, x3=False):
+         operand_type=0, x3=False, a_lo=None):
     """C = epilogue(A @ B^T).  `split_k` (F32_ACC only): 0 = library cost model, 1 = none.
     `x3`: a bf16x3 product (K tripled): the recorded algorithmic FLOPs count K / 3.
+    `a_lo`: split-pair A -- A is the hi buffer and a_lo the lo buffer ([rows][K / 3] each; the
+    conv forward: NHWC with conv.c / 3 channels), read as the K-segments hi | lo | hi.
     `tile`: 0 = library cost model, else a TILES id.  Split-K partials go to fp32 slabs in
     `workspace` (allocated here from the stream-ordered caching allocator when None) and are
     reduced deterministically by a second kernel."""
@@ -116,6 +118,9 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
     d.ldaux_out = int(ldaux_out)
     d.stats = stats.data_ptr() if stats is not None else None
     d.operand_type = int(operand_type)
+    if a_lo is not None:
+        d.a_seg = int(conv.c // 3 if a_mode == L.OPND_CONV_FWD else K // 3)
+        d.a_lo = a_lo.data_ptr()
     d.split_k = int(split_k)
     d.ep_tokens = int(ep_tokens)
     d.tile = int(tile)
@@ -137,7 +142,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
         if a_mode == L.OPND_CONV_DGRAD and conv is not None:
             flops /= conv.stride * conv.stride  # algorithmic: only the 1/stride^2 live taps
         gemm_record.append((d, flops, _algorithmic_bytes(d, conv),
-                            (A, B, C, bias, aux, aux_out, stats, workspace)))
+                            (A, B, C, bias, aux, aux_out, stats, workspace, a_lo)))
 
 
 _COUNTERS = {}
@@ -791,29 +796,34 @@ def patchify_f32_x3(x, ps):
     return out
 
 
-def bn_apply_x3(y, scale, shift, residual, res_mode, relu, M, C, out3=None, out_bf16=None,
-                out_f32=None, y_bf16=None):
+def bn_apply_x3(y, scale, shift, residual, res_mode, relu, M, C, out_lo=None, out_bf16=None,
+                out_f32=None, y_bf16=None, residual_lo=None):
+    """res_mode 2: residual is a split pair (residual = hi, residual_lo = lo); out_lo + out_bf16
+    write the output as a split pair (out_bf16 = hi)."""
     _req(y, F32, "bn_apply_x3")
-    check(lib().dfu_bn_apply_x3(ptr(y), ptr(scale), ptr(shift), ptr(residual), int(res_mode),
-                                int(relu), ptr(out3), ptr(out_bf16), ptr(out_f32), ptr(y_bf16),
-                                int(M), int(C), stream_ptr()), "dfu_bn_apply_x3")
+    check(lib().dfu_bn_apply_x3(ptr(y), ptr(scale), ptr(shift), ptr(residual), ptr(residual_lo),
+                                int(res_mode), int(relu), ptr(out_lo), ptr(out_bf16),
+                                ptr(out_f32), ptr(y_bf16), int(M), int(C), stream_ptr()),
+          "dfu_bn_apply_x3")
 
 
 def maxpool_fwd_x3(x, B, H, W, C):
+    """-> (lo [B*P*Q, C], hi = plain bf16 [B, P, Q, C], argmax, P, Q)"""
     _req(x, F32, "maxpool_fwd_x3")
     P = (H - 1) // 2 + 1
     Q = (W - 1) // 2 + 1
-    y3 = torch.empty((B * P * Q, 3 * C), dtype=BF16, device=x.device)
+    lo = torch.empty((B * P * Q, C), dtype=BF16, device=x.device)
     y = torch.empty((B, P, Q, C), dtype=BF16, device=x.device)
     am = torch.empty((B, P, Q, C), dtype=torch.uint8, device=x.device)
-    check(lib().dfu_maxpool_fwd_x3(ptr(x), B, H, W, C, ptr(y3), ptr(y), ptr(am), P, Q,
+    check(lib().dfu_maxpool_fwd_x3(ptr(x), B, H, W, C, ptr(lo), ptr(y), ptr(am), P, Q,
                                    stream_ptr()), "dfu_maxpool_fwd_x3")
-    return y3, y, am, P, Q
+    return lo, y, am, P, Q
 
 
-def avgpool_fwd_x3(x3, B, HW, C):
-    y = torch.empty((B, C), dtype=F32, device=x3.device)
-    check(lib().dfu_avgpool_fwd_x3(ptr(x3), B, HW, C, ptr(y), stream_ptr()), "dfu_avgpool_fwd_x3")
+def avgpool_fwd_x3(hi, lo, B, HW, C):
+    y = torch.empty((B, C), dtype=F32, device=hi.device)
+    check(lib().dfu_avgpool_fwd_x3(ptr(hi), ptr(lo), B, HW, C, ptr(y), stream_ptr()),
+          "dfu_avgpool_fwd_x3")
     return y
 
 

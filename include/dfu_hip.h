@@ -137,6 +137,13 @@ typedef struct dfu_gemm_desc {
   int32_t operand_type; /* 0 = bf16 A and B; 1 = fp16 A and B (the "parity" precision
                            mode's ViT forward: persistent tiles 8 / 9, K-contiguous A and B,
                            epilogues F32, F32_RESID, F16_DUAL, F16_GELU)                   */
+  /* Split-pair A (a_seg > 0; the bf16x3 ResNet forward's activations): the tripled K (or the
+   * conv's tripled channel axis, conv_c = 3 a_seg) reads its three segments hi | lo | hi of
+   * width a_seg from two bf16 buffers of row (pixel) stride a_seg: hi at A, lo at a_lo.
+   * K-contiguous (lda = a_seg, K = 3 a_seg) or conv-forward A; a_seg % 64 == 0; not on the
+   * phased 256x256 tiles (7-9). */
+  int32_t a_seg;
+  const void* a_lo;
 } dfu_gemm_desc;
 
 int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
@@ -457,16 +464,19 @@ int dfu_im2col_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_
 int dfu_patchify_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
                         int32_t C, int32_t H, int32_t W, int32_t ps, void* out, void* stream);
 /* BN apply on the fp32 conv output y: v = act(y*scale + shift (+ residual)); residual mode 0
- * none, 1 fp32 [M][C], 2 triple [M][3C].  Optional outputs: out3 (triple), out_bf16, out_f32,
- * y_bf16 (= bf16(y), the BN backward's input). */
+ * none, 1 fp32 [M][C], 2 split pair (residual = hi, residual_lo = lo, [M][C] bf16 each).
+ * Optional outputs: the split pair out_bf16 (hi, also the plain bf16 activation) + out_lo
+ * (out_lo requires out_bf16), out_f32, y_bf16 (= bf16(y), the BN backward's input). */
 int dfu_bn_apply_x3(const float* y, const float* scale, const float* shift, const void* residual,
-                    int32_t res_mode, int32_t relu, void* out3, void* out_bf16, float* out_f32,
-                    void* y_bf16, int64_t M, int32_t C, void* stream);
-/* resnet maxpool 3x3/s2/p1 on fp32 NHWC -> triple, plain bf16 and uint8 argmax. */
-int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y3,
+                    const void* residual_lo, int32_t res_mode, int32_t relu, void* out_lo,
+                    void* out_bf16, float* out_f32, void* y_bf16, int64_t M, int32_t C,
+                    void* stream);
+/* resnet maxpool 3x3/s2/p1 on fp32 NHWC -> split pair (y_bf16 = hi, y_lo) and uint8 argmax. */
+int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y_lo,
                        void* y_bf16, uint8_t* argmax, int32_t P, int32_t Q, void* stream);
-/* AdaptiveAvgPool2d(1) on a triple [B*HW][3C] -> fp32 [B][C]. */
-int dfu_avgpool_fwd_x3(const void* x3, int32_t B, int32_t HW, int32_t C, float* y, void* stream);
+/* AdaptiveAvgPool2d(1) on a split pair (hi, lo: [B*HW][C] bf16 each) -> fp32 [B][C]. */
+int dfu_avgpool_fwd_x3(const void* hi, const void* lo, int32_t B, int32_t HW, int32_t C, float* y,
+                       void* stream);
 /* timm LayerNorm -> triple [rows][3D] + plain bf16 [rows][D]; mean / rstd per row. */
 int dfu_layernorm_fwd_x3(const float* x, int64_t ldx, int32_t rows, int32_t D,
                          const float* gamma, const float* beta, float eps, void* out3,

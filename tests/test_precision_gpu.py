@@ -26,6 +26,12 @@ def _trip(t3, C):
     return t[:, :C] + t[:, C:2 * C], t[:, :C], t[:, 2 * C:]
 
 
+def _pair(x):
+    """Split pair of fp32 x: (hi, lo) bf16 with hi + lo = x to 2^-17."""
+    hi = x.to(torch.bfloat16)
+    return hi, (x - hi.float()).to(torch.bfloat16)
+
+
 def test_split_x3_patterns_and_padding():
     L, ops = _ops()
     torch.manual_seed(0)
@@ -127,23 +133,66 @@ def test_f32_stats_epilogue(tile):
         assert torch.allclose(st[t, 1].double(), q, rtol=1e-4, atol=1e-2)
 
 
-def test_conv_fwd_x3_matches_fp32_conv():
+@pytest.mark.parametrize("R,stride", [(3, 1), (3, 2), (1, 1), (1, 2)])
+def test_conv_fwd_x3_matches_fp32_conv(R, stride):
+    """Conv forward over a split pair (the GEMM reads hi | lo | hi from two buffers: K-major
+    for the 1x1 stride-1 case, the implicit-GEMM loader otherwise) against fp64 conv2d, and
+    bit-identical to the same GEMM over the materialised triple."""
     from dfu_hip import functional as Fn
     L, ops = _ops()
     torch.manual_seed(3)
     Bn, C, H, W, Kout = 4, 64, 14, 14, 128
     x = torch.randn(Bn, C, H, W, device=DEV)
-    w = torch.randn(Kout, C, 3, 3, device=DEV) * 0.05
-    for stride in (1, 2):
-        g = ops.ConvGeom(Bn, H, W, C, Kout, 3, 3, stride, 1)
-        x3 = ops.split_x3(x.permute(0, 2, 3, 1).reshape(-1, C), ops.X3_A)
-        y = torch.empty(Bn * g.p * g.q, Kout, device=DEV)
-        st = torch.empty(ops.stats_tiles(y.shape[0]), 2, Kout, device=DEV)
-        Fn.conv_fwd_x3(x3, g, Fn.conv_weight_x3(w), y, st)
-        ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=stride, padding=1)
-        ref = ref.permute(0, 2, 3, 1).reshape(-1, Kout)
-        err = ((y.double() - ref).norm() / ref.norm()).item()
-        assert err < 2e-5, (stride, err)
+    w = torch.randn(Kout, C, R, R, device=DEV) * 0.05
+    pad = R // 2
+    g = ops.ConvGeom(Bn, H, W, C, Kout, R, R, stride, pad)
+    rows = x.permute(0, 2, 3, 1).reshape(-1, C).contiguous()
+    y = torch.empty(Bn * g.p * g.q, Kout, device=DEV)
+    st = torch.empty(ops.stats_tiles(y.shape[0]), 2, Kout, device=DEV)
+    w3 = Fn.conv_weight_x3(w)
+    Fn.conv_fwd_x3(_pair(rows), g, w3, y, st)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=stride, padding=pad)
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, Kout)
+    err = ((y.double() - ref).norm() / ref.norm()).item()
+    assert err < 2e-5, (R, stride, err)
+    # the same contraction over the materialised triple [hi | lo | hi]
+    x3 = ops.split_x3(rows, ops.X3_A)
+    y3 = torch.empty_like(y)
+    M = y.shape[0]
+    if R == 1 and stride == 1:
+        ops.gemm(M, Kout, 3 * C, x3, 3 * C, w3, 3 * C, y3, Kout, epilogue=L.EPI_F32_STATS,
+                 stats=st, x3=True)
+    else:
+        g3 = ops.ConvGeom(Bn, H, W, 3 * C, Kout, R, R, stride, pad)
+        ops.gemm(M, Kout, R * R * 3 * C, x3, 0, w3, R * R * 3 * C, y3, Kout,
+                 a_mode=L.OPND_CONV_FWD, epilogue=L.EPI_F32_STATS, stats=st, conv=g3, x3=True)
+    assert torch.equal(y, y3)
+
+
+def test_split_pair_gemm_ragged_and_rejects_bad_pairs():
+    """K-major split pair on a ragged M (the lo buffer's rows past M are never read) and the
+    descriptor checks: lda must equal the segment, the segment a multiple of 64."""
+    L, ops = _ops()
+    torch.manual_seed(8)
+    M, N, C = 1001, 256, 192
+    x = torch.randn(M, C, device=DEV)
+    w = torch.randn(N, C, device=DEV) / math.sqrt(C)
+    hi, lo = _pair(x)
+    w3 = ops.split_x3(w, ops.X3_B)
+    y = torch.empty(M, N, device=DEV)
+    st = torch.empty(ops.stats_tiles(M), 2, N, device=DEV)
+    ops.gemm(M, N, 3 * C, hi, C, w3, 3 * C, y, N, epilogue=L.EPI_F32_STATS, stats=st, x3=True,
+             a_lo=lo)
+    ref = x.double() @ w.double().T
+    assert ((y.double() - ref).norm() / ref.norm()).item() < 2e-5
+    with pytest.raises(L.DfuError):
+        ops.gemm(M, N, 3 * C, hi, 2 * C, w3, 3 * C, y, N, epilogue=L.EPI_F32_STATS, stats=st,
+                 x3=True, a_lo=lo)
+    x2 = torch.randn(M, 96, device=DEV)
+    h2, l2 = _pair(x2)
+    with pytest.raises(L.DfuError):
+        ops.gemm(M, N, 288, h2, 96, ops.split_x3(torch.randn(N, 96, device=DEV), ops.X3_B), 288,
+                 y, N, epilogue=L.EPI_F32_STATS, stats=st, x3=True, a_lo=l2)
 
 
 def test_bn_apply_x3_residual_modes():
@@ -154,22 +203,23 @@ def test_bn_apply_x3_residual_modes():
     sc = torch.rand(C, device=DEV) + 0.5
     sh = torch.randn(C, device=DEV)
     res = torch.randn(M, C, device=DEV)
-    res3 = ops.split_x3(res, ops.X3_A)
-    for mode, r in ((0, None), (1, res), (2, res3)):
-        out3 = torch.empty(M, 3 * C, dtype=torch.bfloat16, device=DEV)
+    rhi, rlo = _pair(res)
+    for mode, r, rl in ((0, None, None), (1, res, None), (2, rhi, rlo)):
+        lo = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
         ob = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
         of = torch.empty(M, C, device=DEV)
         yb = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
-        ops.bn_apply_x3(y, sc, sh, r, mode, True, M, C, out3=out3, out_bf16=ob, out_f32=of,
-                        y_bf16=yb)
+        ops.bn_apply_x3(y, sc, sh, r, mode, True, M, C, out_lo=lo, out_bf16=ob, out_f32=of,
+                        y_bf16=yb, residual_lo=rl)
         ref = y * sc + sh + (res if mode else 0)
         ref = ref.clamp_min(0)
-        tol = 2e-6 if mode != 2 else 2e-5  # the triple residual carries 16 mantissa bits
+        tol = 2e-6 if mode != 2 else 2e-5  # the pair residual carries 16 mantissa bits
         assert torch.allclose(of, ref, rtol=tol, atol=tol), mode
-        v, h0, h2 = _trip(out3, C)
-        assert ((v - of).abs() <= of.abs() * 2.0 ** -16).all() and torch.equal(h0, h2)
+        assert ((ob.float() + lo.float() - of).abs() <= of.abs() * 2.0 ** -16).all()
         assert torch.equal(ob.float(), of.to(torch.bfloat16).float())
         assert torch.equal(yb, y.to(torch.bfloat16))
+    with pytest.raises(L.DfuError):  # a pair residual needs its lo buffer
+        ops.bn_apply_x3(y, sc, sh, rhi, 2, True, M, C, out_bf16=ob)
 
 
 def test_maxpool_and_avgpool_x3():
@@ -177,15 +227,14 @@ def test_maxpool_and_avgpool_x3():
     torch.manual_seed(5)
     B, H, W, C = 2, 112, 112, 64
     x = torch.randn(B, H, W, C, device=DEV)
-    y3, yb, am, P, Q = ops.maxpool_fwd_x3(x.reshape(-1, C), B, H, W, C)
+    ylo, yb, am, P, Q = ops.maxpool_fwd_x3(x.reshape(-1, C), B, H, W, C)
     ref = torch.nn.functional.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
-    v, _, _ = _trip(y3, C)
+    v = yb.float().reshape(-1, C) + ylo.float()
     assert torch.allclose(v.view(B, P, Q, C), ref, rtol=2e-5, atol=0)
     assert torch.equal(yb.float(), ref.to(torch.bfloat16).float())
-    # avgpool over a triple
+    # avgpool over a split pair
     t = torch.randn(B * 49, 2048, device=DEV)
-    t3 = ops.split_x3(t, ops.X3_A)
-    a = ops.avgpool_fwd_x3(t3, B, 49, 2048)
+    a = ops.avgpool_fwd_x3(*_pair(t), B, 49, 2048)
     assert torch.allclose(a, t.view(B, 49, 2048).mean(1), rtol=1e-5, atol=1e-6)
 
 

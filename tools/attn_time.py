@@ -37,5 +37,7 @@ tb = timeit(lambda: ops.attention_bwd(qkv, o, dout, lse, B, N, H, dh, scale, dq)
 qf = qkv.float()
 qb = torch.empty_like(qkv)
 tx = timeit(lambda: ops.attention_fwd_f32(qf, B, N, H, dh, scale, qkv_bf16=qb))
-print(f"attention fwd {tf:.1f} us ({fl / tf / 1e6:.0f} TFLOP/s)  bwd {tb:.1f} us "
-      f"({2.5 * fl / tb / 1e6:.0f} TFLOP/s)  fwd bf16x3 {tx:.1f} us")
+q16 = qkv.to(torch.float16)
+th = timeit(lambda: ops.attention_fwd_f16(q16, B, N, H, dh, scale))
+print(f"attention fwd {tf:.1f} us ({fl / tf / 1e6:.0f} TFLOP/s)  fwd fp16 {th:.1f} us  bwd "
+      f"{tb:.1f} us ({2.5 * fl / tb / 1e6:.0f} TFLOP/s)  fwd bf16x3 {tx:.1f} us")

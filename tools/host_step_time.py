@@ -24,7 +24,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--profile", action="store_true", help="cProfile the host side instead")
+    ap.add_argument("--precision", default="parity")
     a = ap.parse_args()
+    Fn.set_precision(a.precision)
+    if a.profile:
+        return profile()
     dev = torch.device("cuda", 0)
     torch.manual_seed(42)
     model, fwd = bench.build("fusion", dev)
@@ -94,7 +98,4 @@ def profile(steps=5):
 
 
 if __name__ == "__main__":
-    if "--profile" in sys.argv:
-        profile()
-    else:
-        main()
+    main()
