@@ -14,4 +14,4 @@ timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $
 python -c "import json;d=json.loads(open('$OUT/pair_bench.json').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'],d['precision_modes'],d['parity'])"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_pair -o bench -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt-precision --no-parity > $OUT/prof_pair_bench.json 2> $OUT/prof_pair_bench.err || { echo "rocprof rc=$?"; tail -5 $OUT/prof_pair_bench.err; exit 1; }
-cd $R && python tools/trace_phases.py $(ls $OUT/prof_pair/*/bench_kernel_trace.csv | head -1) | tail -5
+cd $R && python tools/trace_phases.py $OUT/prof_pair/bench_kernel_trace.csv | tail -5
