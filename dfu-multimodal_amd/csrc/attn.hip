@@ -451,38 +451,24 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
         dv[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
         dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
-      // software-pipelined over query-tile pairs: the S / dP MFMAs of pair u + 1 are issued
-      // before pair u's exponentials, so the MFMA -> exp -> pack -> MFMA chain of one pair runs
-      // under the next pair's products instead of stalling the wave
-      f32x4 st[2][2], dp[2][2];  // [buffer][hh]
-      auto products = [&](int u, f32x4* st_, f32x4* dp_) {
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int qt = 2 * u + hh;
-          st_[hh] = (f32x4){0.f, 0.f, 0.f, 0.f};
-          dp_[hh] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            st_[hh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * qt, ks, lane), kf[ks], st_[hh], 0, 0, 0);
-            dp_[hh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * qt, ks, lane), vf[ks], dp_[hh], 0, 0, 0);
-          }
-        }
-      };
-      products(0, st[0], dp[0]);
-#pragma unroll
+#pragma unroll 1
       for (int u = 0; u < KT / 2; ++u) {
-        const int cb = u & 1;
-        if (u + 1 < KT / 2) products(u + 1, st[cb ^ 1], dp[cb ^ 1]);
         f32x4 ph[2], dsh[2];
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-          const int q0 = 16 * (2 * u + hh) + 4 * g;
-          const f32x4 l4 = *(const f32x4*)(Ls + q0), e4 = *(const f32x4*)(Es + q0);
+          const int qt = 2 * u + hh;
+          f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Qs, 16 * qt, ks, lane), kf[ks], st, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(Ds, 16 * qt, ks, lane), vf[ks], dp, 0, 0, 0);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float pv = fast_exp2(fmaf(st[cb][hh][r], c, -l4[r]));
+            const int q = 16 * qt + 4 * g + r;
+            const float pv = fast_exp2(fmaf(st[r], c, -Ls[q]));
             ph[hh][r] = pv;
-            dsh[hh][r] = pv * (dp[cb][hh][r] - e4[r]);
+            dsh[hh][r] = pv * (dp[r] - Es[q]);
           }
         }
         const bf16x8 pb = pack_frag(ph[0], ph[1]);

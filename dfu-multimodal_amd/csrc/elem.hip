@@ -92,17 +92,29 @@ DFU_DEV void store_triple8(bf16_t* row, int C, int c, const float* f) {
   *(u32x4*)(row + C + c) = pack8(lo);
   *(u32x4*)(row + 2 * C + c) = h;
 }
+// 8 values as a split pair (csrc/precise.hip): hi at hi[e], lo = bf16(f - hi) at lo[e]
+DFU_DEV void store_pair8(bf16_t* hi, bf16_t* lo, int64_t e, const float* f) {
+  float h[8], l[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h[i] = bf2f(f2bf(f[i]));
+    l[i] = f[i] - h[i];
+  }
+  *(u32x4*)(hi + e) = pack8(h);
+  *(u32x4*)(lo + e) = pack8(l);
+}
 
 // out[m][k], m = (b, oh, ow), k = c*R*S + r*S + s; each thread writes one 16-B vector (8 k).
 // Stem im2col: fp32 NCHW input -> bf16 [B*P*Q][Kp] rows, k = (c, r, s) (OIHW weight order),
 // zero-padded to Kp.  Each thread owns one 16-byte chunk kv of the row (its 8 taps decoded
 // once); a block of VPR*RPB threads covers RPB consecutive rows per iteration, so a wave's
 // stores are contiguous row bytes.  One division per row decodes (b, oh, ow).
-// X3: the split-bf16 triple [hi | lo | hi] (row stride 3 Kp; csrc/precise.hip) instead.
+// X3: the split pair (hi rows in out, lo rows in out_lo, both row stride Kp; csrc/precise.hip).
 template <int VPR, bool X3 = false>
 __global__ __launch_bounds__(VPR * 16) void k_im2col_f32(
     const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int B, int C,
-    int H, int W, int R, int S, int stride, int pad, int P, int Q, bf16_t* __restrict__ out) {
+    int H, int W, int R, int S, int stride, int pad, int P, int Q, bf16_t* __restrict__ out,
+    bf16_t* __restrict__ out_lo = nullptr) {
   constexpr int RPB = 16;
   constexpr int Kp = VPR * 8;
   const int kv = threadIdx.x % VPR, rsub = threadIdx.x / VPR;
@@ -131,7 +143,7 @@ __global__ __launch_bounds__(VPR * 16) void k_im2col_f32(
       f[e] = ok ? xb[tc[e] * sc + ih * sh + iw * sw] : 0.f;
     }
     if constexpr (X3) {
-      store_triple8(out + (int64_t)m * 3 * Kp, Kp, kv * 8, f);
+      store_pair8(out, out_lo, (int64_t)m * Kp + kv * 8, f);
     } else {
       *(u32x4*)(out + (int64_t)m * Kp + kv * 8) = pack8(f);
     }
@@ -178,7 +190,7 @@ template <bool X3>
 __global__ __launch_bounds__(256) void k_im2col_lds(
     const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int B, int C,
     int H, int W, int R, int S, int stride, int pad, int P, int Q, int Kp,
-    bf16_t* __restrict__ out) {
+    bf16_t* __restrict__ out, bf16_t* __restrict__ out_lo = nullptr) {
   extern __shared__ float tile[];  // [C * R][W]
   const int KK = C * R * S;
   const int VPR = Kp / 8;
@@ -194,7 +206,7 @@ __global__ __launch_bounds__(256) void k_im2col_lds(
     tsx[e] = rs - r * S;
   }
   const int CR = C * R;
-  const int64_t ldo = X3 ? 3 * Kp : Kp;
+  const int64_t ldo = Kp;
   for (int row = blockIdx.x; row < B * P; row += gridDim.x) {
     const int b = row / P, oh = row - b * P;
     __syncthreads();  // the previous row's gathers are done
@@ -216,7 +228,7 @@ __global__ __launch_bounds__(256) void k_im2col_lds(
       if (cr < CR && iw < W) tile[cr * W + iw] = v[cr];
     __syncthreads();
     if (og >= groups) continue;
-    bf16_t* orow = out + (int64_t)row * Q * ldo + kv * 8;
+    const int64_t orow = (int64_t)row * Q * ldo + kv * 8;
     for (int ow = og; ow < Q; ow += groups) {
       const int iw0 = ow * stride - pad;
       float f[8];
@@ -226,9 +238,9 @@ __global__ __launch_bounds__(256) void k_im2col_lds(
         f[e] = (off[e] >= 0 && (unsigned)iw < (unsigned)W) ? tile[off[e] + iw] : 0.f;
       }
       if constexpr (X3) {
-        store_triple8(orow - kv * 8 + ow * ldo, Kp, kv * 8, f);
+        store_pair8(out, out_lo, orow + ow * ldo, f);
       } else {
-        *(u32x4*)(orow + ow * ldo) = pack8(f);
+        *(u32x4*)(out + orow + ow * ldo) = pack8(f);
       }
     }
   }
@@ -941,21 +953,24 @@ extern "C" int dfu_patchify_f32(const float* x, int64_t sn, int64_t sc, int64_t 
 extern "C" int dfu_im2col_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
                                  int32_t B, int32_t C, int32_t H, int32_t W, int32_t R, int32_t S,
                                  int32_t stride, int32_t pad, int32_t P, int32_t Q, void* out,
-                                 int32_t Kp, void* stream) {
-  DFU_CHECK_ARG(x && out && Kp == 160 && Kp >= C * R * S, "dfu_im2col_f32_x3: bad Kp=%d", Kp);
-  DFU_CHECK_ARG(((uintptr_t)out & 15) == 0, "dfu_im2col_f32_x3: out must be 16-B aligned");
+                                 void* out_lo, int32_t Kp, void* stream) {
+  DFU_CHECK_ARG(x && out && out_lo && Kp == 160 && Kp >= C * R * S, "dfu_im2col_f32_x3: bad Kp=%d",
+                Kp);
+  DFU_CHECK_ARG(((uintptr_t)out & 15) == 0 && ((uintptr_t)out_lo & 15) == 0,
+                "dfu_im2col_f32_x3: out and out_lo must be 16-B aligned");
   const int64_t rows = (int64_t)B * P * Q;
   DFU_CHECK_ARG(rows < (1ll << 31), "dfu_im2col_f32_x3: too many rows");
   if (im2col_lds_fits(C, R, W, Kp)) {
     hipLaunchKernelGGL(k_im2col_lds<true>, dim3(B * P), dim3(256), (size_t)C * R * W * 4,
                        (hipStream_t)stream, x, sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q,
-                       Kp, (bf16_t*)out);
+                       Kp, (bf16_t*)out, (bf16_t*)out_lo);
     DFU_LAUNCH_CHECK();
     return DFU_OK;
   }
   const int blocks = (int)((rows + 15) / 16 < 8192 ? (rows + 15) / 16 : 8192);
   hipLaunchKernelGGL((k_im2col_f32<20, true>), dim3(blocks), dim3(320), 0, (hipStream_t)stream,
-                     x, sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q, (bf16_t*)out);
+                     x, sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q, (bf16_t*)out,
+                     (bf16_t*)out_lo);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -428,14 +428,14 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
     DFU_CHECK_ARG(d->stats != nullptr, "dfu_gemm: STATS epilogue needs a stats slab");
   if (d->a_seg) {
     const bool conv_a = d->a_mode == DFU_OPND_CONV_FWD;
-    DFU_CHECK_ARG(d->a_lo != nullptr && d->a_seg > 0 && d->a_seg % 64 == 0 &&
+    DFU_CHECK_ARG(d->a_lo != nullptr && d->a_seg > 0 && d->a_seg % (conv_a ? 64 : 8) == 0 &&
                       (d->a_mode == DFU_OPND_KMAJOR || conv_a) &&
                       (conv_a ? d->conv_c == 3 * d->a_seg : (d->K == 3 * d->a_seg &&
                                                              d->lda == d->a_seg)) &&
                       ((uintptr_t)d->a_lo & 15) == 0 &&
                       ((const char*)d->a_lo - (const char*)d->A) % 2 == 0,
-                  "dfu_gemm: split-pair A needs a_lo, a_seg %% 64 == 0, K-contiguous or conv-"
-                  "forward A with K (conv_c) = 3 a_seg and lda = a_seg");
+                  "dfu_gemm: split-pair A needs a_lo, a_seg %% 8 == 0 (conv forward: %% 64), "
+                  "K-contiguous or conv-forward A with K (conv_c) = 3 a_seg and lda = a_seg");
     DFU_CHECK_ARG(pl.tile != T256x256p8 && pl.tile != T256x256ps && pl.tile != T192x256ps,
                   "dfu_gemm: split-pair A is not supported on the phased tiles (plan %d)",
                   pl.tile + 1);

@@ -219,12 +219,13 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
   const void* zero = (const void*)g_zero16;
   if constexpr (MODE == DFU_OPND_KMAJOR) {
     const bool kin = k0 + st.kc < kend;
-    // split-pair A: segment 1 of the tripled K from the lo buffer, segment 2 from hi again (the
-    // whole K-step lies in one segment: a_seg % 64 == 0, host-checked; a wave-uniform offset)
+    // split-pair A: segment 1 of the tripled K from the lo buffer, segment 2 from hi again, by
+    // this lane's 16-B chunk (a_seg % 8 == 0, host-checked: no chunk straddles two segments)
     int64_t adj = 0;
-    if (is_a && p.a_seg)
-      adj = k0 >= 2 * p.a_seg ? -2 * (int64_t)p.a_seg
-                              : (k0 >= p.a_seg ? p.a_lo_delta - p.a_seg : 0);
+    if (is_a && p.a_seg) {
+      const int k = k0 + st.kc;
+      adj = k >= 2 * p.a_seg ? -2 * (int64_t)p.a_seg : (k >= p.a_seg ? p.a_lo_delta - p.a_seg : 0);
+    }
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const bool ok = st.valid[i] && kin;
@@ -563,6 +564,8 @@ DFU_DEV int epi_stores(const GemmArgs& p) {
                             EPI == DFU_EPI_BF16_ADD || EPI == DFU_EPI_BF16_STATS;
   const int per = bf16_out && p.n8 ? T::FM * T::FN / 2 : T::FM * T::FN * (p.n4 ? 1 : 4);
   if constexpr (EPI == DFU_EPI_BF16_GELU) return 2 * per;
+  if constexpr (EPI == DFU_EPI_F32_STATS)  // split-pair output: two bf16 rows per fragment row
+    if (p.aux_out) return 2 * (p.n8 ? T::FM * T::FN / 2 : T::FM * T::FN * (p.n4 ? 1 : 4));
   if constexpr (EPI == DFU_EPI_F32_ACC)
     if ((p.slab == nullptr && p.split > 1) || p.counters != nullptr) return 0;
   return per;
@@ -841,6 +844,21 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
         for (int r = 0; r < 4; ++r) v[j][r] = acc[i][j][r];
       if constexpr (EPI == DFU_EPI_BF16_STATS) {
         st_row_bf16<FN>(rc, (int64_t)m * p.ldc, m < M, n0 + wc * WTN, N, p.n8, n4, lane, v);
+      } else if (p.aux_out) {
+        // split pair (the bf16x3 ResNet forward): hi = bf16(v) into C, lo = bf16(v - hi) into
+        // aux_out; the BN apply reads the pair and hi is also the BN backward's bf16 y
+        float lo[FN][4];
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float h = bf2f(f2bf(v[j][r]));
+            lo[j][r] = v[j][r] - h;
+            v[j][r] = h;
+          }
+        st_row_bf16<FN>(rc, (int64_t)m * p.ldc, m < M, n0 + wc * WTN, N, p.n8, n4, lane, v);
+        st_row_bf16<FN>(make_rsrc(p.aux_out), (int64_t)m * p.ldaux_out, m < M, n0 + wc * WTN, N,
+                        p.n8, n4, lane, lo);
       } else {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {

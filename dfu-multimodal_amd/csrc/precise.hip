@@ -129,12 +129,14 @@ DFU_DEV void ld8_pair(const bf16_t* hi, const bf16_t* lo, int64_t e, float* f) {
 }
 
 // ---------------------------------------------------------------- BatchNorm apply
-// out = act(y*scale + shift + res) from the fp32 conv output y (F32_STATS epilogue).
-// res_mode 0 none, 1 fp32 [M][C], 2 split pair (res = hi, res_lo = lo, [M][C] each).  Outputs
+// out = act(y*scale + shift + res) from the fp32 conv output y (F32_STATS epilogue), or from
+// the split pair (y = hi, y_lo = lo) that epilogue writes with aux_out (hi is then the BN
+// backward's bf16 y itself, so y_bf is not written).  res_mode 0 none, 1 fp32 [M][C], 2 split pair (res = hi, res_lo = lo, [M][C] each).  Outputs
 // (each optional): the pair hi = out_bf (the plain bf16 tensor the backward saves and the next
 // convolution's hi operand) and out_lo, fp32 (a residual), and y rounded to bf16 (the BN
 // backward's input).
-__global__ void k_bn_apply_x3(const float* __restrict__ y, const float* __restrict__ scale,
+__global__ void k_bn_apply_x3(const void* __restrict__ y, const bf16_t* __restrict__ y_lo,
+                              const float* __restrict__ scale,
                               const float* __restrict__ shift, const void* __restrict__ res,
                               const bf16_t* __restrict__ res_lo, int res_mode, int relu,
                               bf16_t* __restrict__ out_lo, bf16_t* __restrict__ out_bf,
@@ -148,8 +150,12 @@ __global__ void k_bn_apply_x3(const float* __restrict__ y, const float* __restri
     const int c = (int)(i - m * cv) * 8;
     const int64_t e = m * C + c;
     float f[8], r[8];
-    ld8_f32(y + e, f);
-    if (y_bf) *(u32x4*)(y_bf + e) = pack8(f);
+    if (y_lo) {
+      ld8_pair((const bf16_t*)y, y_lo, e, f);
+    } else {
+      ld8_f32((const float*)y + e, f);
+      if (y_bf) *(u32x4*)(y_bf + e) = pack8(f);
+    }
     if (res_mode == 1) ld8_f32((const float*)res + e, r);
     else if (res_mode == 2) ld8_pair((const bf16_t*)res, res_lo, e, r);
 #pragma unroll
@@ -342,8 +348,9 @@ extern "C" int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int
   return DFU_OK;
 }
 
-extern "C" int dfu_bn_apply_x3(const float* y, const float* scale, const float* shift,
-                               const void* residual, const void* residual_lo, int32_t res_mode,
+extern "C" int dfu_bn_apply_x3(const void* y, const void* y_lo, const float* scale,
+                               const float* shift, const void* residual,
+                               const void* residual_lo, int32_t res_mode,
                                int32_t relu, void* out_lo, void* out_bf16, float* out_f32,
                                void* y_bf16, int64_t M, int32_t C, void* stream) {
   DFU_CHECK_ARG(y && scale && shift && C % 8 == 0 && M >= 0 && res_mode >= 0 && res_mode <= 2 &&
@@ -352,8 +359,9 @@ extern "C" int dfu_bn_apply_x3(const float* y, const float* scale, const float* 
                 "dfu_bn_apply_x3: bad args");
   const int64_t n = M * (C / 8);
   if (n == 0) return DFU_OK;
-  hipLaunchKernelGGL(k_bn_apply_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, y, scale,
-                     shift, residual, (const bf16_t*)residual_lo, res_mode, relu, (bf16_t*)out_lo,
+  hipLaunchKernelGGL(k_bn_apply_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, y,
+                     (const bf16_t*)y_lo, scale, shift, residual, (const bf16_t*)residual_lo,
+                     res_mode, relu, (bf16_t*)out_lo,
                      (bf16_t*)out_bf16, out_f32, (bf16_t*)y_bf16, M, C);
   DFU_LAUNCH_CHECK();
   return DFU_OK;

@@ -549,22 +549,24 @@ def conv_fwd(x_rows, geom, w_krsc, y, stats):
                  epilogue=L.EPI_BF16_STATS, stats=stats, conv=g)
 
 
-def conv_fwd_x3(x_pair, geom, w3, y, stats):
-    """bf16x3: fp32 y[M, K] = conv(x) over the split pair x = (hi, lo) [N*H*W, C] (the GEMM
-    reads the channel-tripled hi | lo | hi) and KRSC' weights; BN tile statistics of the
-    unrounded outputs into stats."""
+def conv_fwd_x3(x_pair, geom, w3, y, stats, y_lo=None):
+    """bf16x3: y[M, K] = conv(x) over the split pair x = (hi, lo) [N*H*W, C] (the GEMM reads
+    the channel-tripled hi | lo | hi) and KRSC' weights, fp32 -- or with y_lo, the split pair
+    (y = bf16 hi, y_lo = lo) of the fp32 result; BN tile statistics of the unrounded outputs
+    into stats."""
     g = geom
     hi, lo = x_pair
     M = g.n * g.p * g.q
     C3 = 3 * g.c
+    out = dict(aux_out=y_lo, ldaux_out=g.k if y_lo is not None else 0)
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
         ops.gemm(M, g.k, C3, hi, g.c, w3, C3, y, g.k, epilogue=L.EPI_F32_STATS, stats=stats,
-                 x3=True, a_lo=lo)
+                 x3=True, a_lo=lo, **out)
     else:
         g3 = ops.ConvGeom(g.n, g.h, g.w, C3, g.k, g.r, g.s, g.stride, g.pad)
         K = g.r * g.s * C3
         ops.gemm(M, g.k, K, hi, 0, w3, K, y, g.k, a_mode=L.OPND_CONV_FWD,
-                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3, x3=True, a_lo=lo)
+                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3, x3=True, a_lo=lo, **out)
 
 
 def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, w_flip=None, w_t=None):
@@ -644,7 +646,7 @@ class StemFn(torch.autograd.Function):
         Cout = w.shape[0]
         x3 = _x3(mod)
         if x3:
-            col, P, Q = ops.im2col_f32_x3(xf, R, S, st, pad, Kp)  # [M][3 Kp] triple
+            (col, col_lo), P, Q = ops.im2col_f32_x3(xf, R, S, st, pad, Kp)  # split pair
         else:
             col, P, Q = ops.im2col_f32(xf, R, S, st, pad, Kp)
         M = B * P * Q
@@ -653,13 +655,16 @@ class StemFn(torch.autograd.Function):
         bns = _BN(bn, M, Cout, x.device)
         if x3:
             a = _empty((M, Cout), BF16, x.device)
-            yf = _empty((M, Cout), F32, x.device)
-            ops.gemm(M, Cout, 3 * Kp, col, 3 * Kp, weight_x3_rows(w, seg=Kp), 3 * Kp, yf, Cout,
-                     epilogue=L.EPI_F32_STATS, stats=stats, x3=True)
+            y_lo = _empty((M, Cout), BF16, x.device)  # the conv output as a split pair (y, y_lo)
+            ops.gemm(M, Cout, 3 * Kp, col, Kp, weight_x3_rows(w, seg=Kp), 3 * Kp, y, Cout,
+                     epilogue=L.EPI_F32_STATS, stats=stats, x3=True, a_lo=col_lo, aux_out=y_lo,
+                     ldaux_out=Cout)
+            del col_lo
             bns.forward_coeffs(stats)
             af = _empty((M, Cout), F32, x.device)
-            ops.bn_apply_x3(yf, bns.scale, bns.shift, None, 0, True, M, Cout, out_bf16=a,
-                            out_f32=af, y_bf16=y)
+            ops.bn_apply_x3(y, bns.scale, bns.shift, None, 0, True, M, Cout, out_bf16=a,
+                            out_f32=af, y_lo=y_lo)
+            del y_lo
             out_lo, out, am, P2, Q2 = ops.maxpool_fwd_x3(af, B, P, Q, Cout)
         else:
             ops.gemm(M, Cout, Kp, col, Kp, wb, Kp, y, Cout, epilogue=L.EPI_BF16_STATS,
@@ -698,7 +703,7 @@ class StemFn(torch.autograd.Function):
         if _wants(w):
             dw = grad_buffer(w).view(Cout, -1)
             K = C * R * S
-            # bf16 im2col rows: the col itself, or the hi segment of the bf16x3 triple
+            # bf16 im2col rows: the col itself, or the hi rows of the bf16x3 split pair
             ops.gemm(Cout, K, M, dy, Cout, col, col.stride(0), dw, K, a_mode=L.OPND_MNMAJOR,
                      b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
             grads_done(w)
@@ -760,18 +765,19 @@ class BottleneckFn(torch.autograd.Function):
             """bf16x3: fp32 conv + BN (+res) (+ReLU) -> (y bf16, out bf16 (hi), out lo, out
             fp32, BN state); res_mode 2: res is a split pair."""
             M = geom.n * geom.p * geom.q
-            yf = _empty((M, geom.k), F32, dev)
+            # the conv output as a split pair: y (= bf16(y), what the BN backward reads) + y_lo
+            y = _empty((M, geom.k), BF16, dev)
+            y_lo = _empty((M, geom.k), BF16, dev)
             stats = _empty((ops.stats_tiles(M), 2, geom.k), F32, dev)
-            conv_fwd_x3(xpair, geom, w3x, yf, stats)
+            conv_fwd_x3(xpair, geom, w3x, y, stats, y_lo=y_lo)
             st = _BN(bnmod, M, geom.k, dev)
             st.forward_coeffs(stats)
-            y = _empty((M, geom.k), BF16, dev)
             out = _empty((M, geom.k), BF16, dev) if want_pair else None
             lo = _empty((M, geom.k), BF16, dev) if want_pair else None
             of = _empty((M, geom.k), F32, dev) if want_f32 else None
             rhi, rlo = res if res_mode == 2 else (res, None)
-            ops.bn_apply_x3(yf, st.scale, st.shift, rhi, res_mode, relu, M, geom.k, out_lo=lo,
-                            out_bf16=out, out_f32=of, y_bf16=y, residual_lo=rlo)
+            ops.bn_apply_x3(y, st.scale, st.shift, rhi, res_mode, relu, M, geom.k, out_lo=lo,
+                            out_bf16=out, out_f32=of, residual_lo=rlo, y_lo=y_lo)
             return y, out, lo, of, st
 
         out_lo = None

@@ -775,15 +775,17 @@ def pack_conv_weight_x3(w):
 
 
 def im2col_f32_x3(x, R, S, stride, pad, Kp):
+    """-> ((hi, lo) split pair [B*P*Q][Kp] each, P, Q)"""
     _req(x, F32, "im2col_f32_x3")
     B, C, H, W = x.shape
     P = (H + 2 * pad - R) // stride + 1
     Q = (W + 2 * pad - S) // stride + 1
-    out = torch.empty((B * P * Q, 3 * Kp), dtype=BF16, device=x.device)
+    hi = torch.empty((B * P * Q, Kp), dtype=BF16, device=x.device)
+    lo = torch.empty((B * P * Q, Kp), dtype=BF16, device=x.device)
     sn, sc, sh, sw = x.stride()
     check(lib().dfu_im2col_f32_x3(ptr(x), sn, sc, sh, sw, B, C, H, W, R, S, stride, pad, P, Q,
-                                  ptr(out), Kp, stream_ptr()), "dfu_im2col_f32_x3")
-    return out, P, Q
+                                  ptr(hi), ptr(lo), Kp, stream_ptr()), "dfu_im2col_f32_x3")
+    return (hi, lo), P, Q
 
 
 def patchify_f32_x3(x, ps):
@@ -797,11 +799,13 @@ def patchify_f32_x3(x, ps):
 
 
 def bn_apply_x3(y, scale, shift, residual, res_mode, relu, M, C, out_lo=None, out_bf16=None,
-                out_f32=None, y_bf16=None, residual_lo=None):
-    """res_mode 2: residual is a split pair (residual = hi, residual_lo = lo); out_lo + out_bf16
-    write the output as a split pair (out_bf16 = hi)."""
-    _req(y, F32, "bn_apply_x3")
-    check(lib().dfu_bn_apply_x3(ptr(y), ptr(scale), ptr(shift), ptr(residual), ptr(residual_lo),
+                out_f32=None, y_bf16=None, residual_lo=None, y_lo=None):
+    """y fp32, or (y_lo given) the bf16 hi of a split pair; res_mode 2: residual is a split pair
+    (residual = hi, residual_lo = lo); out_lo + out_bf16 write the output as a split pair
+    (out_bf16 = hi)."""
+    _req(y, F32 if y_lo is None else BF16, "bn_apply_x3")
+    check(lib().dfu_bn_apply_x3(ptr(y), ptr(y_lo), ptr(scale), ptr(shift), ptr(residual),
+                                ptr(residual_lo),
                                 int(res_mode), int(relu), ptr(out_lo), ptr(out_bf16),
                                 ptr(out_f32), ptr(y_bf16), int(M), int(C), stream_ptr()),
           "dfu_bn_apply_x3")

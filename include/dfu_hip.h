@@ -140,8 +140,8 @@ typedef struct dfu_gemm_desc {
   /* Split-pair A (a_seg > 0; the bf16x3 ResNet forward's activations): the tripled K (or the
    * conv's tripled channel axis, conv_c = 3 a_seg) reads its three segments hi | lo | hi of
    * width a_seg from two bf16 buffers of row (pixel) stride a_seg: hi at A, lo at a_lo.
-   * K-contiguous (lda = a_seg, K = 3 a_seg) or conv-forward A; a_seg % 64 == 0; not on the
-   * phased 256x256 tiles (7-9). */
+   * K-contiguous (lda = a_seg, K = 3 a_seg; a_seg % 8 == 0) or conv-forward A (a_seg % 64
+   * == 0); not on the phased 256x256 tiles (7-9). */
   int32_t a_seg;
   const void* a_lo;
 } dfu_gemm_desc;
@@ -457,20 +457,25 @@ int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_t cols, int
 /* fp32 OIHW conv weight -> bf16 KRSC' with C' = 3C, pattern 1 along the channels. */
 int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int32_t C, int32_t R, int32_t S,
                             void* stream);
-/* dfu_im2col_f32 / dfu_patchify_f32 writing the pattern-0 triple (row stride 3 Kp / 3 K). */
+/* dfu_im2col_f32 writing the split pair: hi rows to out, lo rows to out_lo (row stride Kp each:
+ * the stem GEMM's split-pair A, dfu_gemm_desc.a_seg = Kp); dfu_patchify_f32_x3 writes the
+ * pattern-0 triple (row stride 3 K). */
 int dfu_im2col_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
                       int32_t C, int32_t H, int32_t W, int32_t R, int32_t S, int32_t stride,
-                      int32_t pad, int32_t P, int32_t Q, void* out, int32_t Kp, void* stream);
+                      int32_t pad, int32_t P, int32_t Q, void* out, void* out_lo, int32_t Kp,
+                      void* stream);
 int dfu_patchify_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
                         int32_t C, int32_t H, int32_t W, int32_t ps, void* out, void* stream);
-/* BN apply on the fp32 conv output y: v = act(y*scale + shift (+ residual)); residual mode 0
+/* BN apply on the conv output y: v = act(y*scale + shift (+ residual)).  y is fp32 [M][C]
+ * (y_lo null) or the split pair the F32_STATS epilogue writes with aux_out (y = hi, y_lo = lo,
+ * bf16 each; hi is then the BN backward's bf16 y and y_bf16 is not written).  Residual mode 0
  * none, 1 fp32 [M][C], 2 split pair (residual = hi, residual_lo = lo, [M][C] bf16 each).
  * Optional outputs: the split pair out_bf16 (hi, also the plain bf16 activation) + out_lo
- * (out_lo requires out_bf16), out_f32, y_bf16 (= bf16(y), the BN backward's input). */
-int dfu_bn_apply_x3(const float* y, const float* scale, const float* shift, const void* residual,
-                    const void* residual_lo, int32_t res_mode, int32_t relu, void* out_lo,
-                    void* out_bf16, float* out_f32, void* y_bf16, int64_t M, int32_t C,
-                    void* stream);
+ * (out_lo requires out_bf16), out_f32, y_bf16 (= bf16(y) for an fp32 y). */
+int dfu_bn_apply_x3(const void* y, const void* y_lo, const float* scale, const float* shift,
+                    const void* residual, const void* residual_lo, int32_t res_mode, int32_t relu,
+                    void* out_lo, void* out_bf16, float* out_f32, void* y_bf16, int64_t M,
+                    int32_t C, void* stream);
 /* resnet maxpool 3x3/s2/p1 on fp32 NHWC -> split pair (y_bf16 = hi, y_lo) and uint8 argmax. */
 int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y_lo,
                        void* y_bf16, uint8_t* argmax, int32_t P, int32_t Q, void* stream);

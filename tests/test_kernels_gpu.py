@@ -431,10 +431,10 @@ def test_pooling_and_layout():
         ref = F.unfold(xin, 7, padding=3, stride=2).transpose(1, 2).reshape(-1, 147)
         assert torch.equal(col[:, :147].float(), ref.to(torch.bfloat16).float()), "im2col"
         assert col[:, 147:].abs().max().item() == 0
-        # the bf16x3 triple [hi | lo | hi]: hi == the bf16 col, hi + lo == the fp32 unfold
-        c3, _, _ = ops.im2col_f32_x3(xin, 7, 7, 2, 3, 160)
-        assert torch.equal(c3[:, :160], col) and torch.equal(c3[:, 320:], col), "im2col x3 hi"
-        rec = c3[:, :147].float() + c3[:, 160:307].float()
+        # the bf16x3 split pair: hi == the bf16 col, hi + lo == the fp32 unfold
+        (c_hi, c_lo), _, _ = ops.im2col_f32_x3(xin, 7, 7, 2, 3, 160)
+        assert torch.equal(c_hi, col), "im2col x3 hi"
+        rec = c_hi[:, :147].float() + c_lo[:, :147].float()
         close(rec, ref, atol=1e-6, rtol=1e-5, what="im2col x3 hi + lo")
     pt = ops.patchify_f32(xi, 16)
     ref = F.unfold(xi, 16, stride=16).transpose(1, 2).reshape(-1, 768)

@@ -155,6 +155,14 @@ def test_conv_fwd_x3_matches_fp32_conv(R, stride):
     ref = ref.permute(0, 2, 3, 1).reshape(-1, Kout)
     err = ((y.double() - ref).norm() / ref.norm()).item()
     assert err < 2e-5, (R, stride, err)
+    # the same conv writing its output as a split pair (F32_STATS with aux_out): hi = bf16(y),
+    # lo = bf16(y - hi) of the very fp32 values above, and the same statistics
+    yh = torch.empty(y.shape, dtype=torch.bfloat16, device=DEV)
+    yl = torch.empty_like(yh)
+    st2 = torch.empty_like(st)
+    Fn.conv_fwd_x3(_pair(rows), g, w3, yh, st2, y_lo=yl)
+    assert torch.equal(yh, y.to(torch.bfloat16)) and torch.equal(st2, st)
+    assert torch.equal(yl, (y - yh.float()).to(torch.bfloat16))
     # the same contraction over the materialised triple [hi | lo | hi]
     x3 = ops.split_x3(rows, ops.X3_A)
     y3 = torch.empty_like(y)
@@ -169,30 +177,46 @@ def test_conv_fwd_x3_matches_fp32_conv(R, stride):
     assert torch.equal(y, y3)
 
 
-def test_split_pair_gemm_ragged_and_rejects_bad_pairs():
-    """K-major split pair on a ragged M (the lo buffer's rows past M are never read) and the
-    descriptor checks: lda must equal the segment, the segment a multiple of 64."""
+@pytest.mark.parametrize("C", [192, 160, 96])
+def test_split_pair_gemm_ragged_and_rejects_bad_pairs(C):
+    """K-major split pair on a ragged M (the lo buffer's rows past M are never read), segments
+    that are and are not K-step multiples (160: the stem's im2col rows; each lane's 16-B chunk
+    picks its segment), bit-identical to the materialised triple, and the descriptor check:
+    lda must equal the segment."""
     L, ops = _ops()
     torch.manual_seed(8)
-    M, N, C = 1001, 256, 192
+    M, N = 1001, 256
     x = torch.randn(M, C, device=DEV)
     w = torch.randn(N, C, device=DEV) / math.sqrt(C)
     hi, lo = _pair(x)
     w3 = ops.split_x3(w, ops.X3_B)
     y = torch.empty(M, N, device=DEV)
     st = torch.empty(ops.stats_tiles(M), 2, N, device=DEV)
-    ops.gemm(M, N, 3 * C, hi, C, w3, 3 * C, y, N, epilogue=L.EPI_F32_STATS, stats=st, x3=True,
-             a_lo=lo)
-    ref = x.double() @ w.double().T
-    assert ((y.double() - ref).norm() / ref.norm()).item() < 2e-5
+    for tile in (1, 11):
+        ops.gemm(M, N, 3 * C, hi, C, w3, 3 * C, y, N, epilogue=L.EPI_F32_STATS, stats=st,
+                 x3=True, a_lo=lo, tile=tile)
+        ref = x.double() @ w.double().T
+        assert ((y.double() - ref).norm() / ref.norm()).item() < 2e-5
+        y3 = torch.empty_like(y)
+        ops.gemm(M, N, 3 * C, ops.split_x3(x, ops.X3_A), 3 * C, w3, 3 * C, y3, N,
+                 epilogue=L.EPI_F32_STATS, stats=st, x3=True, tile=tile)
+        assert torch.equal(y, y3), tile
     with pytest.raises(L.DfuError):
         ops.gemm(M, N, 3 * C, hi, 2 * C, w3, 3 * C, y, N, epilogue=L.EPI_F32_STATS, stats=st,
                  x3=True, a_lo=lo)
-    x2 = torch.randn(M, 96, device=DEV)
-    h2, l2 = _pair(x2)
-    with pytest.raises(L.DfuError):
-        ops.gemm(M, N, 288, h2, 96, ops.split_x3(torch.randn(N, 96, device=DEV), ops.X3_B), 288,
-                 y, N, epilogue=L.EPI_F32_STATS, stats=st, x3=True, a_lo=l2)
+
+
+def test_stem_im2col_pair():
+    """The stem's fp32 im2col as a split pair: hi = bf16(col), hi + lo = col to 2^-17."""
+    L, ops = _ops()
+    torch.manual_seed(9)
+    x = torch.randn(2, 3, 224, 224, device=DEV)
+    (hi, lo), P, Q = ops.im2col_f32_x3(x, 7, 7, 2, 3, 160)
+    col = torch.nn.functional.unfold(x, 7, padding=3, stride=2).transpose(1, 2).reshape(-1, 147)
+    assert (P, Q) == (112, 112) and hi.shape == (2 * 112 * 112, 160)
+    assert torch.equal(hi[:, :147], col.to(torch.bfloat16)) and torch.all(hi[:, 147:] == 0)
+    v = hi[:, :147].float() + lo[:, :147].float()
+    assert ((v - col).abs() <= col.abs() * 2.0 ** -16).all() and torch.all(lo[:, 147:] == 0)
 
 
 def test_bn_apply_x3_residual_modes():
@@ -218,6 +242,13 @@ def test_bn_apply_x3_residual_modes():
         assert ((ob.float() + lo.float() - of).abs() <= of.abs() * 2.0 ** -16).all()
         assert torch.equal(ob.float(), of.to(torch.bfloat16).float())
         assert torch.equal(yb, y.to(torch.bfloat16))
+        # y as a split pair (the conv epilogue's form): the same output to the pair's 2^-17
+        yh, yl = _pair(y)
+        lo2, ob2 = torch.empty_like(lo), torch.empty_like(ob)
+        ops.bn_apply_x3(yh, sc, sh, r, mode, True, M, C, out_lo=lo2, out_bf16=ob2,
+                        residual_lo=rl, y_lo=yl)
+        v2 = ob2.float() + lo2.float()
+        assert torch.allclose(v2, ref, rtol=3e-5, atol=3e-5), mode
     with pytest.raises(L.DfuError):  # a pair residual needs its lo buffer
         ops.bn_apply_x3(y, sc, sh, rhi, 2, True, M, C, out_bf16=ob)
 
