@@ -133,15 +133,16 @@ DFU_DEV void ld8_pair(const bf16_t* hi, const bf16_t* lo, int64_t e, float* f) {
 // the split pair (y = hi, y_lo = lo) that epilogue writes with aux_out (hi is then the BN
 // backward's bf16 y itself, so y_bf is not written).  res_mode 0 none, 1 fp32 [M][C], 2 split pair (res = hi, res_lo = lo, [M][C] each).  Outputs
 // (each optional): the pair hi = out_bf (the plain bf16 tensor the backward saves and the next
-// convolution's hi operand) and out_lo, fp32 (a residual), and y rounded to bf16 (the BN
-// backward's input).
+// convolution's hi operand) and out_lo, fp32 (a residual), y rounded to bf16 (the BN backward's
+// input), and the ReLU bitmask (bit k of byte i = output element 8i + k > 0: the BN backward's
+// relu = 3 mask, 1/16 of the bytes of re-reading the output; k_bn_apply's format).
 __global__ void k_bn_apply_x3(const void* __restrict__ y, const bf16_t* __restrict__ y_lo,
                               const float* __restrict__ scale,
                               const float* __restrict__ shift, const void* __restrict__ res,
                               const bf16_t* __restrict__ res_lo, int res_mode, int relu,
                               bf16_t* __restrict__ out_lo, bf16_t* __restrict__ out_bf,
-                              float* __restrict__ out_f32, bf16_t* __restrict__ y_bf, int64_t M,
-                              int C) {
+                              float* __restrict__ out_f32, bf16_t* __restrict__ y_bf,
+                              uint8_t* __restrict__ relu_mask, int64_t M, int C) {
   const int cv = C / 8;
   const int64_t n = M * cv;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -167,6 +168,12 @@ __global__ void k_bn_apply_x3(const void* __restrict__ y, const bf16_t* __restri
     if (out_lo) st_pair8(out_bf, out_lo, e, f);
     else if (out_bf) *(u32x4*)(out_bf + e) = pack8(f);
     if (out_f32) st8_f32(out_f32 + e, f);
+    if (relu_mask) {
+      unsigned bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bits |= (unsigned)(f[k] > 0.f) << k;
+      relu_mask[i] = (uint8_t)bits;
+    }
   }
 }
 
@@ -352,7 +359,8 @@ extern "C" int dfu_bn_apply_x3(const void* y, const void* y_lo, const float* sca
                                const float* shift, const void* residual,
                                const void* residual_lo, int32_t res_mode,
                                int32_t relu, void* out_lo, void* out_bf16, float* out_f32,
-                               void* y_bf16, int64_t M, int32_t C, void* stream) {
+                               void* y_bf16, uint8_t* relu_mask, int64_t M, int32_t C,
+                               void* stream) {
   DFU_CHECK_ARG(y && scale && shift && C % 8 == 0 && M >= 0 && res_mode >= 0 && res_mode <= 2 &&
                     (res_mode == 0 || residual) && (res_mode != 2 || residual_lo) &&
                     (!out_lo || out_bf16),
@@ -362,7 +370,7 @@ extern "C" int dfu_bn_apply_x3(const void* y, const void* y_lo, const float* sca
   hipLaunchKernelGGL(k_bn_apply_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, y,
                      (const bf16_t*)y_lo, scale, shift, residual, (const bf16_t*)residual_lo,
                      res_mode, relu, (bf16_t*)out_lo,
-                     (bf16_t*)out_bf16, out_f32, (bf16_t*)y_bf16, M, C);
+                     (bf16_t*)out_bf16, out_f32, (bf16_t*)y_bf16, relu_mask, M, C);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

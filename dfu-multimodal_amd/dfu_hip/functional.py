@@ -654,7 +654,7 @@ class StemFn(torch.autograd.Function):
         stats = _empty((ops.stats_tiles(M), 2, Cout), F32, x.device)
         bns = _BN(bn, M, Cout, x.device)
         if x3:
-            a = _empty((M, Cout), BF16, x.device)
+            a = _empty((M * Cout // 8,), torch.uint8, x.device)  # bn1's ReLU bitmask
             y_lo = _empty((M, Cout), BF16, x.device)  # the conv output as a split pair (y, y_lo)
             ops.gemm(M, Cout, 3 * Kp, col, Kp, weight_x3_rows(w, seg=Kp), 3 * Kp, y, Cout,
                      epilogue=L.EPI_F32_STATS, stats=stats, x3=True, a_lo=col_lo, aux_out=y_lo,
@@ -662,8 +662,8 @@ class StemFn(torch.autograd.Function):
             del col_lo
             bns.forward_coeffs(stats)
             af = _empty((M, Cout), F32, x.device)
-            ops.bn_apply_x3(y, bns.scale, bns.shift, None, 0, True, M, Cout, out_bf16=a,
-                            out_f32=af, y_lo=y_lo)
+            ops.bn_apply_x3(y, bns.scale, bns.shift, None, 0, True, M, Cout, out_f32=af,
+                            y_lo=y_lo, relu_mask=a)
             del y_lo
             out_lo, out, am, P2, Q2 = ops.maxpool_fwd_x3(af, B, P, Q, Cout)
         else:
@@ -695,8 +695,8 @@ class StemFn(torch.autograd.Function):
         da = ops.maxpool_bwd(g, am, B, P, Q, Cout, P2, Q2).view(B * P * Q, Cout)
         M = B * P * Q
         dy = torch.empty_like(y)
-        if ctx.x3:  # the forward's own ReLU mask (its pre-activation was fp32)
-            ctx.bns.backward(da, y, a, 1, dy, None)
+        if ctx.x3:  # the forward's own ReLU bitmask (its pre-activation was fp32)
+            ctx.bns.backward(da, y, a, 3, dy, None)
         else:
             ctx.bns.backward(da, y, None, 2, dy, None)
         w = mod.conv1.weight
@@ -763,7 +763,7 @@ class BottleneckFn(torch.autograd.Function):
         def conv_bn_x3(xpair, geom, w3x, bnmod, relu, res=None, res_mode=0, want_pair=True,
                        want_f32=False):
             """bf16x3: fp32 conv + BN (+res) (+ReLU) -> (y bf16, out bf16 (hi), out lo, out
-            fp32, BN state); res_mode 2: res is a split pair."""
+            fp32, BN state, ReLU bitmask); res_mode 2: res is a split pair."""
             M = geom.n * geom.p * geom.q
             # the conv output as a split pair: y (= bf16(y), what the BN backward reads) + y_lo
             y = _empty((M, geom.k), BF16, dev)
@@ -776,16 +776,19 @@ class BottleneckFn(torch.autograd.Function):
             lo = _empty((M, geom.k), BF16, dev) if want_pair else None
             of = _empty((M, geom.k), F32, dev) if want_f32 else None
             rhi, rlo = res if res_mode == 2 else (res, None)
+            mask = _empty((M * geom.k // 8,), torch.uint8, dev) if relu else None
             ops.bn_apply_x3(y, st.scale, st.shift, rhi, res_mode, relu, M, geom.k, out_lo=lo,
-                            out_bf16=out, out_f32=of, residual_lo=rlo, y_lo=y_lo)
-            return y, out, lo, of, st
+                            out_bf16=out, out_f32=of, residual_lo=rlo, y_lo=y_lo, relu_mask=mask)
+            return y, out, lo, of, st, mask
 
         out_lo = None
+        masks = None
         if x3mode:
-            y1, a1, a1_lo, _, s1 = conv_bn_x3(xin3, g1, conv_weight_x3(mod.conv1.weight),
-                                               mod.bn1, True)
-            y2, a2, a2_lo, _, s2 = conv_bn_x3((a1, a1_lo), g2, conv_weight_x3(mod.conv2.weight),
-                                               mod.bn2, True)
+            y1, a1, a1_lo, _, s1, m1 = conv_bn_x3(xin3, g1, conv_weight_x3(mod.conv1.weight),
+                                                   mod.bn1, True)
+            y2, a2, a2_lo, _, s2, m2 = conv_bn_x3((a1, a1_lo), g2,
+                                                   conv_weight_x3(mod.conv2.weight), mod.bn2, True)
+            masks = (m1, m2)  # the BN + ReLU backward's masks (the pre-activations were fp32)
             del a1_lo
         else:
             y1, a1, s1 = conv_bn(xr, g1, w1, mod.bn1, True)
@@ -795,8 +798,8 @@ class BottleneckFn(torch.autograd.Function):
             gd = _geom(dconv, B, H, W)
             wd = conv_weight_bf16(dconv.weight)
             if x3mode:
-                yd, _, _, idn, sd = conv_bn_x3(xin3, gd, conv_weight_x3(dconv.weight), dbn, False,
-                                               want_pair=False, want_f32=True)
+                yd, _, _, idn, sd, _ = conv_bn_x3(xin3, gd, conv_weight_x3(dconv.weight), dbn,
+                                                  False, want_pair=False, want_f32=True)
                 res, res_mode = idn, 1
             else:
                 yd, idn, sd = conv_bn(xr, gd, wd, dbn, False)
@@ -805,10 +808,10 @@ class BottleneckFn(torch.autograd.Function):
             idn = xr
             res, res_mode = xin3, 2
         if x3mode:
-            y3, out, out_lo, _, s3 = conv_bn_x3((a2, a2_lo), g3, conv_weight_x3(mod.conv3.weight),
-                                                 mod.bn3, True, res=res, res_mode=res_mode)
+            y3, out, out_lo, _, s3, mask3 = conv_bn_x3((a2, a2_lo), g3,
+                                                        conv_weight_x3(mod.conv3.weight), mod.bn3,
+                                                        True, res=res, res_mode=res_mode)
             del a2_lo, res, xin3
-            mask3 = None
         else:
             # bn3 + residual + ReLU also writes its ReLU bitmask: the backward reads M*C/8 bytes
             # instead of the block output twice (reduce and apply)
@@ -828,7 +831,8 @@ class BottleneckFn(torch.autograd.Function):
             ctx.probes = (from_rows(a1, B, g1.p, g1.q, planes).detach().requires_grad_(True),
                           from_rows(a2, B, g2.p, g2.q, planes).detach().requires_grad_(True))
             mod._probes = ctx.probes
-        ctx.save_for_backward(xr, y1, a1, y2, a2, y3, out if mask3 is None else mask3, w1, w2,
+        ctx.masks = masks
+        ctx.save_for_backward(xr, y1, a1, y2, a2, y3, mask3, w1, w2,
                               w3, *( (yd, wd) if yd is not None else ()))
         res = from_rows(out, B, g3.p, g3.q, outc)
         if out_lo is not None:
@@ -853,10 +857,10 @@ class BottleneckFn(torch.autograd.Function):
                 conv_wgrad(dy, x, geom, grad_buffer(conv.weight))
                 grads_done(conv.weight)
 
-        # bn3 (+ residual) + relu: the mask from the forward's bitmask (bf16) or its output (x3)
+        # bn3 (+ residual) + relu: the ReLU bitmask its forward apply wrote
         dy3 = torch.empty_like(y3)
         dres = torch.empty_like(y3)
-        s3.backward(g, y3, out, 3 if out.dtype == torch.uint8 else True, dy3, dres)
+        s3.backward(g, y3, out, 3, dy3, dres)
         # downsample branch (its dgrad is added in place after conv1's, below)
         dyd = None
         if yd is not None:
@@ -871,9 +875,10 @@ class BottleneckFn(torch.autograd.Function):
         wgrad(mod.conv3, dy3, a2, g3)
         # bn2 + relu, conv2
         # BN + ReLU masks: recomputed from y (bf16), or in bf16x3 mode (fp32 pre-activations)
-        # read from the forward's outputs
+        # the bitmasks the forward apply wrote
         dy2 = torch.empty_like(y2)
-        s2.backward(da2, y2, a2 if ctx.x3 else None, 1 if ctx.x3 else 2, dy2, None)
+        m1, m2 = ctx.masks if ctx.masks is not None else (None, None)
+        s2.backward(da2, y2, m2, 3 if ctx.x3 else 2, dy2, None)
         da1 = torch.empty_like(a1)
         conv_dgrad(dy2, g2, w2, da1, w_flip=None if g2.stride != 1 else
                    conv_weight_flipped(mod.conv2.weight))
@@ -882,7 +887,7 @@ class BottleneckFn(torch.autograd.Function):
         wgrad(mod.conv2, dy2, a1, g2)
         # bn1 + relu, conv1 (+ identity gradient fused in the dgrad epilogue)
         dy1 = torch.empty_like(y1)
-        s1.backward(da1, y1, a1 if ctx.x3 else None, 1 if ctx.x3 else 2, dy1, None)
+        s1.backward(da1, y1, m1, 3 if ctx.x3 else 2, dy1, None)
         dx = None
         if ctx.x_requires_grad:
             dxr = _empty((M1, Cin), BF16, dev)

@@ -430,8 +430,8 @@ def bn_apply(y, scale, shift, residual, relu, out, M, C, mask=None):
 
 def bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres,
                   dgamma, dbeta, batch_stats=True, scale=None, shift=None):
-    """BN backward after the reduction: finalize the [blocks][2][C] partial sums (from
-    dfu_bn_bwd_reduce, or a DSTATS dgrad epilogue's per-128-row records) -> apply."""
+    """BN backward after the reduction: finalize the [blocks][2][C] partial sums of
+    dfu_bn_bwd_reduce -> apply."""
     relu = int(relu)
     coef = torch.empty((C, 3), dtype=F32, device=y.device)
     s = stream_ptr()
@@ -799,16 +799,15 @@ def patchify_f32_x3(x, ps):
 
 
 def bn_apply_x3(y, scale, shift, residual, res_mode, relu, M, C, out_lo=None, out_bf16=None,
-                out_f32=None, y_bf16=None, residual_lo=None, y_lo=None):
+                out_f32=None, y_bf16=None, residual_lo=None, y_lo=None, relu_mask=None):
     """y fp32, or (y_lo given) the bf16 hi of a split pair; res_mode 2: residual is a split pair
     (residual = hi, residual_lo = lo); out_lo + out_bf16 write the output as a split pair
-    (out_bf16 = hi)."""
+    (out_bf16 = hi); relu_mask (uint8 [M*C/8]): the ReLU bitmask for bn_bwd(relu=3)."""
     _req(y, F32 if y_lo is None else BF16, "bn_apply_x3")
     check(lib().dfu_bn_apply_x3(ptr(y), ptr(y_lo), ptr(scale), ptr(shift), ptr(residual),
-                                ptr(residual_lo),
-                                int(res_mode), int(relu), ptr(out_lo), ptr(out_bf16),
-                                ptr(out_f32), ptr(y_bf16), int(M), int(C), stream_ptr()),
-          "dfu_bn_apply_x3")
+                                ptr(residual_lo), int(res_mode), int(relu), ptr(out_lo),
+                                ptr(out_bf16), ptr(out_f32), ptr(y_bf16), ptr(relu_mask), int(M),
+                                int(C), stream_ptr()), "dfu_bn_apply_x3")
 
 
 def maxpool_fwd_x3(x, B, H, W, C):

@@ -471,11 +471,12 @@ int dfu_patchify_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int6
  * bf16 each; hi is then the BN backward's bf16 y and y_bf16 is not written).  Residual mode 0
  * none, 1 fp32 [M][C], 2 split pair (residual = hi, residual_lo = lo, [M][C] bf16 each).
  * Optional outputs: the split pair out_bf16 (hi, also the plain bf16 activation) + out_lo
- * (out_lo requires out_bf16), out_f32, y_bf16 (= bf16(y) for an fp32 y). */
+ * (out_lo requires out_bf16), out_f32, y_bf16 (= bf16(y) for an fp32 y), relu_mask (M*C/8
+ * bytes: bit k of byte i = output element 8i + k > 0, the dfu_bn_bwd_* relu = 3 mask). */
 int dfu_bn_apply_x3(const void* y, const void* y_lo, const float* scale, const float* shift,
                     const void* residual, const void* residual_lo, int32_t res_mode, int32_t relu,
-                    void* out_lo, void* out_bf16, float* out_f32, void* y_bf16, int64_t M,
-                    int32_t C, void* stream);
+                    void* out_lo, void* out_bf16, float* out_f32, void* y_bf16,
+                    uint8_t* relu_mask, int64_t M, int32_t C, void* stream);
 /* resnet maxpool 3x3/s2/p1 on fp32 NHWC -> split pair (y_bf16 = hi, y_lo) and uint8 argmax. */
 int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y_lo,
                        void* y_bf16, uint8_t* argmax, int32_t P, int32_t Q, void* stream);

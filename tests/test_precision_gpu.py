@@ -245,10 +245,15 @@ def test_bn_apply_x3_residual_modes():
         # y as a split pair (the conv epilogue's form): the same output to the pair's 2^-17
         yh, yl = _pair(y)
         lo2, ob2 = torch.empty_like(lo), torch.empty_like(ob)
+        mask = torch.empty(M * C // 8, dtype=torch.uint8, device=DEV)
         ops.bn_apply_x3(yh, sc, sh, r, mode, True, M, C, out_lo=lo2, out_bf16=ob2,
-                        residual_lo=rl, y_lo=yl)
+                        residual_lo=rl, y_lo=yl, relu_mask=mask)
         v2 = ob2.float() + lo2.float()
         assert torch.allclose(v2, ref, rtol=3e-5, atol=3e-5), mode
+        # the ReLU bitmask: bit k of byte i = output element 8i + k > 0 (of the fp32 output)
+        pos = ((ob2.float() + lo2.float()) > 0).view(-1, 8).to(torch.int32)
+        want = (pos << torch.arange(8, device=DEV, dtype=torch.int32)).sum(1).to(torch.uint8)
+        assert torch.equal(mask, want), mode
     with pytest.raises(L.DfuError):  # a pair residual needs its lo buffer
         ops.bn_apply_x3(y, sc, sh, rhi, 2, True, M, C, out_bf16=ob)
 
