@@ -57,7 +57,8 @@ class ConvGeom:
 
 
 TILES = {"auto": 0, "128x128": 1, "256x128": 2, "128x256": 3, "256x256": 4, "128x128o2": 5,
-         "128x128w4": 6, "256x256p8": 7}
+         "128x128w4": 6, "256x256p8": 7, "256x256ps": 8, "192x256ps": 9, "256x64": 10,
+         "128x64o2": 11}
 
 # Optional recording of GEMM launches (bench.py's roofline): when set to a list, every
 # dfu_gemm call appends (descriptor, algorithmic flops, tensors it touches) — the tensor
