@@ -235,6 +235,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
         s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (t >= KT - 2 && 16 * t >= N) continue;  // all keys past N: masked below, no MFMAs
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           s[t] = mfma16<H16>(row_frag(Ks, 16 * t, ks, lane), qf[ks], s[t]);
@@ -408,6 +409,10 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
       f32x4 s[KT];
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
+        s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        // key tiles past N (the last of NPAD's 32-row rounding) hold only zero K rows: their
+        // dS adds exactly 0 to dQ, so they are skipped (bit-identical)
+        if (t >= KT - 2 && 16 * t >= N) continue;
         f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -457,6 +462,10 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const int qt = 2 * u + hh;
+          if (qt >= QT) {  // a query tile past N: P = 0 (LSE = +inf), nothing to add
+            ph[hh] = dsh[hh] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
           f32x4 st = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
