@@ -324,7 +324,17 @@ __global__ __launch_bounds__(64 * NW) void k_attn_fwd(const bf16_t* __restrict__
 // items: QT query tiles (dQ: recompute S and P, dP^T = V dO^T, dS = P (dP - delta),
 // dQ^T = K^T dS^T) and QT key tiles (dK/dV: S = Q K^T, dP = dO V^T; dV^T += dO^T P,
 // dK^T += Q^T dS).
-template <int KT>
+// Q16: qkv is the fp16 tensor of the "parity" mode's forward, rounded to bf16 while staging
+// (the bf16 backward's operands; no bf16 copy of qkv is written in the forward).
+DFU_DEV u32x4 f16x8_to_bf16x8(u32x4 v) {
+  const f16x8 h = __builtin_bit_cast(f16x8, v);
+  float f[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = (float)h[e];
+  return pack8(f);
+}
+
+template <int KT, bool Q16 = false>
 __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict__ qkv,
                                                         const bf16_t* __restrict__ o,
                                                         const bf16_t* __restrict__ dout,
@@ -367,6 +377,11 @@ __global__ __launch_bounds__(512) void k_attn_bwd_fused(const bf16_t* __restrict
     if (idx >= NPAD * 8) break;
     const u32x4 z = {0u, 0u, 0u, 0u};
     const bool in = row < N;
+    if constexpr (Q16) {
+      pq[i] = f16x8_to_bf16x8(pq[i]);
+      pk[i] = f16x8_to_bf16x8(pk[i]);
+      pv[i] = f16x8_to_bf16x8(pv[i]);
+    }
     const u32x4 vq = in ? pq[i] : z, vk = in ? pk[i] : z, vv = in ? pv[i] : z,
                 vd = in ? pd[i] : z, vo = in ? po[i] : z;
     const int off = r128_off(row, chunk);
@@ -766,18 +781,34 @@ extern "C" int dfu_attention_fwd_f32(const float* qkv, int32_t B, int32_t N, int
   return DFU_OK;
 }
 
-extern "C" int dfu_attention_bwd(const void* qkv, const void* o, const void* dout,
-                                 const float* lse, int32_t B, int32_t N, int32_t H, int32_t dh,
-                                 float scale, float* delta, void* dqkv, void* stream) {
+namespace {
+template <bool Q16>
+int attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse, int32_t B,
+                  int32_t N, int32_t H, int32_t dh, float scale, float* delta, void* dqkv,
+                  void* stream) {
   DFU_CHECK_ARG(qkv && o && dout && lse && delta && dqkv && B > 0 && H > 0,
                 "dfu_attention_bwd: bad args");
   DFU_CHECK_ARG(dh == 64, "dfu_attention_bwd: head dim %d unsupported (64 only)", dh);
   DFU_CHECK_ARG(N > 0 && N <= 256, "dfu_attention_bwd: N=%d unsupported (<= 256)", N);
   const int KT = dfu_attention_npad(N) / 16;
   hipStream_t s = (hipStream_t)stream;
-#define CALL(K) hipLaunchKernelGGL(k_attn_bwd_fused<K>, dim3(B * H), dim3(512), 0, s, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse, N, H, scale, (bf16_t*)dqkv)
+#define CALL(K) hipLaunchKernelGGL((k_attn_bwd_fused<K, Q16>), dim3(B * H), dim3(512), 0, s, (const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)dout, lse, N, H, scale, (bf16_t*)dqkv)
   DISPATCH_KT(KT, CALL)
 #undef CALL
   DFU_LAUNCH_CHECK();
   return DFU_OK;
+}
+}  // namespace
+
+extern "C" int dfu_attention_bwd(const void* qkv, const void* o, const void* dout,
+                                 const float* lse, int32_t B, int32_t N, int32_t H, int32_t dh,
+                                 float scale, float* delta, void* dqkv, void* stream) {
+  return attention_bwd<false>(qkv, o, dout, lse, B, N, H, dh, scale, delta, dqkv, stream);
+}
+
+extern "C" int dfu_attention_bwd_qkv16(const void* qkv16, const void* o, const void* dout,
+                                       const float* lse, int32_t B, int32_t N, int32_t H,
+                                       int32_t dh, float scale, float* delta, void* dqkv,
+                                       void* stream) {
+  return attention_bwd<true>(qkv16, o, dout, lse, B, N, H, dh, scale, delta, dqkv, stream);
 }

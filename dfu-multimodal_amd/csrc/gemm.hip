@@ -293,8 +293,9 @@ extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* spl
                 d->operand_type);
   if (d->epilogue == DFU_EPI_F16_DUAL || d->epilogue == DFU_EPI_F16_GELU) {
     DFU_CHECK_ARG(d->operand_type == 1, "dfu_gemm: the F16 epilogues need operand_type 1");
-    DFU_CHECK_ARG(d->aux_out != nullptr && d->ldaux_out >= d->N,
-                  "dfu_gemm: F16_DUAL / F16_GELU need aux_out (ldaux_out >= N)");
+    DFU_CHECK_ARG((d->epilogue == DFU_EPI_F16_DUAL && d->aux_out == nullptr) ||
+                      (d->aux_out != nullptr && d->ldaux_out >= d->N),
+                  "dfu_gemm: F16_GELU needs aux_out (F16_DUAL: NULL or ldaux_out >= N)");
     DFU_CHECK_ARG(d->epilogue != DFU_EPI_F16_GELU || d->ldc >= 2LL * d->N,
                   "dfu_gemm: F16_GELU needs ldc >= 2N");
   }
@@ -390,8 +391,9 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
                 d->operand_type);
   if (d->epilogue == DFU_EPI_F16_DUAL || d->epilogue == DFU_EPI_F16_GELU) {
     DFU_CHECK_ARG(d->operand_type == 1, "dfu_gemm: the F16 epilogues need operand_type 1");
-    DFU_CHECK_ARG(d->aux_out != nullptr && d->ldaux_out >= d->N,
-                  "dfu_gemm: F16_DUAL / F16_GELU need aux_out (ldaux_out >= N)");
+    DFU_CHECK_ARG((d->epilogue == DFU_EPI_F16_DUAL && d->aux_out == nullptr) ||
+                      (d->aux_out != nullptr && d->ldaux_out >= d->N),
+                  "dfu_gemm: F16_GELU needs aux_out (F16_DUAL: NULL or ldaux_out >= N)");
     DFU_CHECK_ARG(d->epilogue != DFU_EPI_F16_GELU || d->ldc >= 2LL * d->N,
                   "dfu_gemm: F16_GELU needs ldc >= 2N");
   }

@@ -110,7 +110,7 @@ DFU_DEV int ps_epi_stores(const GemmArgs& p) {
   const int cs = EPI == DFU_EPI_BF16_DGELU && p.stats ? (p.n4 ? 4 : 16) : 0;
   const int per16 = p.n8 ? 2 * NI : 4 * NI * (p.n4 ? 1 : 4);  // one 16-bit output
   if constexpr (EPI == DFU_EPI_X3_GELU) return 4 * per16;
-  if constexpr (EPI == DFU_EPI_F16_DUAL) return 2 * per16;
+  if constexpr (EPI == DFU_EPI_F16_DUAL) return (p.aux_out ? 2 : 1) * per16;
   if constexpr (EPI == DFU_EPI_F16_GELU) return 3 * per16;
   return (EPI == DFU_EPI_BF16_GELU ? 2 * per : per) + cs;
 }
@@ -235,7 +235,7 @@ DFU_DEV void ps_epilogue_n(const GemmArgs& p, f32x4 (&acc)[2 * FMH][4], int m0, 
       } else if constexpr (EPI == DFU_EPI_F16_DUAL) {
         // fp16 operand of the next fp16 step, bf16 copy for the backward
         st_row_bf16<2, 0, true>(rc, mc * p.ldc, okm, n0w, N, p.n8, n4, lane, v);
-        st_row_bf16<2, 0>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, v);
+        if (p.aux_out) st_row_bf16<2, 0>(ro, mc * p.ldaux_out, okm, n0w, N, p.n8, n4, lane, v);
       } else if constexpr (EPI == DFU_EPI_F16_GELU) {
         // gelu(pre) as fp16 (fc2's operand, column 0) and bf16 (the backward's h, column N)
         float g[2][4], d[2][4];

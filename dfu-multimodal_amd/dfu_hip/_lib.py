@@ -125,6 +125,7 @@ PROTOTYPES = {
     "dfu_attention_fwd": [P, I32, I32, I32, I32, F, P, P, P],
     "dfu_attention_fwd_f16": [P, I32, I32, I32, I32, F, P, P, P, P],
     "dfu_attention_bwd": [P, P, P, P, I32, I32, I32, I32, F, P, P, P],
+    "dfu_attention_bwd_qkv16": [P, P, P, P, I32, I32, I32, I32, F, P, P, P],
     "dfu_attention_npad": [I32],
     "dfu_vit_cls_rows": [P, P, P, I32, I32, I32, P],
     "dfu_vit_embed_bwd": [P, I32, I32, I32, P, P, P, P, P, P],

@@ -605,11 +605,13 @@ def attention_fwd_f16(qkv16, B, N, H, dh, scale):
 
 
 def attention_bwd(qkv, o, dout, lse, B, N, H, dh, scale, dqkv=None):
+    """dqkv (bf16) of attention; qkv bf16, or the fp16 qkv of the parity forward."""
     delta = torch.empty((B * H, attention_npad(N)), dtype=F32, device=qkv.device)
     if dqkv is None:
-        dqkv = torch.empty_like(qkv)
-    check(lib().dfu_attention_bwd(ptr(qkv), ptr(o), ptr(dout), ptr(lse), B, N, H, dh, scale,
-                                  ptr(delta), ptr(dqkv), stream_ptr()), "dfu_attention_bwd")
+        dqkv = torch.empty(qkv.shape, dtype=BF16, device=qkv.device)
+    fn = lib().dfu_attention_bwd_qkv16 if qkv.dtype == F16 else lib().dfu_attention_bwd
+    check(fn(ptr(qkv), ptr(o), ptr(dout), ptr(lse), B, N, H, dh, scale, ptr(delta), ptr(dqkv),
+             stream_ptr()), "dfu_attention_bwd")
     return dqkv
 
 

@@ -87,8 +87,8 @@ enum dfu_epilogue {
                                 [M][3N] (ldc >= 3N; segments at columns 0, N, 2N), aux_out
                                 bf16 = gelu'(pre).  Persistent 256x256 tile only.            */
   DFU_EPI_F16_DUAL = 14,     /* v = alpha*acc + bias: C fp16 = v (the next fp16 GEMM's or the
-                                fp16 attention's operand), aux_out bf16 = v (what the bf16
-                                backward saves; may be NULL).  operand_type 1 only.           */
+                                fp16 attention's operand), aux_out bf16 = v when non-NULL (a
+                                bf16 copy for the backward).  operand_type 1 only.            */
   DFU_EPI_F16_GELU = 15      /* fp16 forward of timm Mlp.fc1 + GELU: pre = acc + bias: C =
                                 [fp16 gelu(pre) | bf16 gelu(pre)], 16-bit [M][2N] (ldc >= 2N;
                                 fc2's fp16 operand at column 0, the backward's bf16 h at
@@ -365,6 +365,11 @@ int dfu_attention_fwd_f16(const void* qkv, int32_t B, int32_t N, int32_t H, int3
 int dfu_attention_bwd(const void* qkv, const void* o, const void* dout, const float* lse,
                       int32_t B, int32_t N, int32_t H, int32_t dh, float scale, float* delta,
                       void* dqkv, void* stream);
+/* The same backward reading the "parity" forward's fp16 qkv (rounded to bf16 while staging: no
+ * bf16 copy of qkv is stored in the forward); o, dout and dqkv bf16 as above. */
+int dfu_attention_bwd_qkv16(const void* qkv16, const void* o, const void* dout, const float* lse,
+                            int32_t B, int32_t N, int32_t H, int32_t dh, float scale,
+                            float* delta, void* dqkv, void* stream);
 int dfu_attention_npad(int32_t N);
 
 /* ---------------------------------------------------------------- ViT embedding ----- */

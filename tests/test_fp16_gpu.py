@@ -58,9 +58,10 @@ def test_f16_dual_epilogue(M, N, K):
     ref = A.float() @ B.float().T + bias
     assert ((C.double() - ref.double()).abs() <= ref.double().abs() * 2.0 ** -10 + 1e-4).all()
     assert ((Cb.double() - ref.double()).abs() <= ref.double().abs() * 2.0 ** -7 + 1e-4).all()
-    with pytest.raises(L.DfuError):  # the bf16 copy is required
-        ops.gemm(M, N, K, A, K, B, K, C, N, epilogue=L.EPI_F16_DUAL, bias=bias, tile=8,
-                 operand_type=L.OPERAND_F16)
+    C1 = torch.empty_like(C)  # the bf16 copy is optional (the parity forward's qkv)
+    ops.gemm(M, N, K, A, K, B, K, C1, N, epilogue=L.EPI_F16_DUAL, bias=bias, tile=8,
+             operand_type=L.OPERAND_F16)
+    assert torch.equal(C1, C)
 
 
 @pytest.mark.parametrize("M,N,K", [(12608, 3072, 768), (1000, 520, 200)])
@@ -104,6 +105,23 @@ def test_attention_fwd_f16_matches_sdpa(N):
     assert ((ob.double() - o16.double()).abs() <= o16.double().abs() * 2.0 ** -7 + 1e-3).all()
     lref = torch.logsumexp(s, -1).reshape(B * H, N)
     assert torch.allclose(lse[:, :N].double(), lref, rtol=2.0 ** -14, atol=1e-5)
+
+
+@pytest.mark.parametrize("N", [197, 50])
+def test_attention_bwd_reads_fp16_qkv(N):
+    """dfu_attention_bwd_qkv16 (the parity forward saves qkv in fp16 only) equals the bf16
+    backward on bf16(qkv16): the kernel rounds while staging exactly as the cast does."""
+    L, ops = _ops()
+    torch.manual_seed(8)
+    B, H, dh = 4, 12, 64
+    D = H * dh
+    q16 = (torch.randn(B * N, 3 * D, device=DEV) * 2).to(F16)
+    qb = q16.to(torch.bfloat16)
+    o, lse = ops.attention_fwd(qb, B, N, H, dh, dh ** -0.5)
+    do = (torch.randn(B * N, D, device=DEV) * 0.1).to(torch.bfloat16)
+    d16 = ops.attention_bwd(q16, o, do, lse, B, N, H, dh, dh ** -0.5)
+    db = ops.attention_bwd(qb, o, do, lse, B, N, H, dh, dh ** -0.5)
+    assert d16.dtype == torch.bfloat16 and torch.equal(d16, db)
 
 
 def test_layernorm_h16_and_cast_f16():
