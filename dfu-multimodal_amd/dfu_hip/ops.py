@@ -77,11 +77,15 @@ def _algorithmic_bytes(d, conv):
     a = {L.OPND_CONV_FWD: act_in,
          L.OPND_CONV_DGRAD: 2 * conv.n * conv.p * conv.q * conv.k if conv is not None else 0
          }.get(d.a_mode, 2 * M * K)
+    if d.a_seg:  # split pair: hi and lo read once each (the tripled K reads hi twice)
+        a = a * 2 // 3
     b = act_in if d.b_mode == L.OPND_CONV_WGRAD_X else 2 * N * K
     e = d.epilogue
+    # bytes per output element: C (+ read-modify-write / side outputs)
     c = {L.EPI_F32: 4, L.EPI_F32_RESID: 8, L.EPI_F32_ACC: 8, L.EPI_PATCH: 4, L.EPI_F32_STATS: 4,
          L.EPI_BF16_GELU: 4, L.EPI_BF16_DGELU: 4, L.EPI_BF16_ADD: 4,
-         L.EPI_BF16_DSTATS: 4}.get(e, 2) * M * N
+         L.EPI_X3_GELU: 8, L.EPI_F16_GELU: 6,
+         L.EPI_F16_DUAL: 4 if d.aux_out else 2}.get(e, 2) * M * N
     return a + b + c
 
 
