@@ -17,6 +17,10 @@ const Entry kTable128x128o2[] = {
     E(DFU_OPND_KMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_F32),
     E(DFU_OPND_MNMAJOR, DFU_OPND_MNMAJOR, DFU_EPI_F32_ACC),
     E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_BF16_STATS),
+    // split-K forms of the bf16x3 forward's long-K, few-tile convolutions (fp32 slabs; the BN
+    // statistics and the output pair by dfu_stats_pair_f32 after the reduction)
+    E(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_ACC),
+    E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_F32_ACC),
     E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_BF16),  // stride-1 dgrad on flipped weights
     E(DFU_OPND_CONV_DGRAD, DFU_OPND_CONV_DGRAD_W, DFU_EPI_BF16),
     E(DFU_OPND_CONV_DGRAD, DFU_OPND_CONV_DGRAD_W, DFU_EPI_BF16_ADD),

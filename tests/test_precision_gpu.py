@@ -177,6 +177,44 @@ def test_conv_fwd_x3_matches_fp32_conv(R, stride):
     assert torch.equal(y, y3)
 
 
+@pytest.mark.parametrize("R,stride,C,H", [(3, 1, 512, 7), (3, 2, 256, 28), (1, 1, 2048, 7)])
+def test_conv_fwd_x3_split_k_path(R, stride, C, H):
+    """The layer-3/4 shapes whose 128x128 tiles cannot fill the chip run split-K (fp32 slabs,
+    then dfu_stats_pair_f32): the pair and the BN tile statistics against fp64 conv2d, and the
+    same within fp32 summation order of the unsplit F32_STATS path."""
+    from dfu_hip import functional as Fn
+    L, ops = _ops()
+    torch.manual_seed(10)
+    Bn, Kout = 64, 512 if C >= 512 else 256
+    x = torch.randn(Bn, C, H, H, device=DEV)
+    w = torch.randn(Kout, C, R, R, device=DEV) / math.sqrt(C * R * R)
+    pad = R // 2
+    g = ops.ConvGeom(Bn, H, H, C, Kout, R, R, stride, pad)
+    M = Bn * g.p * g.q
+    assert Fn._x3_split(M, Kout, R * R * 3 * C)
+    rows = x.permute(0, 2, 3, 1).reshape(-1, C).contiguous()
+    w3 = Fn.conv_weight_x3(w)
+    outs = []
+    old = Fn._X3_SPLIT
+    try:
+        for split in (True, False):
+            Fn._X3_SPLIT = split
+            yh = torch.empty(M, Kout, dtype=torch.bfloat16, device=DEV)
+            yl = torch.empty_like(yh)
+            st = torch.empty(ops.stats_tiles(M), 2, Kout, device=DEV)
+            Fn.conv_fwd_x3(_pair(rows), g, w3, yh, st, y_lo=yl)
+            outs.append((yh.float() + yl.float(), st))
+    finally:
+        Fn._X3_SPLIT = old
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=stride, padding=pad)
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, Kout)
+    for y, st in outs:
+        assert ((y.double() - ref).norm() / ref.norm()).item() < 2e-5
+    (ys, ss), (yu, su) = outs
+    assert ((ys - yu).norm() / yu.norm()).item() < 2e-5
+    assert ((ss - su).norm() / su.norm()).item() < 1e-4
+
+
 @pytest.mark.parametrize("C", [192, 160, 96])
 def test_split_pair_gemm_ragged_and_rejects_bad_pairs(C):
     """K-major split pair on a ragged M (the lo buffer's rows past M are never read), segments
