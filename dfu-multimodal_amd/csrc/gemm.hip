@@ -77,14 +77,15 @@ const TunedPlan kTuned[] = {
 #include "gemm_tuned.inc"
     {-1, -1, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
 
-// the dispatch key of a descriptor's kernel: its epilogue, | kF16Key for fp16 operands
+// the dispatch key of a descriptor's kernel: its epilogue, | kF16Key for fp16 operands,
+// | kX3Key for interleaved bf16x3 pairs (also the tuned-plan table's epilogue field)
 inline int epi_key(const dfu_gemm_desc* d) {
-  return d->epilogue | (d->operand_type == 1 ? kF16Key : 0);
+  return d->epilogue | (d->operand_type == 1 ? kF16Key : 0) | (d->x3_pairs ? kX3Key : 0);
 }
 
 const TunedPlan* find_tuned(const dfu_gemm_desc* d) {
   const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
-  const int epi = d->epilogue;
+  const int epi = d->epilogue | (d->x3_pairs ? kX3Key : 0);
   for (const TunedPlan& t : kTuned) {
     if (t.a != d->a_mode || t.b != d->b_mode || t.e != epi || t.M != d->M ||
         t.N != d->N || t.K != d->K)
@@ -428,16 +429,21 @@ extern "C" int dfu_gemm(const dfu_gemm_desc* d, void* stream) {
     DFU_CHECK_ARG(d->ldb >= round8(d->N), "dfu_gemm: MN-major B needs ldb >= round8(N)");
   if (d->epilogue == DFU_EPI_BF16_STATS || d->epilogue == DFU_EPI_F32_STATS)
     DFU_CHECK_ARG(d->stats != nullptr, "dfu_gemm: STATS epilogue needs a stats slab");
+  DFU_CHECK_ARG(d->x3_pairs == 0 || (d->x3_pairs == 1 && d->a_seg > 0 && d->operand_type == 0),
+                "dfu_gemm: x3_pairs (0/1) needs split-pair A (a_seg > 0) and bf16 operands");
   if (d->a_seg) {
     const bool conv_a = d->a_mode == DFU_OPND_CONV_FWD;
-    DFU_CHECK_ARG(d->a_lo != nullptr && d->a_seg > 0 && d->a_seg % (conv_a ? 64 : 8) == 0 &&
+    const int nseg = d->x3_pairs ? 2 : 3;  // interleaved pairs: K = 2 a_seg (a_seg % 32 == 0)
+    const int align = d->x3_pairs ? 32 : (conv_a ? 64 : 8);
+    DFU_CHECK_ARG(d->a_lo != nullptr && d->a_seg > 0 && d->a_seg % align == 0 &&
                       (d->a_mode == DFU_OPND_KMAJOR || conv_a) &&
-                      (conv_a ? d->conv_c == 3 * d->a_seg : (d->K == 3 * d->a_seg &&
-                                                             d->lda == d->a_seg)) &&
+                      (conv_a ? d->conv_c == nseg * d->a_seg : (d->K == nseg * d->a_seg &&
+                                                                d->lda == d->a_seg)) &&
                       ((uintptr_t)d->a_lo & 15) == 0 &&
                       ((const char*)d->a_lo - (const char*)d->A) % 2 == 0,
-                  "dfu_gemm: split-pair A needs a_lo, a_seg %% 8 == 0 (conv forward: %% 64), "
-                  "K-contiguous or conv-forward A with K (conv_c) = 3 a_seg and lda = a_seg");
+                  "dfu_gemm: split-pair A needs a_lo, a_seg %% 8 == 0 (conv forward: %% 64; "
+                  "x3_pairs: %% 32), K-contiguous or conv-forward A with K (conv_c) = 3 a_seg "
+                  "(x3_pairs: 2 a_seg) and lda = a_seg");
     DFU_CHECK_ARG(pl.tile != T256x256p8 && pl.tile != T256x256ps && pl.tile != T192x256ps,
                   "dfu_gemm: split-pair A is not supported on the phased tiles (plan %d)",
                   pl.tile + 1);

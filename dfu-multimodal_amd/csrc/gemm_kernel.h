@@ -84,6 +84,8 @@ struct GemmArgs {
   // Split-pair A (dfu_gemm_desc.a_seg > 0, the bf16x3 ResNet forward): the tripled K is read
   // as segments [hi | lo | hi] of width a_seg from two buffers of row (pixel) stride a_seg,
   // hi at A and lo at A + a_lo_delta (elements); a_pix = the conv gather's pixel stride.
+  // Interleaved pairs (the kernel's X3 instantiations, dfu_gemm_desc.x3_pairs): K = 2 a_seg,
+  // each K-step of 64 is [hi | lo] of 32 real k, and the kernel forms the three products.
   int a_seg, a_pix;
   int64_t a_lo_delta;
   int n4;       // N and every leading dimension % 4 == 0: one vector access per 4 columns
@@ -208,7 +210,7 @@ DFU_DEV void glds16(const void* src, char* lds_dst) {
 
 // Issue this thread's NLD LDS-DMA instructions for K-step kt into `tile` (IS_A: the A operand,
 // which may be in split-pair form, GemmArgs::a_seg).
-template <int MODE, int NLD, int NW, bool IS_A = false>
+template <int MODE, int NLD, int NW, bool IS_A = false, bool X3 = false>
 DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_t* base,
                         int64_t ld, int MN_bound, int kt, int kend, int tid, char* tile) {
   constexpr bool is_a = IS_A;
@@ -224,7 +226,13 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
     int64_t adj = 0;
     if (is_a && p.a_seg) {
       const int k = k0 + st.kc;
-      adj = k >= 2 * p.a_seg ? -2 * (int64_t)p.a_seg : (k >= p.a_seg ? p.a_lo_delta - p.a_seg : 0);
+      if constexpr (X3) {  // k = 64q + 32 seg + r -> real column 32q + r of hi (seg 0) or lo
+        const int seg = (k >> 5) & 1;
+        adj = (seg ? p.a_lo_delta : 0) - 32 * ((k >> 6) + seg);
+      } else {
+        adj = k >= 2 * p.a_seg ? -2 * (int64_t)p.a_seg
+                               : (k >= p.a_seg ? p.a_lo_delta - p.a_seg : 0);
+      }
     }
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
@@ -236,12 +244,17 @@ DFU_DEV void issue_tile(const GemmArgs& p, const LoadState<NLD>& st, const bf16_
     const uint32_t rs = fdiv((uint32_t)k0, p.div_c);
     int c0 = k0 - (int)rs * p.cc;
     int64_t adj = 0;
-    if (p.a_seg) {  // split-pair input: channel segment 1 from the lo buffer, 2 from hi again
-      const int seg = c0 >= 2 * p.a_seg ? 2 : (c0 >= p.a_seg ? 1 : 0);
-      c0 -= seg * p.a_seg;
-      adj = seg == 1 ? p.a_lo_delta : 0;
+    if constexpr (X3) {  // interleaved pairs: this lane's chunk is hi (kc < 32) or lo of the
+      c0 = (c0 >> 1) + (st.kc & 31);  // 32 real channels from c0 / 2
+      adj = (st.kc & 32) ? p.a_lo_delta : 0;
+    } else {
+      if (p.a_seg) {  // split-pair input: channel segment 1 from the lo buffer, 2 from hi again
+        const int seg = c0 >= 2 * p.a_seg ? 2 : (c0 >= p.a_seg ? 1 : 0);
+        c0 -= seg * p.a_seg;
+        adj = seg == 1 ? p.a_lo_delta : 0;
+      }
+      c0 += st.kc;
     }
-    c0 += st.kc;
     const uint32_t r = fdiv(rs, p.div_s);
     const int sx = (int)(rs - r * p.cs);
     const bool kin = k0 < kend;
@@ -973,7 +986,8 @@ DFU_DEV void epilogue(const GemmArgs& p, f32x4 (&acc)[T::FM][T::FN], int m0, int
 }
 
 // ------------------------------------------------------------------------------ kernel
-template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0, int NW = 8>
+template <int AMODE, int BMODE, int EPI, int TM, int TN, int OCC = 1, int NST = 0, int NW = 8,
+          bool X3 = false>
 __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   using T = Tile<TM, TN, OCC, NST, NW>;
   constexpr int WGN = T::WGN, WTM = T::WTM, WTN = T::WTN;
@@ -1052,7 +1066,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   load_init<BMODE, T::NLDB, NW>(p, sb, p.B, p.ldb, in0, p.N, tid);
   auto issue_next = [&](char* stage) {
     if (!(p.dbg & 4)) {
-    issue_tile<AMODE, T::NLDA, NW, true>(p, sa, p.A, p.lda, p.m_ld_bound, ikb + ik, p.K, tid,
+    issue_tile<AMODE, T::NLDA, NW, true, X3>(p, sa, p.A, p.lda, p.m_ld_bound, ikb + ik, p.K, tid,
                                          stage);
     issue_tile<BMODE, T::NLDB, NW>(p, sb, p.B, p.ldb, p.n_ld_bound, ikb + ik, p.K, tid,
                                stage + T::A_BYTES);
@@ -1079,6 +1093,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   // so the LDS latency overlaps MFMAs (counted lgkmcnt waits) instead of draining per group.
   auto compute = [&](const char* la) {
     const char* lb = la + T::A_BYTES;
+    static_assert(!X3 || (FM * FN < 32 && AK && BKc), "interleaved pairs: K-contiguous, <= 64x64 per wave");
     if constexpr (FM * FN >= 32) {
       // 256x256: 128 accumulator registers leave room for one k-half of fragments at a time
 #pragma unroll
@@ -1121,14 +1136,27 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
           for (int j = 0; j < FN; ++j) pin(fb[ks][j]);
         }
       }
+      if constexpr (X3) {
+        // interleaved pairs: k-half 0 holds hi and 1 holds lo of the same 32 real k, so the
+        // step is hi·hi + lo·hi + hi·lo (the tripled-K sum, from 2 operand tiles instead of 3)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+        for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+          for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][j], fa[ks][i], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[t == 2][j], fa[t == 1][i],
+                                                                 acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks][j], fa[ks][i], acc[i][j], 0, 0, 0);
+      }
     }
   };
 

@@ -4,6 +4,7 @@
 // K-contiguous B (the MN-major loader works in 128-column sub-images).
 #include "gemm_table.h"
 #define E(A, B, Ep) DFU_ENTRY_W4(A, B, Ep, 256, 64, 1, dfu::T256x64)
+#define EX(A, B, Ep) DFU_ENTRY_X3(A, B, Ep, 256, 64, 1, 4, dfu::T256x64)
 namespace dfu {
 const Entry kTable256x64[] = {
     E(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_BF16),
@@ -13,6 +14,9 @@ const Entry kTable256x64[] = {
     E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_BF16_STATS),
     E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_F32_STATS),
     E(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_BF16),  // stride-1 dgrad on flipped weights
+    // bf16x3 forward on interleaved split pairs (dfu_gemm_desc.x3_pairs)
+    EX(DFU_OPND_KMAJOR, DFU_OPND_KMAJOR, DFU_EPI_F32_STATS),
+    EX(DFU_OPND_CONV_FWD, DFU_OPND_KMAJOR, DFU_EPI_F32_STATS),
 };
 const int kTable256x64N = sizeof(kTable256x64) / sizeof(Entry);
 }  // namespace dfu

@@ -6,6 +6,8 @@ namespace dfu {
 typedef void (*gemm_fn)(const GemmArgs);
 // Entry.e of an fp16-operand kernel (dfu_gemm_desc.operand_type 1): the epilogue | kF16Key
 constexpr int kF16Key = 64;
+// Entry.e of an interleaved-pair bf16x3 kernel (dfu_gemm_desc.x3_pairs): the epilogue | kX3Key
+constexpr int kX3Key = 128;
 struct Entry {
   int a, b, e, tile;
   gemm_fn fn;
@@ -65,4 +67,10 @@ extern const int kTable128x64o2N;
   {                                                                             \
     A, B, E, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv, OCCv, 0, 4>,             \
         dfu::Tile<TMv, TNv, OCCv, 0, 4>::LDS_BYTES, dfu::Tile<TMv, TNv, OCCv, 0, 4>::NT \
+  }
+// interleaved-pair bf16x3 kernels (gemm_kernel<..., X3 = true>), keyed epilogue | kX3Key
+#define DFU_ENTRY_X3(A, B, E, TMv, TNv, OCCv, NWv, TID)                                      \
+  {                                                                                          \
+    A, B, (E) | dfu::kX3Key, TID, &dfu::gemm_kernel<A, B, E, TMv, TNv, OCCv, 0, NWv, true>,   \
+        dfu::Tile<TMv, TNv, OCCv, 0, NWv>::LDS_BYTES, dfu::Tile<TMv, TNv, OCCv, 0, NWv>::NT  \
   }

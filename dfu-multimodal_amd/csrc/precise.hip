@@ -85,14 +85,23 @@ __global__ void k_split_x3(const float* __restrict__ in, int64_t ld_in, int rows
     float f[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = c + e < cols ? in[r * ld_in + c + e] : 0.f;
-    st_triple8(out + r * 3 * seg, seg, c, f, pattern);
+    if (pattern == 2) {  // interleaved pairs [rows][2 seg]: per 32 columns [hi 32 | lo 32]
+      float hi[8], lo[8];
+      split8(f, hi, lo);
+      bf16_t* o = out + r * 2 * seg + 2 * (c & ~31) + (c & 31);
+      *(u32x4*)o = pack8(hi);
+      *(u32x4*)(o + 32) = pack8(lo);
+    } else {
+      st_triple8(out + r * 3 * seg, seg, c, f, pattern);
+    }
     if (hi_out) *(u32x4*)(hi_out + r * ld_hi + c) = pack8(f);
   }
 }
 
-// fp32 OIHW conv weight -> bf16 KRSC' (C' = 3C, pattern B: [hi | hi | lo] along channels).
+// fp32 OIHW conv weight -> bf16 KRSC' (pattern 1: C' = 3C, [hi | hi | lo] along channels;
+// pattern 2: C' = 2C interleaved pairs, per 32 channels [hi 32 | lo 32]).
 __global__ void k_pack_conv_weight_x3(const float* __restrict__ w, bf16_t* __restrict__ out, int K,
-                                      int C, int R, int S) {
+                                      int C, int R, int S, int pattern) {
   const int64_t n = (int64_t)K * R * S * C;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -105,10 +114,16 @@ __global__ void k_pack_conv_weight_x3(const float* __restrict__ w, bf16_t* __res
     const float v = w[(((int64_t)k * C + c) * R + r) * S + s];
     const bf16_t h = f2bf(v);
     const bf16_t l = f2bf(v - bf2f(h));
-    bf16_t* o = out + t * 3 * C + c;
-    o[0] = h;
-    o[C] = h;
-    o[2 * C] = l;
+    if (pattern == 2) {
+      bf16_t* o = out + t * 2 * C + 2 * (c & ~31) + (c & 31);
+      o[0] = h;
+      o[32] = l;
+    } else {
+      bf16_t* o = out + t * 3 * C + c;
+      o[0] = h;
+      o[C] = h;
+      o[2 * C] = l;
+    }
   }
 }
 
@@ -142,15 +157,26 @@ __global__ void k_bn_apply_x3(const void* __restrict__ y, const bf16_t* __restri
                               const bf16_t* __restrict__ res_lo, int res_mode, int relu,
                               bf16_t* __restrict__ out_lo, bf16_t* __restrict__ out_bf,
                               float* __restrict__ out_f32, bf16_t* __restrict__ y_bf,
-                              uint8_t* __restrict__ relu_mask, int64_t M, int C) {
-  const int cv = C / 8;
+                              uint8_t* __restrict__ relu_mask, int64_t M, int C, int cv_log2) {
+  const int cv = C / 8;  // a power of two (every ResNet-50 width; host-checked): shifts, no division
   const int64_t n = M * cv;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / cv;
-    const int c = (int)(i - m * cv) * 8;
+    const int64_t m = i >> cv_log2;
+    const int c = (int)(i & (cv - 1)) * 8;
     const int64_t e = m * C + c;
-    float f[8], r[8];
+    float f[8], r[8], sc[8], sh[8];
+    {
+      const f32x4 s0 = *(const f32x4*)(scale + c), s1 = *(const f32x4*)(scale + c + 4);
+      const f32x4 h0 = *(const f32x4*)(shift + c), h1 = *(const f32x4*)(shift + c + 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sc[k] = s0[k];
+        sc[k + 4] = s1[k];
+        sh[k] = h0[k];
+        sh[k + 4] = h1[k];
+      }
+    }
     if (y_lo) {
       ld8_pair((const bf16_t*)y, y_lo, e, f);
     } else {
@@ -161,7 +187,7 @@ __global__ void k_bn_apply_x3(const void* __restrict__ y, const bf16_t* __restri
     else if (res_mode == 2) ld8_pair((const bf16_t*)res, res_lo, e, r);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float v = fmaf(f[k], scale[c + k], shift[c + k]);
+      float v = fmaf(f[k], sc[k], sh[k]);
       if (res_mode) v += r[k];
       f[k] = relu ? fmaxf(v, 0.f) : v;
     }
@@ -383,9 +409,10 @@ extern "C" int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_
                             int32_t seg, void* out, int32_t pattern, void* hi_out, int64_t ld_hi,
                             void* stream) {
   DFU_CHECK_ARG(in && out && rows >= 0 && cols > 0 && seg % 8 == 0 && seg >= cols &&
-                    ld_in >= cols && (pattern == 0 || pattern == 1) &&
+                    ld_in >= cols && (pattern >= 0 && pattern <= 2) &&
+                    (pattern != 2 || seg % 32 == 0) &&
                     (!hi_out || (ld_hi % 8 == 0 && ld_hi >= seg)),
-                "dfu_split_x3: bad args (seg %% 8 == 0, seg >= cols, pattern 0/1)");
+                "dfu_split_x3: bad args (seg %% 8 == 0, seg >= cols, pattern 0/1/2; 2: seg %% 32 == 0)");
   const int64_t n = (int64_t)rows * (seg / 8);
   if (n == 0) return DFU_OK;
   hipLaunchKernelGGL(k_split_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, in, ld_in,
@@ -395,11 +422,13 @@ extern "C" int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_
 }
 
 extern "C" int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int32_t C, int32_t R,
-                                       int32_t S, void* stream) {
-  DFU_CHECK_ARG(w && out && K > 0 && C > 0 && R > 0 && S > 0, "dfu_pack_conv_weight_x3: bad args");
+                                       int32_t S, int32_t pattern, void* stream) {
+  DFU_CHECK_ARG(w && out && K > 0 && C > 0 && R > 0 && S > 0 &&
+                    (pattern == 1 || (pattern == 2 && C % 32 == 0)),
+                "dfu_pack_conv_weight_x3: bad args (pattern 1, or 2 with C %% 32 == 0)");
   const int64_t n = (int64_t)K * R * S * C;
   hipLaunchKernelGGL(k_pack_conv_weight_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream,
-                     w, (bf16_t*)out, K, C, R, S);
+                     w, (bf16_t*)out, K, C, R, S, pattern);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }
@@ -421,6 +450,13 @@ extern "C" int dfu_bn_apply_x3(const void* y, const void* y_lo, const float* sca
                                int32_t relu, void* out_lo, void* out_bf16, float* out_f32,
                                void* y_bf16, uint8_t* relu_mask, int64_t M, int32_t C,
                                void* stream) {
+  const int cv = C / 8;
+  int cv_log2 = 0;
+  while ((1 << cv_log2) < cv) ++cv_log2;
+  DFU_CHECK_ARG(C % 8 == 0 && cv > 0 && (1 << cv_log2) == cv,
+                "dfu_bn_apply_x3: C / 8 must be a power of two (C=%d)", C);
+  DFU_CHECK_ARG((((uintptr_t)scale | (uintptr_t)shift) & 15) == 0,
+                "dfu_bn_apply_x3: scale/shift must be 16-byte aligned");
   DFU_CHECK_ARG(y && scale && shift && C % 8 == 0 && M >= 0 && res_mode >= 0 && res_mode <= 2 &&
                     (res_mode == 0 || residual) && (res_mode != 2 || residual_lo) &&
                     (!out_lo || out_bf16),
@@ -430,7 +466,7 @@ extern "C" int dfu_bn_apply_x3(const void* y, const void* y_lo, const float* sca
   hipLaunchKernelGGL(k_bn_apply_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, y,
                      (const bf16_t*)y_lo, scale, shift, residual, (const bf16_t*)residual_lo,
                      res_mode, relu, (bf16_t*)out_lo,
-                     (bf16_t*)out_bf16, out_f32, (bf16_t*)y_bf16, relu_mask, M, C);
+                     (bf16_t*)out_bf16, out_f32, (bf16_t*)y_bf16, relu_mask, M, C, cv_log2);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

@@ -56,6 +56,7 @@ class GemmDesc(ctypes.Structure):
         ("tile_counters", c_void_p), ("tile_counters_len", c_int32),
         ("operand_type", c_int32),
         ("a_seg", c_int32), ("a_lo", c_void_p),
+        ("x3_pairs", c_int32),
     ]
 
 
@@ -148,7 +149,7 @@ PROTOTYPES = {
     "dfu_softmax_rows": [P, I32, I32, P, P],
     "dfu_metrics_accumulate": [P, P, I32, I32, P, P, P, P, P],
     "dfu_split_x3": [P, I64, I32, I32, I32, P, I32, P, I64, P],
-    "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, P],
+    "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, I32, P],
     "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P],
     "dfu_patchify_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
     "dfu_stats_pair_f32": [P, I64, I32, P, P, P, P],

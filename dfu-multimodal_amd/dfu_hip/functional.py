@@ -471,8 +471,19 @@ def weight_x3_rows(w, seg=None):
     return ops.split_x3(w.detach().reshape(w.shape[0], -1), ops.X3_B, seg=seg)
 
 
+# The bf16x3 ResNet forward's GEMMs on interleaved pairs (dfu_gemm_desc.x3_pairs: K = 2C, the
+# three products per K-step from 2 operand tiles) instead of the tripled K; DFU_X3_PAIRS=0: the
+# tripled K (A/B timing).
+_X3_PAIRS = os.environ.get("DFU_X3_PAIRS", "1") != "0"
+
+
 def conv_weight_x3(w):
-    """fp32 OIHW conv weight -> bf16x3 KRSC' operand (C' = 3C; 1x1: the row split)."""
+    """fp32 OIHW conv weight -> bf16x3 KRSC' operand: C' = 2C interleaved pairs (_X3_PAIRS) or
+    C' = 3C [hi | hi | lo]; 1x1: the row split."""
+    if _X3_PAIRS:
+        if w.shape[2] == 1 and w.shape[3] == 1:
+            return ops.split_x3(w.detach().reshape(w.shape[0], -1), ops.X3_PAIRS)
+        return ops.pack_conv_weight_x3(w.detach(), ops.X3_PAIRS)
     if w.shape[2] == 1 and w.shape[3] == 1:
         return weight_x3_rows(w)
     return ops.pack_conv_weight_x3(w.detach())
@@ -560,37 +571,37 @@ def _x3_split(M, N, K3):
 
 def conv_fwd_x3(x_pair, geom, w3, y, stats, y_lo=None):
     """bf16x3: y[M, K] = conv(x) over the split pair x = (hi, lo) [N*H*W, C] (the GEMM reads
-    the channel-tripled hi | lo | hi) and KRSC' weights, fp32 -- or with y_lo, the split pair
-    (y = bf16 hi, y_lo = lo) of the fp32 result; BN tile statistics of the unrounded outputs
-    into stats."""
+    interleaved pairs, or the channel-tripled hi | lo | hi) and KRSC' weights (conv_weight_x3),
+    fp32 -- or with y_lo, the split pair (y = bf16 hi, y_lo = lo) of the fp32 result; BN tile
+    statistics of the unrounded outputs into stats."""
     g = geom
     hi, lo = x_pair
     M = g.n * g.p * g.q
-    C3 = 3 * g.c
+    pairs = _X3_PAIRS
+    C3 = (2 if pairs else 3) * g.c
     K3 = g.r * g.s * C3
-    if y_lo is not None and _x3_split(M, g.k, K3):
+    xk = dict(x3=True, a_lo=lo, x3_pairs=pairs)
+    if y_lo is not None and _x3_split(M, g.k, g.r * g.s * 3 * g.c):
         # few 128x128 tiles over a long tripled K (layers 3-4): split-K into fp32 slabs, then
         # the statistics and the pair from the reduced output
         acc = _empty((M, g.k), F32, y.device)
         ops.zero_(acc)
         if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
-            ops.gemm(M, g.k, C3, hi, g.c, w3, C3, acc, g.k, epilogue=L.EPI_F32_ACC, x3=True,
-                     a_lo=lo)
+            ops.gemm(M, g.k, C3, hi, g.c, w3, C3, acc, g.k, epilogue=L.EPI_F32_ACC, **xk)
         else:
             g3 = ops.ConvGeom(g.n, g.h, g.w, C3, g.k, g.r, g.s, g.stride, g.pad)
             ops.gemm(M, g.k, K3, hi, 0, w3, K3, acc, g.k, a_mode=L.OPND_CONV_FWD,
-                     epilogue=L.EPI_F32_ACC, conv=g3, x3=True, a_lo=lo)
+                     epilogue=L.EPI_F32_ACC, conv=g3, **xk)
         ops.stats_pair_f32(acc, M, g.k, stats, y, y_lo)
         return
     out = dict(aux_out=y_lo, ldaux_out=g.k if y_lo is not None else 0)
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
         ops.gemm(M, g.k, C3, hi, g.c, w3, C3, y, g.k, epilogue=L.EPI_F32_STATS, stats=stats,
-                 x3=True, a_lo=lo, **out)
+                 **xk, **out)
     else:
         g3 = ops.ConvGeom(g.n, g.h, g.w, C3, g.k, g.r, g.s, g.stride, g.pad)
-        K = g.r * g.s * C3
-        ops.gemm(M, g.k, K, hi, 0, w3, K, y, g.k, a_mode=L.OPND_CONV_FWD,
-                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3, x3=True, a_lo=lo, **out)
+        ops.gemm(M, g.k, K3, hi, 0, w3, K3, y, g.k, a_mode=L.OPND_CONV_FWD,
+                 epilogue=L.EPI_F32_STATS, stats=stats, conv=g3, **xk, **out)
 
 
 def conv_dgrad(dy_rows, geom, w_krsc, dx, add=None, w_flip=None, w_t=None):
@@ -680,8 +691,13 @@ class StemFn(torch.autograd.Function):
         if x3:
             a = _empty((M * Cout // 8,), torch.uint8, x.device)  # bn1's ReLU bitmask
             y_lo = _empty((M, Cout), BF16, x.device)  # the conv output as a split pair (y, y_lo)
-            ops.gemm(M, Cout, 3 * Kp, col, Kp, weight_x3_rows(w, seg=Kp), 3 * Kp, y, Cout,
-                     epilogue=L.EPI_F32_STATS, stats=stats, x3=True, a_lo=col_lo, aux_out=y_lo,
+            if _X3_PAIRS and Kp % 32 == 0:  # interleaved pairs (conv_weight_x3)
+                w3, K3, pairs = ops.split_x3(w.detach().reshape(Cout, -1), ops.X3_PAIRS,
+                                             seg=Kp), 2 * Kp, True
+            else:
+                w3, K3, pairs = weight_x3_rows(w, seg=Kp), 3 * Kp, False
+            ops.gemm(M, Cout, K3, col, Kp, w3, K3, y, Cout, epilogue=L.EPI_F32_STATS,
+                     stats=stats, x3=True, a_lo=col_lo, x3_pairs=pairs, aux_out=y_lo,
                      ldaux_out=Cout)
             del col_lo
             bns.forward_coeffs(stats)

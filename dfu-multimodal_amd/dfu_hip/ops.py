@@ -77,7 +77,7 @@ def _algorithmic_bytes(d, conv):
     a = {L.OPND_CONV_FWD: act_in,
          L.OPND_CONV_DGRAD: 2 * conv.n * conv.p * conv.q * conv.k if conv is not None else 0
          }.get(d.a_mode, 2 * M * K)
-    if d.a_seg:  # split pair: hi and lo read once each (the tripled K reads hi twice)
+    if d.a_seg and not d.x3_pairs:  # split pair: hi and lo once each (the tripled K reads hi twice)
         a = a * 2 // 3
     b = act_in if d.b_mode == L.OPND_CONV_WGRAD_X else 2 * N * K
     e = d.epilogue
@@ -100,11 +100,13 @@ def gemm_replay(records, stream=None):
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
          epilogue=L.EPI_BF16, alpha=1.0, bias=None, aux=None, ldaux=0, aux_out=None,
          ldaux_out=0, stats=None, split_k=0, ep_tokens=0, conv=None, tile=0, workspace=None,
-         operand_type=0, x3=False, a_lo=None):
+         operand_type=0, x3=False, a_lo=None, x3_pairs=False):
     """C = epilogue(A @ B^T).  `split_k` (F32_ACC only): 0 = library cost model, 1 = none.
     `x3`: a bf16x3 product (K tripled): the recorded algorithmic FLOPs count K / 3.
     `a_lo`: split-pair A -- A is the hi buffer and a_lo the lo buffer ([rows][K / 3] each; the
     conv forward: NHWC with conv.c / 3 channels), read as the K-segments hi | lo | hi.
+    `x3_pairs` (with a_lo): interleaved pairs instead -- K (conv.c) = 2 x the pair's width, B
+    in pattern X3_PAIRS, the kernel forms the three products per K-step.
     `tile`: 0 = library cost model, else a TILES id.  Split-K partials go to fp32 slabs in
     `workspace` (allocated here from the stream-ordered caching allocator when None) and are
     reduced deterministically by a second kernel."""
@@ -126,8 +128,10 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
     d.stats = stats.data_ptr() if stats is not None else None
     d.operand_type = int(operand_type)
     if a_lo is not None:
-        d.a_seg = int(conv.c // 3 if a_mode == L.OPND_CONV_FWD else K // 3)
+        nseg = 2 if x3_pairs else 3
+        d.a_seg = int(conv.c // nseg if a_mode == L.OPND_CONV_FWD else K // nseg)
         d.a_lo = a_lo.data_ptr()
+        d.x3_pairs = int(bool(x3_pairs))
     d.split_k = int(split_k)
     d.ep_tokens = int(ep_tokens)
     d.tile = int(tile)
@@ -145,7 +149,8 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
         d.tile_counters, d.tile_counters_len = cnt.data_ptr(), cnt.numel()
     check(lib().dfu_gemm(ctypes.byref(d), stream_ptr()), "dfu_gemm")
     if gemm_record is not None:
-        flops = 2.0 * M * N * (K // 3 if x3 else K)  # algorithmic (x3: the product, not its 3 passes)
+        # algorithmic (x3: the product, not its 3 passes)
+        flops = 2.0 * M * N * (K // (2 if x3_pairs else 3) if x3 else K)
         if a_mode == L.OPND_CONV_DGRAD and conv is not None:
             flops /= conv.stride * conv.stride  # algorithmic: only the 1/stride^2 live taps
         gemm_record.append((d, flops, _algorithmic_bytes(d, conv),
@@ -755,6 +760,7 @@ def softmax_rows(x):
 # csrc/precise.hip: a triple is bf16 [rows][3C] = [hi | lo | hi] (pattern 0, GEMM A operand)
 # or [hi | hi | lo] (pattern 1, GEMM B operand / weights), hi = bf16(x), lo = bf16(x - hi).
 X3_A, X3_B = 0, 1
+X3_PAIRS = 2  # B operand of dfu_gemm_desc.x3_pairs: [rows][2 seg], per 32 columns [hi | lo]
 
 
 def split_x3(x, pattern, seg=None, hi_out=None):
@@ -765,21 +771,25 @@ def split_x3(x, pattern, seg=None, hi_out=None):
     if x2.stride(1) != 1:
         x2 = x2.contiguous()
     rows, cols = x2.shape
-    seg = (cols + 7) // 8 * 8 if seg is None else int(seg)
-    out = torch.empty((rows, 3 * seg), dtype=BF16, device=x.device)
+    if seg is None:
+        seg = (cols + 31) // 32 * 32 if pattern == X3_PAIRS else (cols + 7) // 8 * 8
+    seg = int(seg)
+    out = torch.empty((rows, (2 if pattern == X3_PAIRS else 3) * seg), dtype=BF16,
+                      device=x.device)
     check(lib().dfu_split_x3(ptr(x2), x2.stride(0), rows, cols, seg, ptr(out), int(pattern),
                              ptr(hi_out), seg if hi_out is None else hi_out.stride(0),
                              stream_ptr()), "dfu_split_x3")
     return out
 
 
-def pack_conv_weight_x3(w):
-    """fp32 OIHW -> bf16 KRSC' (C' = 3C, pattern 1)."""
+def pack_conv_weight_x3(w, pattern=X3_B):
+    """fp32 OIHW -> bf16 KRSC' (X3_B: C' = 3C [hi | hi | lo]; X3_PAIRS: C' = 2C interleaved)."""
     _req(w, F32, "pack_conv_weight_x3")
     K, C, R, S = w.shape
-    out = torch.empty((K, R, S, 3 * C), dtype=BF16, device=w.device)
-    check(lib().dfu_pack_conv_weight_x3(ptr(w.contiguous()), ptr(out), K, C, R, S, stream_ptr()),
-          "dfu_pack_conv_weight_x3")
+    nseg = 2 if pattern == X3_PAIRS else 3
+    out = torch.empty((K, R, S, nseg * C), dtype=BF16, device=w.device)
+    check(lib().dfu_pack_conv_weight_x3(ptr(w.contiguous()), ptr(out), K, C, R, S, int(pattern),
+                                        stream_ptr()), "dfu_pack_conv_weight_x3")
     return out
 
 

@@ -144,6 +144,12 @@ typedef struct dfu_gemm_desc {
    * == 0); not on the phased 256x256 tiles (7-9). */
   int32_t a_seg;
   const void* a_lo;
+  /* 1 = interleaved pairs (with a_seg, a_seg % 32 == 0): K (conv: conv_c) = 2 a_seg, and each
+   * 64-wide K-step is [hi | lo] of 32 real k -- A read so from the split pair, B stored so
+   * (dfu_split_x3 / dfu_pack_conv_weight_x3 pattern 2); the kernel forms hi·hi + lo·hi + hi·lo
+   * per step, the tripled-K sum from 2 operand tiles instead of 3.  Tiles 1, 2, 5, 10, 11
+   * (F32_STATS; F32_ACC on 1 and 5). */
+  int32_t x3_pairs;
 } dfu_gemm_desc;
 
 int dfu_gemm(const dfu_gemm_desc* desc, void* stream);
@@ -456,12 +462,15 @@ int dfu_metrics_accumulate(const float* logits, const int64_t* labels, int32_t r
  * (DFU_EPI_F32 / F32_RESID / F32_STATS / PATCH); the kernels below also write the plain bf16
  * tensors the (bf16) backward pass saves.  Reference ops: the same as their bf16 twins above. */
 /* fp32 [rows][cols] (ld_in) -> triple [rows][3 seg] of `pattern`, seg >= cols (seg % 8 == 0,
- * columns past cols zero); optional plain bf16 copy hi_out [rows][ld_hi >= seg]. */
+ * columns past cols zero); optional plain bf16 copy hi_out [rows][ld_hi >= seg].  Pattern 2:
+ * interleaved pairs [rows][2 seg] (seg % 32 == 0), per 32 columns [hi 32 | lo 32] (the B
+ * operand of dfu_gemm_desc.x3_pairs). */
 int dfu_split_x3(const float* in, int64_t ld_in, int32_t rows, int32_t cols, int32_t seg,
                  void* out, int32_t pattern, void* hi_out, int64_t ld_hi, void* stream);
-/* fp32 OIHW conv weight -> bf16 KRSC' with C' = 3C, pattern 1 along the channels. */
+/* fp32 OIHW conv weight -> bf16 KRSC': pattern 1, C' = 3C along the channels; pattern 2,
+ * C' = 2C interleaved pairs (C % 32 == 0; dfu_gemm_desc.x3_pairs). */
 int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int32_t C, int32_t R, int32_t S,
-                            void* stream);
+                            int32_t pattern, void* stream);
 /* dfu_im2col_f32 writing the split pair: hi rows to out, lo rows to out_lo (row stride Kp each:
  * the stem GEMM's split-pair A, dfu_gemm_desc.a_seg = Kp); dfu_patchify_f32_x3 writes the
  * pattern-0 triple (row stride 3 K). */

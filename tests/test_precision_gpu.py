@@ -59,6 +59,96 @@ def test_pack_conv_weight_x3():
     assert ((p[..., :32] + p[..., 64:] - krsc).abs() <= krsc.abs() * 2.0 ** -16).all()
 
 
+def test_interleaved_pair_layouts():
+    """Pattern X3_PAIRS (dfu_gemm_desc.x3_pairs' B operand): per 32 columns [hi 32 | lo 32],
+    zero-padded to the segment; the conv weight packing the same along each tap's channels."""
+    L, ops = _ops()
+    torch.manual_seed(12)
+    x = torch.randn(37, 147, device=DEV) * 3.0
+    p = ops.split_x3(x, ops.X3_PAIRS, seg=160).float()
+    assert p.shape == (37, 320)
+    g = p.view(37, 5, 2, 32)
+    hi, lo = g[:, :, 0].reshape(37, 160), g[:, :, 1].reshape(37, 160)
+    assert torch.equal(hi[:, :147], x.to(torch.bfloat16).float()) and torch.all(hi[:, 147:] == 0)
+    assert torch.equal(lo[:, :147], (x - hi[:, :147]).to(torch.bfloat16).float())
+    assert torch.all(lo[:, 147:] == 0)
+    assert ops.split_x3(x[:, :64], ops.X3_PAIRS).shape == (37, 128)
+    with pytest.raises(L.DfuError):  # pattern 2 needs whole 32-column groups
+        ops.split_x3(x, ops.X3_PAIRS, seg=152)
+    w = torch.randn(64, 96, 3, 3, device=DEV)
+    q = ops.pack_conv_weight_x3(w, ops.X3_PAIRS).float().view(64, 3, 3, 3, 2, 32)
+    krsc = w.permute(0, 2, 3, 1)
+    assert torch.equal(q[..., 0, :].reshape(64, 3, 3, 96), krsc.to(torch.bfloat16).float())
+    kh = krsc.to(torch.bfloat16).float()
+    assert torch.equal(q[..., 1, :].reshape(64, 3, 3, 96), (krsc - kh).to(torch.bfloat16).float())
+    with pytest.raises(L.DfuError):
+        ops.pack_conv_weight_x3(torch.randn(8, 48, 3, 3, device=DEV), ops.X3_PAIRS)
+
+
+@pytest.mark.parametrize("conv,C", [(False, 160), (True, 128), (True, 96)])
+def test_x3_pairs_gemm_every_tile(conv, C):
+    """The interleaved-pair bf16x3 kernels (three products per K-step from a hi and a lo tile)
+    on every tile that instantiates them -- F32_STATS with the pair output on tiles 1, 2, 10,
+    11, F32_ACC split-K on 1 and 5 -- K-major and implicit-conv A, ragged M: fp32-accurate
+    against fp64, and within fp32 summation order of the tripled-K kernels (which need the
+    conv's C % 64 == 0: C = 96 runs the pair kernels only)."""
+    L, ops = _ops()
+    torch.manual_seed(13)
+    if conv:
+        Bn, H, Kout, R, st_ = 5, 13, 192, 3, 2
+        g = ops.ConvGeom(Bn, H, H, C, Kout, R, R, st_, 1)
+        M = Bn * g.p * g.q
+        x = torch.randn(Bn, C, H, H, device=DEV)
+        w = torch.randn(Kout, C, R, R, device=DEV) / math.sqrt(C * R * R)
+        rows = x.permute(0, 2, 3, 1).reshape(-1, C).contiguous()
+        ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=st_, padding=1)
+        ref = ref.permute(0, 2, 3, 1).reshape(-1, Kout)
+        w2, w3 = ops.pack_conv_weight_x3(w, ops.X3_PAIRS), ops.pack_conv_weight_x3(w)
+        K2, K3 = R * R * 2 * C, R * R * 3 * C
+        kw2 = dict(a_mode=L.OPND_CONV_FWD, conv=ops.ConvGeom(Bn, H, H, 2 * C, Kout, R, R, st_, 1))
+        kw3 = dict(a_mode=L.OPND_CONV_FWD, conv=ops.ConvGeom(Bn, H, H, 3 * C, Kout, R, R, st_, 1))
+        lda = 0
+    else:
+        M, Kout = 1001, 192
+        rows = torch.randn(M, C, device=DEV)
+        w = torch.randn(Kout, C, device=DEV) / math.sqrt(C)
+        ref = rows.double() @ w.double().T
+        w2, w3 = ops.split_x3(w, ops.X3_PAIRS), ops.split_x3(w, ops.X3_B)
+        K2, K3, kw2, kw3, lda = 2 * C, 3 * C, {}, {}, C
+    hi, lo = _pair(rows)
+    st3 = torch.empty(ops.stats_tiles(M), 2, Kout, device=DEV)
+    y3 = None
+    if not conv or C % 64 == 0:
+        y3 = torch.empty(M, Kout, device=DEV)
+        ops.gemm(M, Kout, K3, hi, lda, w3, K3, y3, Kout, epilogue=L.EPI_F32_STATS, stats=st3,
+                 x3=True, a_lo=lo, tile=1, **kw3)
+    for tile in (1, 2, 10, 11):
+        y = torch.full((M, Kout), float("nan"), device=DEV)
+        st = torch.empty_like(st3)
+        ops.gemm(M, Kout, K2, hi, lda, w2, K2, y, Kout, epilogue=L.EPI_F32_STATS, stats=st,
+                 x3=True, a_lo=lo, x3_pairs=True, tile=tile, **kw2)
+        assert ((y.double() - ref).norm() / ref.norm()).item() < 2e-5, tile
+        if y3 is None:
+            y3, st3 = y.clone(), st.clone()  # C = 96: the tiles against each other
+        assert ((y - y3).norm() / y3.norm()).item() < 2e-6, tile
+        assert ((st - st3).norm() / st3.norm()).item() < 1e-5, tile
+        # the pair output (aux_out): hi = bf16(y), lo = bf16(y - hi)
+        yh = torch.empty(M, Kout, dtype=torch.bfloat16, device=DEV)
+        yl = torch.empty_like(yh)
+        ops.gemm(M, Kout, K2, hi, lda, w2, K2, yh, Kout, epilogue=L.EPI_F32_STATS, stats=st,
+                 x3=True, a_lo=lo, x3_pairs=True, tile=tile, aux_out=yl, ldaux_out=Kout, **kw2)
+        assert torch.equal(yh, y.to(torch.bfloat16)), tile
+        assert torch.equal(yl, (y - yh.float()).to(torch.bfloat16)), tile
+    for tile, split in ((1, 1), (1, 4), (5, 3)):
+        acc = torch.zeros(M, Kout, device=DEV)
+        ops.gemm(M, Kout, K2, hi, lda, w2, K2, acc, Kout, epilogue=L.EPI_F32_ACC, x3=True,
+                 a_lo=lo, x3_pairs=True, tile=tile, split_k=split, **kw2)
+        assert ((acc - y3).norm() / y3.norm()).item() < 2e-6, (tile, split)
+    with pytest.raises(L.DfuError):  # no interleaved-pair kernel on the persistent tiles
+        ops.gemm(M, Kout, K2, hi, lda, w2, K2, y3, Kout, epilogue=L.EPI_F32_STATS, stats=st3,
+                 x3=True, a_lo=lo, x3_pairs=True, tile=8, **kw2)
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 768, 768), (1000, 384, 3072), (333, 200, 160)])
 def test_gemm_over_triples_is_fp32_accurate(M, N, K):
     """A3 . B3^T on the bf16 MFMA GEMM equals fp32 A . B^T to ~1e-5 relative (bf16: ~4e-3)."""
@@ -135,8 +225,9 @@ def test_f32_stats_epilogue(tile):
 
 @pytest.mark.parametrize("R,stride", [(3, 1), (3, 2), (1, 1), (1, 2)])
 def test_conv_fwd_x3_matches_fp32_conv(R, stride):
-    """Conv forward over a split pair (the GEMM reads hi | lo | hi from two buffers: K-major
-    for the 1x1 stride-1 case, the implicit-GEMM loader otherwise) against fp64 conv2d, and
+    """Conv forward over a split pair against fp64 conv2d: the interleaved-pair kernels (the
+    default) within fp32 summation order of the tripled-K ones (hi | lo | hi read from two
+    buffers: K-major for the 1x1 stride-1 case, the implicit-GEMM loader otherwise), which are
     bit-identical to the same GEMM over the materialised triple."""
     from dfu_hip import functional as Fn
     L, ops = _ops()
@@ -147,26 +238,35 @@ def test_conv_fwd_x3_matches_fp32_conv(R, stride):
     pad = R // 2
     g = ops.ConvGeom(Bn, H, W, C, Kout, R, R, stride, pad)
     rows = x.permute(0, 2, 3, 1).reshape(-1, C).contiguous()
-    y = torch.empty(Bn * g.p * g.q, Kout, device=DEV)
-    st = torch.empty(ops.stats_tiles(y.shape[0]), 2, Kout, device=DEV)
-    w3 = Fn.conv_weight_x3(w)
-    Fn.conv_fwd_x3(_pair(rows), g, w3, y, st)
+    M = Bn * g.p * g.q
     ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=stride, padding=pad)
     ref = ref.permute(0, 2, 3, 1).reshape(-1, Kout)
-    err = ((y.double() - ref).norm() / ref.norm()).item()
-    assert err < 2e-5, (R, stride, err)
-    # the same conv writing its output as a split pair (F32_STATS with aux_out): hi = bf16(y),
-    # lo = bf16(y - hi) of the very fp32 values above, and the same statistics
-    yh = torch.empty(y.shape, dtype=torch.bfloat16, device=DEV)
-    yl = torch.empty_like(yh)
-    st2 = torch.empty_like(st)
-    Fn.conv_fwd_x3(_pair(rows), g, w3, yh, st2, y_lo=yl)
-    assert torch.equal(yh, y.to(torch.bfloat16)) and torch.equal(st2, st)
-    assert torch.equal(yl, (y - yh.float()).to(torch.bfloat16))
-    # the same contraction over the materialised triple [hi | lo | hi]
+    old = Fn._X3_PAIRS
+    ys = []
+    try:
+        for pairs in (True, False):
+            Fn._X3_PAIRS = pairs
+            w3 = Fn.conv_weight_x3(w)
+            y = torch.empty(M, Kout, device=DEV)
+            st = torch.empty(ops.stats_tiles(M), 2, Kout, device=DEV)
+            Fn.conv_fwd_x3(_pair(rows), g, w3, y, st)
+            err = ((y.double() - ref).norm() / ref.norm()).item()
+            assert err < 2e-5, (R, stride, pairs, err)
+            # the same conv writing its output as a split pair (F32_STATS with aux_out): hi =
+            # bf16(y), lo = bf16(y - hi) of the very fp32 values above, the same statistics
+            yh = torch.empty(y.shape, dtype=torch.bfloat16, device=DEV)
+            yl = torch.empty_like(yh)
+            st2 = torch.empty_like(st)
+            Fn.conv_fwd_x3(_pair(rows), g, w3, yh, st2, y_lo=yl)
+            assert torch.equal(yh, y.to(torch.bfloat16)) and torch.equal(st2, st)
+            assert torch.equal(yl, (y - yh.float()).to(torch.bfloat16))
+            ys.append(y)
+    finally:
+        Fn._X3_PAIRS = old
+    assert ((ys[0] - ys[1]).norm() / ys[1].norm()).item() < 2e-6
+    # the tripled-K contraction over the materialised triple [hi | lo | hi]: bit-identical
     x3 = ops.split_x3(rows, ops.X3_A)
     y3 = torch.empty_like(y)
-    M = y.shape[0]
     if R == 1 and stride == 1:
         ops.gemm(M, Kout, 3 * C, x3, 3 * C, w3, 3 * C, y3, Kout, epilogue=L.EPI_F32_STATS,
                  stats=st, x3=True)
@@ -174,7 +274,7 @@ def test_conv_fwd_x3_matches_fp32_conv(R, stride):
         g3 = ops.ConvGeom(Bn, H, W, 3 * C, Kout, R, R, stride, pad)
         ops.gemm(M, Kout, R * R * 3 * C, x3, 0, w3, R * R * 3 * C, y3, Kout,
                  a_mode=L.OPND_CONV_FWD, epilogue=L.EPI_F32_STATS, stats=st, conv=g3, x3=True)
-    assert torch.equal(y, y3)
+    assert torch.equal(ys[1], y3)
 
 
 @pytest.mark.parametrize("R,stride,C,H", [(3, 1, 512, 7), (3, 2, 256, 28), (1, 1, 2048, 7)])

@@ -31,7 +31,8 @@ CONV_FIELDS = ("conv_n", "conv_h", "conv_w", "conv_c", "conv_k", "conv_r", "conv
 
 def key(d):
     conv = d.a_mode >= L.OPND_CONV_FWD or d.b_mode >= L.OPND_CONV_FWD
-    return (d.a_mode, d.b_mode, d.epilogue, d.M, d.N, d.K) + (
+    # the table's epilogue field is the dispatch key (| 128: interleaved bf16x3 pairs)
+    return (d.a_mode, d.b_mode, d.epilogue | (128 if d.x3_pairs else 0), d.M, d.N, d.K) + (
         tuple(getattr(d, f) for f in CONV_FIELDS) if conv else (0,) * 9)
 
 
@@ -73,6 +74,8 @@ def main():
     ap.add_argument("--tiles", default="1-11", help="tile ids to try, e.g. 1-11 or 6,8")
     ap.add_argument("--precision", default="bf16", help="record the step in this mode (bf16x3: "
                     "its forward GEMMs with tripled K)")
+    ap.add_argument("--only-x3-pairs", action="store_true",
+                    help="tune only the interleaved-pair bf16x3 GEMMs (dfu_gemm_desc.x3_pairs)")
     ap.add_argument("--dump", default=None,
                     help="also write every timing (shape -> {tile/split: us}) to this JSON")
     a = ap.parse_args()
@@ -98,6 +101,8 @@ def main():
     torch.cuda.synchronize()
     uniq = {}
     for d, flops, _, refs in rec:
+        if a.only_x3_pairs and not d.x3_pairs:
+            continue
         uniq.setdefault(key(d), (d, flops, refs, []))[3].append(1)
     print(f"{len(rec)} launches, {len(uniq)} distinct GEMMs", flush=True)
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
@@ -125,7 +130,7 @@ def main():
                     best = (t, tile, sk)
         t_auto_sum += n * t_auto
         t_best_sum += n * min(best[0], t_auto)
-        name = (f"{OPND[d0.a_mode]}x{OPND[d0.b_mode]}->{EPI[d0.epilogue]} "
+        name = (f"{OPND[d0.a_mode]}x{OPND[d0.b_mode]}->{EPI[d0.epilogue]}{'/P' if d0.x3_pairs else ''} "
                 f"{d0.M}x{d0.N}x{d0.K} (x{n}/step)")
         print(f"{name:62s} auto {t_auto:8.1f} us  best {best[0]:8.1f} us tile {best[1]} "
               f"split {best[2]}  {flops / best[0] / 1e6:6.0f} TFLOP/s", flush=True)
