@@ -83,9 +83,10 @@ inline int epi_key(const dfu_gemm_desc* d) {
   return d->epilogue | (d->operand_type == 1 ? kF16Key : 0) | (d->x3_pairs ? kX3Key : 0);
 }
 
-const TunedPlan* find_tuned(const dfu_gemm_desc* d) {
+// An fp16-operand descriptor takes its own entry (epilogue | kF16Key) if tuned, else the bf16
+// entry of the same shape.
+const TunedPlan* find_tuned_key(const dfu_gemm_desc* d, int epi) {
   const bool conv = d->a_mode >= DFU_OPND_CONV_FWD || d->b_mode >= DFU_OPND_CONV_FWD;
-  const int epi = d->epilogue | (d->x3_pairs ? kX3Key : 0);
   for (const TunedPlan& t : kTuned) {
     if (t.a != d->a_mode || t.b != d->b_mode || t.e != epi || t.M != d->M ||
         t.N != d->N || t.K != d->K)
@@ -97,6 +98,15 @@ const TunedPlan* find_tuned(const dfu_gemm_desc* d) {
     return &t;
   }
   return nullptr;
+}
+
+const TunedPlan* find_tuned(const dfu_gemm_desc* d) {
+  const int epi = d->epilogue | (d->x3_pairs ? kX3Key : 0);
+#ifndef DFU_NO_F16_TUNED  // (A/B builds only: the fp16 GEMMs on the bf16 shapes' plans)
+  if (d->operand_type == 1)
+    if (const TunedPlan* t = find_tuned_key(d, epi | kF16Key)) return t;
+#endif
+  return find_tuned_key(d, epi);
 }
 
 Plan plan_gemm(const dfu_gemm_desc* d) {

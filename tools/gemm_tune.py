@@ -31,8 +31,10 @@ CONV_FIELDS = ("conv_n", "conv_h", "conv_w", "conv_c", "conv_k", "conv_r", "conv
 
 def key(d):
     conv = d.a_mode >= L.OPND_CONV_FWD or d.b_mode >= L.OPND_CONV_FWD
-    # the table's epilogue field is the dispatch key (| 128: interleaved bf16x3 pairs)
-    return (d.a_mode, d.b_mode, d.epilogue | (128 if d.x3_pairs else 0), d.M, d.N, d.K) + (
+    # the table's epilogue field is the dispatch key (| 128: interleaved bf16x3 pairs, | 64: fp16
+    # operands -- whose lookup falls back to the bf16 entry of the same shape)
+    e = d.epilogue | (128 if d.x3_pairs else 0) | (64 if d.operand_type == 1 else 0)
+    return (d.a_mode, d.b_mode, e, d.M, d.N, d.K) + (
         tuple(getattr(d, f) for f in CONV_FIELDS) if conv else (0,) * 9)
 
 
@@ -76,6 +78,8 @@ def main():
                     "its forward GEMMs with tripled K)")
     ap.add_argument("--only-x3-pairs", action="store_true",
                     help="tune only the interleaved-pair bf16x3 GEMMs (dfu_gemm_desc.x3_pairs)")
+    ap.add_argument("--only-f16", action="store_true",
+                    help="tune only the fp16-operand GEMMs (dfu_gemm_desc.operand_type 1)")
     ap.add_argument("--dump", default=None,
                     help="also write every timing (shape -> {tile/split: us}) to this JSON")
     a = ap.parse_args()
@@ -102,6 +106,8 @@ def main():
     uniq = {}
     for d, flops, _, refs in rec:
         if a.only_x3_pairs and not d.x3_pairs:
+            continue
+        if a.only_f16 and d.operand_type != 1:
             continue
         uniq.setdefault(key(d), (d, flops, refs, []))[3].append(1)
     print(f"{len(rec)} launches, {len(uniq)} distinct GEMMs", flush=True)
@@ -130,7 +136,7 @@ def main():
                     best = (t, tile, sk)
         t_auto_sum += n * t_auto
         t_best_sum += n * min(best[0], t_auto)
-        name = (f"{OPND[d0.a_mode]}x{OPND[d0.b_mode]}->{EPI[d0.epilogue]}{'/P' if d0.x3_pairs else ''} "
+        name = (f"{OPND[d0.a_mode]}x{OPND[d0.b_mode]}->{EPI[d0.epilogue]}{'/P' if d0.x3_pairs else ''}{'/f16' if d0.operand_type == 1 else ''} "
                 f"{d0.M}x{d0.N}x{d0.K} (x{n}/step)")
         print(f"{name:62s} auto {t_auto:8.1f} us  best {best[0]:8.1f} us tile {best[1]} "
               f"split {best[2]}  {flops / best[0] / 1e6:6.0f} TFLOP/s", flush=True)
