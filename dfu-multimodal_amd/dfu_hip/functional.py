@@ -1099,6 +1099,8 @@ _X3_TILE = int(os.environ.get("DFU_X3_TILE", "8"))
 # for 256 CUs; 8-16 % faster standalone, tools/gpu_tile192.sh) when the ViT runs alone.  Inside
 # the two-stream fusion step the 256-row tile's idle CUs run the ResNet's kernels: there tile 9
 # measured 19.11 vs 18.97 ms per step (same box, three rounds), so it keeps the 256-row plan.
+# (The parity mode's fp16 proj / fc2 follow their own tuned entries, tile 9: 20.79-20.85 vs
+# 20.83-20.87 ms with the 256-row plan, same box.)
 # DFU_GEMM_NO_T192=1: the 256-row plan everywhere (A/B).
 _NO_T192 = os.environ.get("DFU_GEMM_NO_T192", "0") != "0"
 
