@@ -73,6 +73,27 @@ def test_gemm_validation_errors(kw, msg):
         L.check(rc, "dfu_gemm")
 
 
+def test_x3_pairs_validation_and_plan():
+    """Interleaved-pair bf16x3 descriptors (dfu_gemm_desc.x3_pairs): they need split-pair A with
+    K = 2 a_seg, a_seg % 32 == 0; the planner picks one of the tiles that instantiate them."""
+    lib = L.load()
+    base = dict(epilogue=L.EPI_F32_STATS, stats=1 << 20, x3_pairs=1)
+    d = _desc(**base)  # no a_seg
+    assert lib.dfu_gemm(ctypes.byref(d), None) == L.DFU_E_INVALID
+    assert "x3_pairs" in lib.dfu_last_error_string().decode()
+    d = _desc(a_seg=128, a_lo=(1 << 21), lda=128, **base)  # K = 256 = 2 a_seg: valid
+    t, sk = ctypes.c_int32(), ctypes.c_int32()
+    assert lib.dfu_gemm_plan(ctypes.byref(d), ctypes.byref(t), ctypes.byref(sk)) == 0
+    assert t.value in (1, 2, 10, 11)
+    d = _desc(a_seg=128, a_lo=(1 << 21), lda=128, K=384, **base)  # K = 3 a_seg: not pairs
+    assert lib.dfu_gemm(ctypes.byref(d), None) == L.DFU_E_INVALID
+    assert "split-pair A" in lib.dfu_last_error_string().decode()
+    d = _desc(a_seg=120, a_lo=(1 << 21), lda=120, K=240, **base)  # a_seg % 32 != 0
+    assert lib.dfu_gemm(ctypes.byref(d), None) == L.DFU_E_INVALID
+    d = _desc(a_seg=128, a_lo=(1 << 21), lda=128, tile=8, **base)  # no persistent-tile pairs
+    assert lib.dfu_gemm(ctypes.byref(d), None) == L.DFU_E_UNSUPPORTED
+
+
 def test_gemm_unsupported_combination():
     lib = L.load()
     d = _desc(epilogue=L.EPI_F32, tile=4)  # EPI_F32 is built for 128x128 only
