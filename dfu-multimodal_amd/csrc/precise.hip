@@ -203,55 +203,6 @@ __global__ void k_bn_apply_x3(const void* __restrict__ y, const bf16_t* __restri
   }
 }
 
-// ---------------------------------------------------------------- split-K conv output
-// The F32_STATS epilogue's two products for a conv output computed by a split-K GEMM (fp32 y
-// after the slab reduction): per 128-row tile and channel (sum, M2) over the rows -- two-pass,
-// as the epilogue -- and the split pair hi = bf16(y), lo = bf16(y - hi).  Block = 64 channels x
-// 4 row groups of 32 rows.
-__global__ __launch_bounds__(256) void k_stats_pair_f32(const float* __restrict__ y, int M, int C,
-                                                        float* __restrict__ stats,
-                                                        bf16_t* __restrict__ hi,
-                                                        bf16_t* __restrict__ lo) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.y * 64 + lane;
-  const int r0 = blockIdx.x * 128, nb = min(128, M - r0);
-  const int ra = r0 + g * 32, rb = min(r0 + nb, ra + 32);
-  float v[32];
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const int r = ra + i;
-    v[i] = (c < C && r < rb) ? y[(int64_t)r * C + c] : 0.f;
-  }
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 32; ++i) s += v[i];
-  red[g][lane] = s;
-  __syncthreads();
-  const float tot = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-  const float mu = tot / (float)nb;
-  __syncthreads();
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const int r = ra + i;
-    const float d = r < rb ? v[i] - mu : 0.f;
-    q += d * d;
-    if (c < C && r < rb) {
-      const bf16_t h = f2bf(v[i]);
-      hi[(int64_t)r * C + c] = h;
-      lo[(int64_t)r * C + c] = f2bf(v[i] - bf2f(h));
-    }
-  }
-  red[g][lane] = q;
-  __syncthreads();
-  if (g == 0 && c < C) {
-    stats[((int64_t)blockIdx.x * 2 + 0) * C + c] = tot;
-    stats[((int64_t)blockIdx.x * 2 + 1) * C + c] = red[0][lane] + red[1][lane] + red[2][lane] +
-                                                    red[3][lane];
-  }
-}
-
 // ---------------------------------------------------------------- pooling
 // resnet maxpool 3x3/s2/p1 over fp32 NHWC -> split pair (plain bf16 = hi, y_lo) + argmax
 // (first max in row-major window order wins, as k_maxpool_fwd).
@@ -429,17 +380,6 @@ extern "C" int dfu_pack_conv_weight_x3(const float* w, void* out, int32_t K, int
   const int64_t n = (int64_t)K * R * S * C;
   hipLaunchKernelGGL(k_pack_conv_weight_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream,
                      w, (bf16_t*)out, K, C, R, S, pattern);
-  DFU_LAUNCH_CHECK();
-  return DFU_OK;
-}
-
-extern "C" int dfu_stats_pair_f32(const float* y, int64_t M, int32_t C, float* stats, void* hi,
-                                  void* lo, void* stream) {
-  DFU_CHECK_ARG(y && stats && hi && lo && M > 0 && M < (1ll << 31) && C > 0,
-                "dfu_stats_pair_f32: bad args");
-  hipLaunchKernelGGL(k_stats_pair_f32, dim3((unsigned)((M + 127) / 128), (C + 63) / 64),
-                     dim3(256), 0, (hipStream_t)stream, y, (int)M, C, stats, (bf16_t*)hi,
-                     (bf16_t*)lo);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

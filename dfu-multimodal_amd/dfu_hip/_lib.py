@@ -152,7 +152,6 @@ PROTOTYPES = {
     "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, I32, P],
     "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P],
     "dfu_patchify_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
-    "dfu_stats_pair_f32": [P, I64, I32, P, P, P, P],
     "dfu_bn_apply_x3": [P, P, P, P, P, P, I32, I32, P, P, P, P, P, I64, I32, P],
     "dfu_maxpool_fwd_x3": [P, I32, I32, I32, I32, P, P, P, I32, I32, P],
     "dfu_avgpool_fwd_x3": [P, P, I32, I32, I32, P, P],

@@ -560,15 +560,6 @@ def conv_fwd(x_rows, geom, w_krsc, y, stats):
                  epilogue=L.EPI_BF16_STATS, stats=stats, conv=g)
 
 
-# Split-K for the bf16x3 forward's convolutions whose 128x128 tiles cannot fill the chip over a
-# long tripled K (layer 3-4: 100-196 tiles, 96-216 K-steps); DFU_X3_SPLIT=0: never (A/B).
-_X3_SPLIT = os.environ.get("DFU_X3_SPLIT", "1") != "0"
-
-
-def _x3_split(M, N, K3):
-    return _X3_SPLIT and ((M + 127) // 128) * ((N + 127) // 128) < 256 and K3 >= 64 * 64
-
-
 def conv_fwd_x3(x_pair, geom, w3, y, stats, y_lo=None):
     """bf16x3: y[M, K] = conv(x) over the split pair x = (hi, lo) [N*H*W, C] (the GEMM reads
     interleaved pairs, or the channel-tripled hi | lo | hi) and KRSC' weights (conv_weight_x3),
@@ -581,19 +572,6 @@ def conv_fwd_x3(x_pair, geom, w3, y, stats, y_lo=None):
     C3 = (2 if pairs else 3) * g.c
     K3 = g.r * g.s * C3
     xk = dict(x3=True, a_lo=lo, x3_pairs=pairs)
-    if y_lo is not None and _x3_split(M, g.k, g.r * g.s * 3 * g.c):
-        # few 128x128 tiles over a long tripled K (layers 3-4): split-K into fp32 slabs, then
-        # the statistics and the pair from the reduced output
-        acc = _empty((M, g.k), F32, y.device)
-        ops.zero_(acc)
-        if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
-            ops.gemm(M, g.k, C3, hi, g.c, w3, C3, acc, g.k, epilogue=L.EPI_F32_ACC, **xk)
-        else:
-            g3 = ops.ConvGeom(g.n, g.h, g.w, C3, g.k, g.r, g.s, g.stride, g.pad)
-            ops.gemm(M, g.k, K3, hi, 0, w3, K3, acc, g.k, a_mode=L.OPND_CONV_FWD,
-                     epilogue=L.EPI_F32_ACC, conv=g3, **xk)
-        ops.stats_pair_f32(acc, M, g.k, stats, y, y_lo)
-        return
     out = dict(aux_out=y_lo, ldaux_out=g.k if y_lo is not None else 0)
     if g.r == 1 and g.s == 1 and g.stride == 1 and g.pad == 0:
         ops.gemm(M, g.k, C3, hi, g.c, w3, C3, y, g.k, epilogue=L.EPI_F32_STATS, stats=stats,

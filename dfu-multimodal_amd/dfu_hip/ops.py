@@ -829,13 +829,6 @@ def bn_apply_x3(y, scale, shift, residual, res_mode, relu, M, C, out_lo=None, ou
                                 int(C), stream_ptr()), "dfu_bn_apply_x3")
 
 
-def stats_pair_f32(y, M, C, stats, hi, lo):
-    """BN tile statistics + split pair of a split-K conv's fp32 output (dfu_stats_pair_f32)."""
-    _req(y, F32, "stats_pair_f32")
-    check(lib().dfu_stats_pair_f32(ptr(y), int(M), int(C), ptr(stats), ptr(hi), ptr(lo),
-                                   stream_ptr()), "dfu_stats_pair_f32")
-
-
 def maxpool_fwd_x3(x, B, H, W, C):
     """-> (lo [B*P*Q, C], hi = plain bf16 [B, P, Q, C], argmax, P, Q)"""
     _req(x, F32, "maxpool_fwd_x3")

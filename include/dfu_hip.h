@@ -147,8 +147,8 @@ typedef struct dfu_gemm_desc {
   /* 1 = interleaved pairs (with a_seg, a_seg % 32 == 0): K (conv: conv_c) = 2 a_seg, and each
    * 64-wide K-step is [hi | lo] of 32 real k -- A read so from the split pair, B stored so
    * (dfu_split_x3 / dfu_pack_conv_weight_x3 pattern 2); the kernel forms hi·hi + lo·hi + hi·lo
-   * per step, the tripled-K sum from 2 operand tiles instead of 3.  Tiles 1, 2, 5, 10, 11
-   * (F32_STATS; F32_ACC on 1 and 5). */
+   * per step, the tripled-K sum from 2 operand tiles instead of 3.  Tiles 1, 2, 10, 11
+   * (F32_STATS). */
   int32_t x3_pairs;
 } dfu_gemm_desc;
 
@@ -480,11 +480,6 @@ int dfu_im2col_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_
                       void* stream);
 int dfu_patchify_f32_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
                         int32_t C, int32_t H, int32_t W, int32_t ps, void* out, void* stream);
-/* After a split-K bf16x3 convolution (fp32 y [M][C], slabs reduced): the DFU_EPI_F32_STATS
- * epilogue's products -- per 128-row tile (sum, M2) records into stats [ceil(M/128)][2][C] and
- * the split pair hi = bf16(y), lo = bf16(y - hi) [M][C] each. */
-int dfu_stats_pair_f32(const float* y, int64_t M, int32_t C, float* stats, void* hi, void* lo,
-                       void* stream);
 /* BN apply on the conv output y: v = act(y*scale + shift (+ residual)).  y is fp32 [M][C]
  * (y_lo null) or the split pair the F32_STATS epilogue writes with aux_out (y = hi, y_lo = lo,
  * bf16 each; hi is then the BN backward's bf16 y and y_bf16 is not written).  Residual mode 0

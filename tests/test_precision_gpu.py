@@ -89,7 +89,7 @@ def test_interleaved_pair_layouts():
 def test_x3_pairs_gemm_every_tile(conv, C):
     """The interleaved-pair bf16x3 kernels (three products per K-step from a hi and a lo tile)
     on every tile that instantiates them -- F32_STATS with the pair output on tiles 1, 2, 10,
-    11, F32_ACC split-K on 1 and 5 -- K-major and implicit-conv A, ragged M: fp32-accurate
+    11 -- K-major and implicit-conv A, ragged M: fp32-accurate
     against fp64, and within fp32 summation order of the tripled-K kernels (which need the
     conv's C % 64 == 0: C = 96 runs the pair kernels only)."""
     L, ops = _ops()
@@ -139,11 +139,6 @@ def test_x3_pairs_gemm_every_tile(conv, C):
                  x3=True, a_lo=lo, x3_pairs=True, tile=tile, aux_out=yl, ldaux_out=Kout, **kw2)
         assert torch.equal(yh, y.to(torch.bfloat16)), tile
         assert torch.equal(yl, (y - yh.float()).to(torch.bfloat16)), tile
-    for tile, split in ((1, 1), (1, 4), (5, 3)):
-        acc = torch.zeros(M, Kout, device=DEV)
-        ops.gemm(M, Kout, K2, hi, lda, w2, K2, acc, Kout, epilogue=L.EPI_F32_ACC, x3=True,
-                 a_lo=lo, x3_pairs=True, tile=tile, split_k=split, **kw2)
-        assert ((acc - y3).norm() / y3.norm()).item() < 2e-6, (tile, split)
     with pytest.raises(L.DfuError):  # no interleaved-pair kernel on the persistent tiles
         ops.gemm(M, Kout, K2, hi, lda, w2, K2, y3, Kout, epilogue=L.EPI_F32_STATS, stats=st3,
                  x3=True, a_lo=lo, x3_pairs=True, tile=8, **kw2)
@@ -278,10 +273,9 @@ def test_conv_fwd_x3_matches_fp32_conv(R, stride):
 
 
 @pytest.mark.parametrize("R,stride,C,H", [(3, 1, 512, 7), (3, 2, 256, 28), (1, 1, 2048, 7)])
-def test_conv_fwd_x3_split_k_path(R, stride, C, H):
-    """The layer-3/4 shapes whose 128x128 tiles cannot fill the chip run split-K (fp32 slabs,
-    then dfu_stats_pair_f32): the pair and the BN tile statistics against fp64 conv2d, and the
-    same within fp32 summation order of the unsplit F32_STATS path."""
+def test_conv_fwd_x3_long_k_few_tiles(R, stride, C, H):
+    """The layer-3/4 shapes (few output tiles over a long K) on the pair kernels: the output
+    pair and the BN tile statistics against fp64 conv2d / fp64 statistics of the fp32 output."""
     from dfu_hip import functional as Fn
     L, ops = _ops()
     torch.manual_seed(10)
@@ -291,28 +285,20 @@ def test_conv_fwd_x3_split_k_path(R, stride, C, H):
     pad = R // 2
     g = ops.ConvGeom(Bn, H, H, C, Kout, R, R, stride, pad)
     M = Bn * g.p * g.q
-    assert Fn._x3_split(M, Kout, R * R * 3 * C)
     rows = x.permute(0, 2, 3, 1).reshape(-1, C).contiguous()
-    w3 = Fn.conv_weight_x3(w)
-    outs = []
-    old = Fn._X3_SPLIT
-    try:
-        for split in (True, False):
-            Fn._X3_SPLIT = split
-            yh = torch.empty(M, Kout, dtype=torch.bfloat16, device=DEV)
-            yl = torch.empty_like(yh)
-            st = torch.empty(ops.stats_tiles(M), 2, Kout, device=DEV)
-            Fn.conv_fwd_x3(_pair(rows), g, w3, yh, st, y_lo=yl)
-            outs.append((yh.float() + yl.float(), st))
-    finally:
-        Fn._X3_SPLIT = old
+    yh = torch.empty(M, Kout, dtype=torch.bfloat16, device=DEV)
+    yl = torch.empty_like(yh)
+    st = torch.empty(ops.stats_tiles(M), 2, Kout, device=DEV)
+    Fn.conv_fwd_x3(_pair(rows), g, Fn.conv_weight_x3(w), yh, st, y_lo=yl)
+    y = yh.double() + yl.double()
     ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=stride, padding=pad)
     ref = ref.permute(0, 2, 3, 1).reshape(-1, Kout)
-    for y, st in outs:
-        assert ((y.double() - ref).norm() / ref.norm()).item() < 2e-5
-    (ys, ss), (yu, su) = outs
-    assert ((ys - yu).norm() / yu.norm()).item() < 2e-5
-    assert ((ss - su).norm() / su.norm()).item() < 1e-4
+    assert ((y - ref).norm() / ref.norm()).item() < 2e-5
+    for t in range(ops.stats_tiles(M)):
+        blk = y[t * 128:(t + 1) * 128]
+        assert torch.allclose(st[t, 0].double(), blk.sum(0), rtol=1e-4, atol=1e-3)
+        q = ((blk - blk.mean(0)) ** 2).sum(0)
+        assert torch.allclose(st[t, 1].double(), q, rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("C", [192, 160, 96])
