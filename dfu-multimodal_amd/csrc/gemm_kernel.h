@@ -1093,7 +1093,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_kernel(const GemmArgs p) {
   // so the LDS latency overlaps MFMAs (counted lgkmcnt waits) instead of draining per group.
   auto compute = [&](const char* la) {
     const char* lb = la + T::A_BYTES;
-    static_assert(!X3 || (FM * FN < 32 && AK && BKc), "interleaved pairs: K-contiguous, <= 64x64 per wave");
+    static_assert(!X3 || (FM * FN < 32 && AK && BKc),
+                  "interleaved pairs: K-contiguous operands, at most 64x64 per wave");
     if constexpr (FM * FN >= 32) {
       // 256x256: 128 accumulator registers leave room for one k-half of fragments at a time
 #pragma unroll

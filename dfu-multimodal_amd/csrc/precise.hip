@@ -146,7 +146,8 @@ DFU_DEV void ld8_pair(const bf16_t* hi, const bf16_t* lo, int64_t e, float* f) {
 // ---------------------------------------------------------------- BatchNorm apply
 // out = act(y*scale + shift + res) from the fp32 conv output y (F32_STATS epilogue), or from
 // the split pair (y = hi, y_lo = lo) that epilogue writes with aux_out (hi is then the BN
-// backward's bf16 y itself, so y_bf is not written).  res_mode 0 none, 1 fp32 [M][C], 2 split pair (res = hi, res_lo = lo, [M][C] each).  Outputs
+// backward's bf16 y itself, so y_bf is not written).  res_mode 0 none, 1 fp32 [M][C], 2 split
+// pair (res = hi, res_lo = lo, [M][C] each).  Outputs
 // (each optional): the pair hi = out_bf (the plain bf16 tensor the backward saves and the next
 // convolution's hi operand) and out_lo, fp32 (a residual), y rounded to bf16 (the BN backward's
 // input), and the ReLU bitmask (bit k of byte i = output element 8i + k > 0: the BN backward's
@@ -158,7 +159,7 @@ __global__ void k_bn_apply_x3(const void* __restrict__ y, const bf16_t* __restri
                               bf16_t* __restrict__ out_lo, bf16_t* __restrict__ out_bf,
                               float* __restrict__ out_f32, bf16_t* __restrict__ y_bf,
                               uint8_t* __restrict__ relu_mask, int64_t M, int C, int cv_log2) {
-  const int cv = C / 8;  // a power of two (every ResNet-50 width; host-checked): shifts, no division
+  const int cv = C / 8;  // a power of two (every ResNet-50 width; host-checked): no division
   const int64_t n = M * cv;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
