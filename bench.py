@@ -29,9 +29,10 @@ import torch.distributed as dist  # noqa: E402
 FLOPS_PER_UNIT = {"fusion": 129.44e9, "thermal": 105.15e9, "rgb": 24.29e9, "gradcam": 173.20e9}
 PEAK_BF16_TFLOPS = 2500.0
 PRECISION_NOTE = {
-    "parity": "forward: ResNet50 bf16x3 (split-bf16 MFMA, fp32-accurate), ViT-B/16 fp16 MFMA "
-              "(fp32 accumulate / residual / LN / softmax); backward + AdamW: bf16 MFMA, fp32 "
-              "master weights and optimizer state (DESIGN.md §4)",
+    "parity": "the library default.  forward: ResNet50 bf16x3 (split-bf16 MFMA, fp32-accurate), "
+              "ViT-B/16 Blocks fp16 MFMA inside the fusion model (fp32 accumulate / residual / "
+              "LN / softmax), bf16x3 when the ViT classifies alone (C2); backward + AdamW: bf16 "
+              "MFMA, fp32 master weights and optimizer state (DESIGN.md §4)",
     "bf16": "bf16 MFMA operands and activations, fp32 accumulate / statistics / master weights",
     "bf16x3": "forward fp32-accurate on split-bf16 MFMA everywhere; backward bf16"}  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 RGB_MEAN = (0.485, 0.456, 0.406)
@@ -54,11 +55,13 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU baseline threads (default: the host's physical cores, lscpu "
                          "sockets x cores per socket, BASELINE.md)")
-    ap.add_argument("--precision", default="parity", choices=["parity", "bf16", "bf16x3"],
-                    help="forward precision of the timed step (value).  parity (default): the "
-                         "ResNet forward bf16x3, the ViT forward fp16, backward bf16 -- the "
-                         "mode that meets north_star's 1e-3 logits bar with margin (DESIGN.md "
-                         "§4); the other modes are timed beside it under precision_modes")
+    ap.add_argument("--precision", default=None, choices=["parity", "bf16", "bf16x3"],
+                    help="forward precision of the timed step (value).  Default: the library's "
+                         "own default (dfu_hip.functional.DEFAULT_PRECISION = parity: the ResNet "
+                         "forward bf16x3, the ViT Blocks fp16 in the fusion model / bf16x3 when "
+                         "the ViT classifies alone, backward bf16 -- the mode that meets "
+                         "north_star's 1e-3 logits bar with margin, DESIGN.md §4), with no "
+                         "set_precision call; the other modes are timed beside it")
     ap.add_argument("--no-alt-precision", action="store_true",
                     help="skip timing the other precision modes")
     ap.add_argument("--no-parity", action="store_true",
@@ -74,6 +77,20 @@ def baseline_threads(args):
     if args.cpu_threads:
         return args.cpu_threads
     return host_cores().get("physical_cores") or os.cpu_count() or 1
+
+
+def arithmetic_label(model):
+    """What the timed step computes in, per encoder, under the current precision mode (the
+    line's `dtype`): the forward stage modes (models.precision.stages), then the backward."""
+    from dfu_hip import functional as Fn
+    from models import precision as P
+    fwd = {}
+    for name, m in P.stages(model).items():
+        enc = "ResNet50" if name.startswith("resnet") else "ViT-B/16 Blocks"
+        fwd.setdefault(enc, set()).add(Fn.stage_mode(m))
+    parts = [f"{enc} {'/'.join(sorted(ms))}" for enc, ms in fwd.items()]
+    return (f"fwd {', '.join(parts)} (fp32 accumulate, residual stream, statistics); "
+            f"bwd bf16 MFMA; fp32 master weights / AdamW")
 
 
 def synthetic(B, device, seed):
@@ -289,15 +306,17 @@ def gemm_roofline(fwd_bwd, tail, replays=3):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / replays  # per step
     flops = sum(r[1] for r in rec)
-    # MFMA work executed: a bf16x3 GEMM runs its K three times (the record counts it once)
-    executed = sum(2.0 * r[0].M * r[0].N * r[0].K for r in rec)
+    # MFMA work executed (ops.gemm's record): a bf16x3 GEMM runs three products of the real K,
+    # on the tripled K and on interleaved pairs alike (K = 2C: three 32-wide MFMAs per 64-wide
+    # K-step)
+    executed = sum(r[4] for r in rec)
     nbytes = sum(r[2] for r in rec)
     n = len(rec)
     return {"launches_per_step": n, "avg_launch_us": us / n, "flops_per_launch": flops / n,
             "bytes_per_launch": nbytes / n, "gemm_ms_per_step": us / 1e3,
             "achieved": flops / (us * 1e-6) / 1e12,
             "mfma_executed": executed / (us * 1e-6) / 1e12,
-            "x3_launches": sum(1 for r in rec if 2.0 * r[0].M * r[0].N * r[0].K != r[1])}
+            "x3_launches": sum(1 for r in rec if r[4] == 3.0 * r[1])}
 
 
 def main_gradcam(args, rank, world, dev):
@@ -308,6 +327,10 @@ def main_gradcam(args, rank, world, dev):
     over ranks (each its own samples; no data-path collective)."""
     from models.fusion import MultimodalFusionModel
     from models.gradcam import GradCAM
+    from dfu_hip import functional as Fn
+    if args.precision is not None:
+        Fn.set_precision(args.precision)
+    args.precision = Fn.get_precision()  # the library default unless --precision names one
     model = MultimodalFusionModel(num_classes=2, dropout=0.7).to(dev).eval()
     rgb, th, _ = synthetic(args.batch, dev, seed=42 + rank)
     cam_rgb = GradCAM(model.resnet, ["layer4"])
@@ -399,7 +422,10 @@ def main_gradcam(args, rank, world, dev):
             "value": round(value, 2), "unit": "samples/sec", "n_gpus": args.gpus,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1000.0 / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "scaling": "weak", "vs_baseline": None, "dtype": arithmetic_label(model),
+            "precision": args.precision,
+            "precision_source": "library default (no set_precision call)"
+            if args.precision == Fn.DEFAULT_PRECISION else "--precision",
             "data": "synthetic 224x224 RGB+thermal pairs (uint8 U{0..255}, reference "
                     "normalisation), random-init weights (seed 42), resident in HBM",
             "config": {"workload": "C5 fusion eval predict + ResNet 'layer4' Grad-CAM + ViT "
@@ -691,7 +717,11 @@ def main():
     from dfu_hip import functional as Fn
     from dfu_hip import nn as hnn
     from dfu_hip.optim import FusedAdamW
-    Fn.set_precision(args.precision)
+    precision_source = "library default (no set_precision call)"
+    if args.precision is not None:
+        Fn.set_precision(args.precision)
+        precision_source = "--precision"
+    args.precision = Fn.get_precision()
     model, fwd = build(args.config, dev)
     parallel.broadcast_parameters(model)
     opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
@@ -814,8 +844,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": arithmetic_label(model),
             "precision": args.precision,
+            "precision_source": precision_source,
             "precision_note": PRECISION_NOTE.get(args.precision),
             "data": "synthetic 224x224 RGB+thermal pairs (uint8 U{0..255}, reference "
                     "normalisation), random-init weights (seed 42), resident in HBM",

@@ -66,9 +66,11 @@ class ShardedSequentialSampler(torch.utils.data.Sampler):
     and confusion counts is the single-process one, with batch_size = the loader's), and
     ``global_indices()`` tells evaluate() how to put the gathered per-rank rows back in the
     reference's order.  Ranks may run different numbers of batches (eval has no per-batch
-    collective)."""
+    collective).  ``batch_size`` is required and must equal the loader's (training.loop checks
+    it): a sampler split by one batch size under a loader batching by another would form
+    batches the single-process run never forms."""
 
-    def __init__(self, n, rank=0, world_size=1, batch_size=1):
+    def __init__(self, n, rank=0, world_size=1, *, batch_size):
         if world_size < 1 or not 0 <= rank < world_size:
             raise ValueError(f"rank {rank} of world {world_size}")
         if batch_size < 1:

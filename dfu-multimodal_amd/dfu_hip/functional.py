@@ -33,7 +33,9 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 # ------------------------------------------------------------------------ precision mode
-# "bf16" (default): bf16 GEMM operands and activations, fp32 accumulation and statistics.
+# "parity" is the library default (DEFAULT_PRECISION): a drop-in script that never names a mode
+# gets logits within north_star's 1e-3 of the reference's fp32 path.
+# "bf16" (opt-in): bf16 GEMM operands and activations, fp32 accumulation and statistics.
 # "bf16x3": the FORWARD pass at fp32 accuracy (csrc/precise.hip): every forward contraction
 #   runs on the same MFMA GEMM over split-bf16 triples (hi/lo operands, K tripled), activations
 #   stay fp32 between kernels and attention runs in fp32, so the fusion logits meet north_star's
@@ -45,7 +47,8 @@ F32 = torch.float32
 # "parity": the headline mode -- per stage the precision its module class names in
 #   ``dfu_parity_precision``: every ResNet stage bf16x3, every ViT Block fp16 (the cheapest
 #   assignment measured to keep the fusion logits within north_star's 1e-3 of the fp32 oracle
-#   with margin: profiles/r16_precision_study.md).
+#   with margin: profiles/r16a_precision_grid.json, profiles/r19_precision_study.json).  A
+#   model may override a stage's class default on the instance (models.single.ThermalOnlyModel).
 # "mixed": per stage -- a ResNet Bottleneck / ViT Block (or the ResNet module itself, for the
 #   stem) runs its ``dfu_precision`` attribute's mode ("bf16", "bf16x3", ViT Blocks also
 #   "fp16"), bf16x3 where unset (models.precision.apply_policy sets the attributes).  A bf16 or
@@ -53,7 +56,8 @@ F32 = torch.float32
 #   stage's output reaches a bf16 stage as the bf16 copy it also writes.
 PRECISIONS = ("bf16", "bf16x3", "mixed", "parity")
 STAGE_MODES = ("bf16", "bf16x3", "fp16")
-_precision = ["bf16"]
+DEFAULT_PRECISION = "parity"
+_precision = [DEFAULT_PRECISION]
 
 
 def set_precision(mode):

@@ -93,8 +93,8 @@ def gemm_replay(records, stream=None):
     """Re-issue recorded dfu_gemm launches (same descriptors) on the current stream."""
     s = stream_ptr() if stream is None else stream
     fn = lib().dfu_gemm
-    for d, _, _, _ in records:
-        check(fn(ctypes.byref(d), s), "dfu_gemm replay")
+    for r in records:
+        check(fn(ctypes.byref(r[0]), s), "dfu_gemm replay")
 
 
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KMAJOR,
@@ -153,8 +153,10 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
         flops = 2.0 * M * N * (K // (2 if x3_pairs else 3) if x3 else K)
         if a_mode == L.OPND_CONV_DGRAD and conv is not None:
             flops /= conv.stride * conv.stride  # algorithmic: only the 1/stride^2 live taps
+        # executed MFMA work: a bf16x3 GEMM runs three products of the real K
+        executed = 3.0 * flops if x3 else 2.0 * M * N * K
         gemm_record.append((d, flops, _algorithmic_bytes(d, conv),
-                            (A, B, C, bias, aux, aux_out, stats, workspace, a_lo)))
+                            (A, B, C, bias, aux, aux_out, stats, workspace, a_lo), executed))
 
 
 _COUNTERS = {}

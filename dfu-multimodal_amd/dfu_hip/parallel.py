@@ -71,26 +71,37 @@ def _supports_avg(group=None):
 
 
 class GradAllReducer:
-    """Bucketed all-reduce (sum, then /world) over the FusedAdamW flat gradient buffer.
+    """Bucketed all-reduce (mean over ranks) over the FusedAdamW flat gradient buffer.
 
-    overlap=True: buckets launch from grad-ready notifications on a side stream during
-    backward; call ``finish()`` before the optimizer step.  overlap=False: ``finish()`` issues
-    every bucket after backward (graph-capture friendly)."""
+    overlap=True: each bucket's collective is issued from the grad-ready notifications while
+    backward still runs; call ``finish()`` before the optimizer step.  overlap=False:
+    ``finish()`` issues every bucket after backward (graph-capture friendly).
+
+    No stream of its own.  A bucket is issued asynchronously on the
+    stream that produced its last gradient (the "carrier": the ViT branch's side stream or the
+    backward's own stream); the process group's internal stream (PG-NCCL's) waits on that
+    stream's position and runs the collective there, so the backward on the carrier is not
+    held.  Gradients of the same bucket produced on another stream are covered by an event
+    recorded on that stream when the bucket's producer last switched away from it (a few
+    records per step, not one per parameter).  ``finish()`` makes the caller's stream wait for
+    every collective.  So the fusion step at N > 1 uses the main stream, the ViT side stream and
+    the process group's stream: 3 of the box's 4 hardware queues (GPU_MAX_HW_QUEUES), where a
+    reducer stream of its own made 4 and any further stream would serialise the encoders."""
 
     def __init__(self, flat, bucket_mb=None, overlap=True, group=None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.overlap = overlap and self.world > 1
-        self.stream = torch.cuda.Stream() if flat.grad.is_cuda else None
+        self.cuda = flat.grad.is_cuda
         # Buckets exist to start reducing while backward still runs.  Without overlap every
         # bucket is issued back to back after backward, so one large bucket (fewer collective
         # launches, full-size ring transfers over xGMI) is strictly better.
         if bucket_mb is None:
             bucket_mb = 32.0 if self.overlap else 1024.0
         # the mean as one collective (RCCL/NCCL ReduceOp.AVG: the 1/world scaling rides in the
-        # reduction) where the backend has it; otherwise SUM then one scaling pass per bucket
-        self.avg = self.world > 1 and flat.grad.is_cuda and _supports_avg(group)
+        # reduction) where the backend has it; otherwise SUM, then one scaling pass at finish()
+        self.avg = self.world > 1 and self.cuda and _supports_avg(group)
         cap = int(bucket_mb * (1 << 20) / 4)
         # reverse parameter order: the last parameters' gradients are produced first
         order = list(range(len(flat.params)))[::-1]
@@ -110,7 +121,9 @@ class GradAllReducer:
         self._pending = None
         self._issued = None
         self._hook = None
+        self._works = []
         self.issue_log = []  # bucket indices in launch order (ranks must agree: RCCL pairs them)
+        self.carriers = {}  # id(stream) -> stream: the streams collectives were issued from
         if self.overlap:
             self._hook = Fn.register_grad_ready_hook(self._on_ready)
 
@@ -118,27 +131,48 @@ class GradAllReducer:
         """Arm the per-step bucket state (call before backward)."""
         self._pending = [set(b[2]) for b in self.buckets]
         self._issued = [False] * len(self.buckets)
+        # per bucket: the stream of its latest gradient, and {id: (stream, event)} of the other
+        # streams it drew gradients from (event recorded when the producer switched away)
+        self._last = [None] * len(self.buckets)
+        self._marks = [{} for _ in self.buckets]
+        self._works = []
 
-    def _launch(self, k):
+    def _producer(self, p):
+        if not self.cuda:
+            return None
+        st = getattr(p, "_dfu_grad_stream", None)
+        return st if st else False  # False: several (or unknown) producer streams
+
+    def _note(self, k, st):
+        prev = self._last[k]
+        if prev is not None and prev is not st and prev is not False:
+            ev = torch.cuda.Event()
+            ev.record(prev)
+            self._marks[k][id(prev)] = (prev, ev)
+        self._last[k] = st
+
+    def _launch(self, k, carrier=None):
         lo, hi, _ = self.buckets[k]
         view = self.flat.grad[lo:hi]
-        if self.stream is not None:
-            # a bucket may hold gradients of both encoder branches (two streams): wait for all
-            self.stream.wait_stream(torch.cuda.current_stream())
-            Fn.join_grad_streams(self.stream, clear=False)
-            with torch.cuda.stream(self.stream):
-                self._reduce(view)
+        if self.cuda:
+            if carrier is None or carrier is False:
+                # unknown producers: every gradient stream joins the caller's stream first
+                carrier = torch.cuda.current_stream()
+                Fn.join_grad_streams(carrier, clear=False)
+            for sid, (st, ev) in self._marks[k].items():
+                if st is not carrier:
+                    carrier.wait_event(ev)
+            self.carriers[id(carrier)] = carrier
+            with torch.cuda.stream(carrier):
+                self._works.append(self._reduce(view))
         else:
-            self._reduce(view)
+            self._works.append(self._reduce(view))
         self._issued[k] = True
         self.issue_log.append(k)
 
     def _reduce(self, view):
-        if self.avg:
-            dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group)
-        else:
-            dist.all_reduce(view, group=self.group)
-            view.mul_(1.0 / self.world)
+        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        return dist.all_reduce(view, op=op, group=self.group, async_op=True)
 
     def _on_ready(self, p):
         if self._pending is None:
@@ -147,8 +181,11 @@ class GradAllReducer:
         for k, pend in enumerate(self._pending):
             if pid in pend:
                 pend.discard(pid)
+                st = self._producer(p)
+                if st is not None:
+                    self._note(k, st)
                 if not pend and not self._issued[k]:
-                    self._launch(k)
+                    self._launch(k, st)
                 break
 
     def finish(self):
@@ -160,8 +197,13 @@ class GradAllReducer:
         for k in range(len(self.buckets)):
             if not self._issued[k]:
                 self._launch(k)
-        if self.stream is not None:
-            torch.cuda.current_stream().wait_stream(self.stream)
+        for w in self._works:
+            w.wait()  # the caller's stream waits for the collective (host-blocking on gloo)
+        if not self.avg:
+            lo = min(b[0] for b in self.buckets)
+            hi = max(b[1] for b in self.buckets)
+            self.flat.grad[lo:hi].mul_(1.0 / self.world)
+        self._works = []
         self._pending = None
         self._issued = None
 

@@ -6,10 +6,11 @@ operands and activations), "bf16x3" (fp32-accurate split-bf16 operands) or, for 
 "fp16" (fp16 operands, fp32 accumulation and residual stream).  The backward is bf16 in every
 mode.
 
-  * functional.precision("parity") -- the headline mode -- runs each stage at its module
-    class's ``dfu_parity_precision``: ResNet stages bf16x3, ViT Blocks fp16.  It is the cheapest
-    assignment the per-stage study found to keep the fusion logits within half of north_star's
-    1e-3 of the fp32 oracle on every seed (profiles/r16_precision_study.md,
+  * functional.precision("parity") -- the headline mode and the library default -- runs each
+    stage at its ``dfu_parity_precision``: ResNet stages bf16x3, ViT Blocks fp16.  It is the
+    cheapest assignment the per-stage study found to keep the fusion logits within half of
+    north_star's 1e-3 of the fp32 oracle on every seed (profiles/r16a_precision_grid.json,
+    profiles/r16b_precision_study.json, profiles/r19_precision_study.json,
     tools/precision_policy_study.py): the random-init ResNet amplifies rounding ~30x more than
     the ViT, so its forward needs ~2^-17 products while the ViT's holds the bar with fp16's
     2^-11 -- and bf16 anywhere, even in the last ResNet block or ViT Block alone, costs 4-7e-4.

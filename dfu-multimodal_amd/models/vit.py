@@ -134,6 +134,27 @@ class VisionTransformer(tnn.Module):
     def get_classifier(self):
         return self.head
 
+    # The "parity" mode's Block precision when this ViT classifies by itself (its head is not
+    # Identity: train_thermal_only.py:188-205, C2).  Its logits see the blocks' rounding
+    # undiluted by a fusion head: with fp16 Blocks the thermal-only logits sit 1.2-1.6e-3 from
+    # the fp32 oracle (HIP 1.612e-3; tools/c2_precision_study.py, five seeds, CPU emulation of
+    # the fp16 sites), and no cheaper mix holds the 5e-4 margin (the first 1-3 Blocks bf16x3:
+    # 6.6e-4-1.2e-3; exact weights or LayerNorm outputs: 5.5e-4-9.5e-4), so every Block runs
+    # bf16x3.  As a fusion feature extractor (num_classes=0, head Identity) the class default,
+    # fp16, holds the fusion logits within 5e-4.
+    classifier_parity_precision = "bf16x3"
+
+    def _parity_policy(self):
+        """Set every Block's parity-mode precision for this ViT's role (see above); called at
+        the top of each forward, since the reference scripts replace ``head`` after
+        construction (train_thermal_only.py:188-205)."""
+        alone = not isinstance(self.head, tnn.Identity)
+        for blk in self.blocks:
+            if alone:
+                blk.dfu_parity_precision = self.classifier_parity_precision
+            elif "dfu_parity_precision" in blk.__dict__:
+                del blk.dfu_parity_precision
+
     def _embed(self, x):
         pe = self.patch_embed
         return Fn.PatchEmbedFn.apply(x, pe.proj.weight, pe.proj.bias, self.cls_token,
@@ -141,6 +162,7 @@ class VisionTransformer(tnn.Module):
 
     def forward_features(self, x):
         """Tokens after the final norm, fp32 (B, 197, 768) (all rows normalised)."""
+        self._parity_policy()
         x = self._embed(x)
         x = self.blocks(x)
         return self.norm(x)
@@ -152,6 +174,7 @@ class VisionTransformer(tnn.Module):
         return x if pre_logits else self.head(x)
 
     def forward(self, x):
+        self._parity_policy()
         x = self._embed(x)
         x = self.blocks(x)
         # final norm on the class-token rows only (== norm(x)[:, 0] for a per-token norm)
@@ -163,6 +186,7 @@ class VisionTransformer(tnn.Module):
     def forward_stages(self, x):
         """forward() as a generator yielding after the embedding and every Block (see
         models.resnet.ResNet.forward_stages)."""
+        self._parity_policy()
         x = self._embed(x)
         yield
         for blk in self.blocks:

@@ -128,6 +128,17 @@ def broadcast_buffers(model, src=0, group=None):
                 dist.broadcast(b.data, src, group=group)
 
 
+def _check_batch_split(loader):
+    """A sampler that splits the sample order by whole batches (data.sharding.
+    ShardedSequentialSampler) must split by the loader's own batch size, or the ranks' batches
+    are not batches of the single-process run (and the batch-mean losses differ from it)."""
+    sampler = getattr(loader, "sampler", None)
+    sb, lb = getattr(sampler, "batch_size", None), getattr(loader, "batch_size", None)
+    if sb is not None and lb is not None and sb != lb:
+        raise ValueError(f"sampler batch_size {sb} != loader batch_size {lb}: pass "
+                         f"ShardedSequentialSampler(..., batch_size=<the loader's>)")
+
+
 def run_epoch(model, loader, criterion, optimizer=None, train=True, reducer=None,
               forward=None, num_classes=2, device="cuda", group=None, collect=None):
     """One pass over `loader` (batches (*inputs, labels) on the GPU).  train=True runs the
@@ -136,6 +147,7 @@ def run_epoch(model, loader, criterion, optimizer=None, train=True, reducer=None
     summed over the ranks of `group` (data parallelism).  collect: a list that receives
     (logits, labels) per batch (the test phase)."""
     forward = forward or _forward_fn(model)
+    _check_batch_split(loader)
     model.train(train)
     met = DeviceMetrics(num_classes, device)
     with torch.set_grad_enabled(train):

@@ -10,6 +10,19 @@ for p in (REPO, PKG):
         sys.path.insert(0, p)
 
 
+@pytest.fixture(autouse=True)
+def _library_default_precision():
+    """Every test starts and ends in the library's default forward precision (a test that
+    changes it with set_precision cannot leak its mode into the next one)."""
+    fn = sys.modules.get("dfu_hip.functional")
+    if fn is not None:
+        fn.set_precision(fn.DEFAULT_PRECISION)
+    yield
+    fn = sys.modules.get("dfu_hip.functional")
+    if fn is not None:
+        fn.set_precision(fn.DEFAULT_PRECISION)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
 

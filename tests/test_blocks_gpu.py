@@ -9,6 +9,15 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _bf16_kernels():
+    """These checks hold the bf16 kernels to the bf16-rounded oracle (same rounding sites): run
+    the bf16 mode explicitly (the library default is "parity")."""
+    from dfu_hip import functional as Fn
+    with Fn.precision("bf16"):
+        yield
+
+
 def rel(a, b):
     a = a.detach().float().cpu()
     b = b.detach().float().cpu()

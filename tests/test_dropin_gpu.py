@@ -10,8 +10,10 @@ plain torch.nn heads and torch.optim.AdamW around models.encoders, exactly as wr
                                    ReLU, Dropout, Linear(512, 256), ReLU, Dropout, Linear(256, 2)),
                                    nn.CrossEntropyLoss(weight), AdamW(lr 1e-4, wd 1e-4)
 
-Each trains one step against the CPU oracle built the same way (bf16x3 logits within 1e-3,
-parameters after the AdamW step within one Adam step), then two more steps stay finite.  Also:
+Each trains one step against the CPU oracle built the same way, with NO precision call (the
+library default, "parity": logits within 1e-3; parameters after the AdamW step within one Adam
+step), then two more steps stay finite; the fusion construct also at C3's B = 64 within the
+5e-4 margin (what a drop-in caller gets).  Also:
 gradients edited in place between backward and step (clip_grad_norm_) reach the optimizer --
 the end-of-backward stream join and FusedAdamW's early-update guard."""
 import copy
@@ -40,8 +42,9 @@ def _train_step(model, opt, crit, inputs, y):
     return out.detach(), loss.detach()
 
 
-def _compare(name, hip, ref, make_inputs, B=8, steps_after=2):
+def _compare(name, hip, ref, make_inputs, B=8, steps_after=2, bar=BAR):
     from dfu_hip import functional as Fn
+    assert Fn.get_precision() == "parity" == Fn.DEFAULT_PRECISION
     torch.manual_seed(3)
     rgb, th, y = R.synthetic_batch(B, seed=5)
     w = R.class_weights(y)
@@ -52,9 +55,7 @@ def _compare(name, hip, ref, make_inputs, B=8, steps_after=2):
     out_r, loss_r = _train_step(m, opt_r, nn.CrossEntropyLoss(weight=w), make_inputs(rgb, th), y)
     opt_h = torch.optim.AdamW(hip.parameters(), lr=1e-4, weight_decay=1e-4)
     crit_h = nn.CrossEntropyLoss(weight=w.to(DEV))
-    with Fn.precision("bf16x3"):
-        out_h, loss_h = _train_step(hip, opt_h, crit_h, make_inputs(rgb.to(DEV), th.to(DEV)),
-                                    y.to(DEV))
+    out_h, loss_h = _train_step(hip, opt_h, crit_h, make_inputs(rgb.to(DEV), th.to(DEV)), y.to(DEV))
     torch.cuda.synchronize()
     d = _maxd(out_h, out_r)
     p_r = dict(m.named_parameters())
@@ -66,12 +67,13 @@ def _compare(name, hip, ref, make_inputs, B=8, steps_after=2):
         same = torch.sign(a - z) == torch.sign(b - z)
         agree += int(same.sum())
         total += same.numel()
-    print(f"\n[{name}] bf16x3 logits vs fp32 oracle {d:.3e}, loss {abs(loss_h.item() - loss_r.item()):.2e}; "
-          f"after torch AdamW: max |p - p_oracle| {worst:.2e}, update signs agree {agree / total:.4%}")
-    assert d <= BAR and abs(loss_h.item() - loss_r.item()) <= BAR
+    print(f"\n[{name} B={B}] default-mode logits vs fp32 oracle {d:.3e} (bar {bar}), loss "
+          f"{abs(loss_h.item() - loss_r.item()):.2e}; after torch AdamW: max |p - p_oracle| "
+          f"{worst:.2e}, update signs agree {agree / total:.4%}")
+    assert d <= bar and abs(loss_h.item() - loss_r.item()) <= bar
     assert worst <= 2.05e-4 and agree / total > 0.97
     assert all(p.grad is not None for p in hip.parameters())
-    for _ in range(steps_after):  # default bf16 mode, the reference's dropout
+    for _ in range(steps_after):
         _, loss = _train_step(hip, opt_h, crit_h, make_inputs(rgb.to(DEV), th.to(DEV)), y.to(DEV))
         assert torch.isfinite(loss).item()
     torch.cuda.synchronize()
@@ -121,6 +123,20 @@ def test_fusion_script_construct_lines_torch_head_and_adamw():
                         encoders.create_model("vit_base_patch16_224", pretrained=False,
                                               num_classes=0))
     _compare("train_multimodal_fusion.py construct", hip, ref, lambda r, t: (r, t))
+
+
+def test_c3_fusion_construct_default_precision_b64():
+    """INTEGRATION.md §1's switch of train_multimodal_fusion.py (hub_load + create_model, the
+    script's own torch.nn 3-layer head, nn.CrossEntropyLoss, torch.optim.AdamW), no precision
+    call anywhere, at C3's batch of 64: logits within the 5e-4 margin of the fp32 oracle."""
+    from models import encoders
+    torch.manual_seed(0)
+    ref = _ScriptFusion(R.ResNet(), R.VisionTransformer(num_classes=0))
+    hip = _ScriptFusion(encoders.hub_load("pytorch/vision:v0.13.1", "resnet50", pretrained=False),
+                        encoders.create_model("vit_base_patch16_224", pretrained=False,
+                                              num_classes=0))
+    _compare("train_multimodal_fusion.py construct", hip, ref, lambda r, t: (r, t), B=64,
+             steps_after=1, bar=5e-4)
 
 
 def _fusion_step(clip, early):

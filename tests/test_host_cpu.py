@@ -208,3 +208,16 @@ def test_fusion_head_hidden_dims_list_or_tuple():
     keys = [k for k in MultimodalFusionModel(layout="train").state_dict() if k.startswith("fusion")]
     assert keys == ["fusion.0.weight", "fusion.0.bias", "fusion.3.weight", "fusion.3.bias",
                     "fusion.6.weight", "fusion.6.bias"]
+
+
+def test_default_precision_is_the_parity_mode():
+    """The drop-in surface meets north_star's bar without any precision call (VERDICT round 4
+    item 1): the library default is "parity", as INTEGRATION.md §1 states."""
+    from dfu_hip import functional as Fn
+    assert Fn.DEFAULT_PRECISION == "parity" and Fn.get_precision() == "parity"
+    doc = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "INTEGRATION.md")).read()
+    assert '"parity" (the default' in doc
+    with Fn.precision("bf16"):
+        assert Fn.get_precision() == "bf16"
+    assert Fn.get_precision() == "parity"

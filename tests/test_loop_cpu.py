@@ -43,6 +43,22 @@ def test_sharded_samplers_cover_one_draw(n, world):
                 assert j % world == r and blk == list(range(j * B, min(n, (j + 1) * B)))
 
 
+def test_sequential_sampler_batch_size_required_and_checked():
+    """the val/test shard must split by the loader's batch size."""
+    from training.loop import run_epoch
+    with pytest.raises(TypeError):
+        ShardedSequentialSampler(10, 0, 2)  # batch_size is keyword-only and required
+
+    class _Loader:
+        batch_size = 4
+        sampler = ShardedSequentialSampler(10, 0, 2, batch_size=3)
+
+        def __iter__(self):
+            return iter(())
+    with pytest.raises(ValueError, match="batch_size"):
+        run_epoch(torch.nn.Identity(), _Loader(), None, train=False, device="cpu")
+
+
 def test_metrics_from_confusion_matches_sklearn():
     from sklearn.metrics import accuracy_score, f1_score
     g = torch.Generator().manual_seed(0)

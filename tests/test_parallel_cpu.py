@@ -41,6 +41,9 @@ def _worker(rank, port, overlap, q):
         # ~1 KiB buckets: several buckets, some holding one parameter, some several
         red = parallel.GradAllReducer(flat, bucket_mb=1.0 / 1024, overlap=overlap)
         assert len(red.buckets) >= 3
+        # no stream of its own (the step's streams must fit the box's
+        # 4 hardware queues): collectives ride the producing stream, asynchronously
+        assert not any(isinstance(v, torch.cuda.Stream) for v in vars(red).values())
         for p, g in zip(flat.params, _grads(rank)):
             p.grad.copy_(g)
         red.start()

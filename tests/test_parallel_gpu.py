@@ -43,7 +43,7 @@ def test_bucket_ready_points_are_final():
     red = parallel.GradAllReducer(opt.flat, bucket_mb=32.0, overlap=False)  # world 1
     snaps = {}
 
-    def launch(k):
+    def launch(k, carrier=None):
         lo, hi, _ = red.buckets[k]
         torch.cuda.synchronize()
         snaps[k] = opt.flat.grad[lo:hi].clone()
@@ -94,12 +94,22 @@ def _dp_worker(rank, port, q):
         crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
         rgb, th, y = bench.synthetic(4, dev, seed=42 + rank)  # each rank its own batch
 
+        streams = {}
+
         def step(red=None):
             opt.zero_grad()
             if red is not None:
                 red.start()
             loss = crit(model(rgb, th), y)
             loss.backward()
+            # the streams this step ran gradient work or collectives on (besides the process
+            # group's own internal stream)
+            streams.clear()
+            streams.update(Fn._grad_streams)
+            cur = torch.cuda.current_stream()
+            streams[id(cur)] = cur
+            if red is not None:
+                streams.update(red.carriers)
             Fn.join_grad_streams()
             if red is not None:
                 red.finish()
@@ -109,6 +119,8 @@ def _dp_worker(rank, port, q):
         local = opt.flat.grad.clone()
         red = parallel.GradAllReducer(opt.flat, overlap=True)
         step(red)  # overlapped bucketed all-reduce launched from the grad-ready hooks
+        nstreams = len({s.cuda_stream for s in streams.values()})
+        ncarriers = len(red.carriers)
         got = opt.flat.grad.clone()
         dist.all_reduce(local)  # the expectation: one plain all-reduce of the local gradients
         local /= 2
@@ -117,7 +129,8 @@ def _dp_worker(rank, port, q):
         scale = local.abs().max().item()
         g64 = got.double()
         idx = torch.arange(0, got.numel(), 997, device=dev)
-        q.put((rank, dict(diff=diff, scale=scale, log=list(red.issue_log),
+        q.put((rank, dict(diff=diff, scale=scale, log=list(red.issue_log), nstreams=nstreams,
+                          ncarriers=ncarriers,
                           nbuckets=len(red.buckets), sum=g64.sum().item(),
                           sq=(g64 * g64).sum().item(), sample=got[idx].cpu().numpy()), None))
         red.close()
@@ -132,7 +145,10 @@ def _dp_worker(rank, port, q):
 def test_fusion_dp_world2_overlapped_reducer():
     """SURVEY §8e check on the real fusion model with overlap=True: the
     averaged gradients equal the mean of the per-rank gradients, both ranks issue the buckets
-    in the same order (every one from the hooks), and hold identical averaged gradients."""
+    in the same order (every one from the hooks), and hold identical averaged gradients.  The
+    step stays inside the box's 4 hardware queues: gradient work and
+    collective launches use 2 streams (the main stream and the ViT branch's side stream) -- 3
+    with the process group's internal one."""
     import socket
 
     import torch.multiprocessing as mp
@@ -155,6 +171,9 @@ def test_fusion_dp_world2_overlapped_reducer():
     a, b = res[0], res[1]
     print(f"\n[DP world 2] buckets {a['nbuckets']}, issue order r0 {a['log']} r1 {b['log']}; "
           f"max |avg - mean(local)| {a['diff']:.2e} / {b['diff']:.2e} (scale {a['scale']:.2e})")
+    print(f"  streams used (grad producers + collective carriers): {a['nstreams']} / "
+          f"{b['nstreams']}; carriers {a['ncarriers']}")
+    assert a["nstreams"] <= 2 and b["nstreams"] <= 2
     assert a["log"] == b["log"] and sorted(a["log"]) == list(range(a["nbuckets"]))
     for d in (a, b):
         assert d["diff"] <= 1e-6 * max(d["scale"], 1e-30)

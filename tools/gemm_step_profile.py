@@ -75,7 +75,7 @@ def main():
     rec, ops.gemm_record = ops.gemm_record, None
     torch.cuda.synchronize()
     uniq = {}
-    for d, flops, nbytes, refs in rec:
+    for d, flops, nbytes, refs, _ in rec:
         e = uniq.setdefault(key(d), [d, flops, nbytes, refs, 0])
         e[4] += 1
     rows = []

@@ -104,7 +104,7 @@ def main():
     rec, ops.gemm_record = ops.gemm_record, None
     torch.cuda.synchronize()
     uniq = {}
-    for d, flops, _, refs in rec:
+    for d, flops, _, refs, _ in rec:
         if a.only_x3_pairs and not d.x3_pairs:
             continue
         if a.only_f16 and d.operand_type != 1:
