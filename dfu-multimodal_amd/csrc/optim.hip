@@ -82,13 +82,22 @@ DFU_DEV void adam_update(float& p, float g, float& m, float& v, const AdamCoef& 
   p -= a.step_size * (m / denom);
 }
 
+// The interleaved-pair bf16x3 shadow (dfu_adamw_flat's shadow_x3): elements [x3_begin,
+// x3_end) of the range, per 32-element block [hi 32 | lo 32] (hi = bf16(p), lo = bf16(p - hi)).
+struct X3Shadow {
+  bf16_t* base;
+  int64_t begin, end;  // element range (relative to the AdamW range); begin % 4 == 0
+};
+
 // Optionally also writes the bf16 shadow of the updated parameters (the GEMM operand copy),
-// so no per-step cast kernels are needed, and an fp16 shadow (the "parity" precision mode's
-// ViT forward operands).
+// so no per-step cast kernels are needed, an fp16 shadow (the "parity" precision mode's ViT
+// forward operands) and the interleaved-pair split of a sub-range (its ResNet forward's conv
+// weight operands: FlatParams.enable_x3).
 __device__ __forceinline__ void adamw_vec4(float* __restrict__ p, const float* __restrict__ g,
                                            float* __restrict__ m, float* __restrict__ v,
                                            bf16_t* __restrict__ shadow,
-                                           bf16_t* __restrict__ shadow16, int64_t i, f32x4 pp,
+                                           bf16_t* __restrict__ shadow16, const X3Shadow& x3,
+                                           int64_t i, f32x4 pp,
                                            f32x4 gg, f32x4 mm, f32x4 vv, const AdamCoef& a,
                                            float b1, float b2, float eps) {
 #pragma unroll
@@ -102,6 +111,18 @@ __device__ __forceinline__ void adamw_vec4(float* __restrict__ p, const float* _
   ((f32x4*)v)[i] = vv;
   if (shadow) ((u32x2*)shadow)[i] = (u32x2){pack2(pp[0], pp[1]), pack2(pp[2], pp[3])};
   if (shadow16) ((u32x2*)shadow16)[i] = (u32x2){pack2h(pp[0], pp[1]), pack2h(pp[2], pp[3])};
+  const int64_t e = 4 * i - x3.begin;
+  if (x3.base && e >= 0 && 4 * i < x3.end) {
+    float hi[4], lo[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hi[k] = bf2f(f2bf(pp[k]));
+      lo[k] = pp[k] - hi[k];
+    }
+    bf16_t* o = x3.base + 2 * e - (e & 31);  // block e / 32 at 64 (e / 32): [hi | lo]
+    *(u32x2*)o = (u32x2){pack2(hi[0], hi[1]), pack2(hi[2], hi[3])};
+    *(u32x2*)(o + 32) = (u32x2){pack2(lo[0], lo[1]), pack2(lo[2], lo[3])};
+  }
 }
 
 // Each thread handles ADAM_UNROLL float4 groups per grid-stride pass, spaced one grid apart so
@@ -118,7 +139,8 @@ __global__ void __launch_bounds__(256) k_adamw_flat(float* __restrict__ p,
                                                     float eps, float wd,
                                                     const int64_t* __restrict__ step_dev,
                                                     bf16_t* __restrict__ shadow,
-                                                    bf16_t* __restrict__ shadow16) {
+                                                    bf16_t* __restrict__ shadow16,
+                                                    const X3Shadow x3) {
   const AdamCoef a = adam_coef(*step_dev, lr, b1, b2, wd);
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -135,11 +157,11 @@ __global__ void __launch_bounds__(256) k_adamw_flat(float* __restrict__ p,
     }
 #pragma unroll
     for (int u = 0; u < ADAM_UNROLL; ++u)
-      adamw_vec4(p, g, m, v, shadow, shadow16, i + u * stride, pp[u], gg[u], mm[u], vv[u], a, b1,
-                 b2, eps);
+      adamw_vec4(p, g, m, v, shadow, shadow16, x3, i + u * stride, pp[u], gg[u], mm[u], vv[u], a,
+                 b1, b2, eps);
   }
   for (; i < n4; i += stride)
-    adamw_vec4(p, g, m, v, shadow, shadow16, i, ((f32x4*)p)[i], ((const f32x4*)g)[i],
+    adamw_vec4(p, g, m, v, shadow, shadow16, x3, i, ((f32x4*)p)[i], ((const f32x4*)g)[i],
                ((f32x4*)m)[i],
                ((f32x4*)v)[i], a, b1, b2, eps);
   for (int64_t k = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n;
@@ -209,9 +231,18 @@ extern "C" int dfu_ce_weighted_bwd(const float* saved, const float* grad_loss, i
 extern "C" int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                               int64_t n, float lr, float beta1, float beta2, float eps,
                               float weight_decay, const int64_t* step_dev, void* shadow_bf16,
-                              void* shadow_f16, void* stream) {
+                              void* shadow_f16, void* shadow_x3, int64_t x3_begin,
+                              int64_t x3_end, void* stream) {
   DFU_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step_dev && n > 0,
                 "dfu_adamw_flat: bad args");
+  // the pair blocks of 32 must sit inside whole float4 groups of the range, which must cover
+  // them: n % 4 == 0 there (the scalar tail writes no pairs)
+  DFU_CHECK_ARG(!shadow_x3 || (x3_begin >= 0 && x3_begin % 4 == 0 && x3_end >= x3_begin &&
+                               x3_end <= n / 4 * 4 && (x3_end - x3_begin) % 32 == 0 &&
+                               ((uintptr_t)shadow_x3 & 7) == 0),
+                "dfu_adamw_flat: x3 range [%lld, %lld) must be 4-aligned, a multiple of 32 long, "
+                "inside the range's float4 groups (n=%lld)", (long long)x3_begin,
+                (long long)x3_end, (long long)n);
   DFU_CHECK_ARG(((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 &&
                     ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0 &&
                     ((uintptr_t)shadow_bf16 & 7) == 0 && ((uintptr_t)shadow_f16 & 7) == 0,
@@ -228,7 +259,8 @@ extern "C" int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, f
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_adamw_flat<1>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param,
                      grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step_dev,
-                     (bf16_t*)shadow_bf16, (bf16_t*)shadow_f16);
+                     (bf16_t*)shadow_bf16, (bf16_t*)shadow_f16,
+                     X3Shadow{(bf16_t*)shadow_x3, x3_begin, shadow_x3 ? x3_end : 0});
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

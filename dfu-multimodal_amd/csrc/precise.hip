@@ -248,6 +248,75 @@ __global__ void k_maxpool_fwd_x3(const float* __restrict__ x, int B, int H, int 
   }
 }
 
+// The stem's bn1 + ReLU + maxpool 3x3/s2/p1 in one pass over the conv output's split pair
+// (y = hi, y_lo = lo; NHWC [B*H*W][C]): each window element is relu(fmaf(hi + lo, scale, shift))
+// -- k_bn_apply_x3's arithmetic -- and the max / argmax are k_maxpool_fwd_x3's, so the result
+// is bitwise the two-kernel path's, without its fp32 BN output (4 B written and read per conv
+// output element).  The BN backward's ReLU bitmask (k_bn_apply_x3's format) is written by the
+// window that owns each input element (its taps wi, wj in {1, 2}: rows 2p, 2p+1, columns 2q,
+// 2q+1 -- every element once, since H <= 2P and W <= 2Q).  One thread per (output pixel,
+// 8 channels); the nine taps' loads are all issued before the first compare.
+__global__ __launch_bounds__(256) void k_maxpool_bn_fwd_x3(
+    const bf16_t* __restrict__ yhi, const bf16_t* __restrict__ ylo,
+    const float* __restrict__ scale, const float* __restrict__ shift, int B, int H, int W, int C,
+    bf16_t* __restrict__ out_lo, bf16_t* __restrict__ out_bf, uint8_t* __restrict__ am,
+    uint8_t* __restrict__ relu_mask, int P, int Q, int cv_log2) {
+  const int cv = C >> 3;
+  const int n = B * P * Q * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c8 = i & (cv - 1);
+    const int pix = i >> cv_log2;
+    const int q = pix % Q;
+    const int t = pix / Q;
+    const int p = t % P;
+    const int b = t / P;
+    float sc[8], sh[8];
+    ld8_f32(scale + 8 * c8, sc);
+    ld8_f32(shift + 8 * c8, sh);
+    u32x4 hv[9], lv[9];
+    int64_t eo[9];
+    bool ok[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int ih = 2 * p - 1 + k / 3, iw = 2 * q - 1 + k % 3;
+      ok[k] = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      eo[k] = ok[k] ? ((int64_t)(b * H + ih) * W + iw) * C + 8 * c8 : 0;
+      hv[k] = *(const u32x4*)(yhi + eo[k]);
+      lv[k] = *(const u32x4*)(ylo + eo[k]);
+    }
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      if (!ok[k]) continue;
+      float h[8], l[8], f[8];
+      unpack8(hv[k], h);
+      unpack8(lv[k], l);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(h[e] + l[e], sc[e], sh[e]), 0.f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (f[e] > best[e] || (f[e] != f[e] && best[e] == best[e])) {
+          best[e] = f[e];
+          arg[e] = k;
+        }
+      if (relu_mask && k / 3 >= 1 && k % 3 >= 1) {  // this window owns the element
+        unsigned bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bits |= (unsigned)(f[e] > 0.f) << e;
+        relu_mask[eo[k] >> 3] = (uint8_t)bits;
+      }
+    }
+    st_pair8(out_bf, out_lo, (int64_t)pix * C + 8 * c8, best);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) packed |= (uint64_t)arg[e] << (8 * e);
+    *(uint64_t*)(am + (int64_t)pix * C + 8 * c8) = packed;
+  }
+}
+
 // AdaptiveAvgPool2d(1) over a split pair (hi, lo: [B*HW][C] each) -> fp32 [B][C].
 __global__ void k_avgpool_fwd_x3(const bf16_t* __restrict__ hi, const bf16_t* __restrict__ lo,
                                  int B, int HW, int C, float* __restrict__ y) {
@@ -419,6 +488,28 @@ extern "C" int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t 
   const int64_t n = (int64_t)B * P * Q * (C / 8);
   hipLaunchKernelGGL(k_maxpool_fwd_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream, x, B,
                      H, W, C, (bf16_t*)y_lo, (bf16_t*)y_bf16, argmax, P, Q);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
+
+extern "C" int dfu_maxpool_bn_fwd_x3(const void* y, const void* y_lo, const float* scale,
+                                     const float* shift, int32_t B, int32_t H, int32_t W,
+                                     int32_t C, void* out_lo, void* out_bf16, uint8_t* argmax,
+                                     uint8_t* relu_mask, int32_t P, int32_t Q, void* stream) {
+  const int cv = C / 8;
+  int cv_log2 = 0;
+  while ((1 << cv_log2) < cv) ++cv_log2;
+  DFU_CHECK_ARG(y && y_lo && scale && shift && out_lo && out_bf16 && argmax && C % 8 == 0 &&
+                    cv > 0 && (1 << cv_log2) == cv && P == (H - 1) / 2 + 1 &&
+                    Q == (W - 1) / 2 + 1 && (int64_t)B * H * W * C < (int64_t)1 << 31 &&
+                    (((uintptr_t)scale | (uintptr_t)shift) & 15) == 0,
+                "dfu_maxpool_bn_fwd_x3: bad args (C / 8 a power of two, P, Q of a 3x3/s2/p1 "
+                "pool, < 2^31 elements, 16-B aligned scale / shift)");
+  const int64_t n = (int64_t)B * P * Q * cv;
+  if (n == 0) return DFU_OK;
+  hipLaunchKernelGGL(k_maxpool_bn_fwd_x3, dim3(nblocks(n)), dim3(TPB), 0, (hipStream_t)stream,
+                     (const bf16_t*)y, (const bf16_t*)y_lo, scale, shift, B, H, W, C,
+                     (bf16_t*)out_lo, (bf16_t*)out_bf16, argmax, relu_mask, P, Q, cv_log2);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
 }

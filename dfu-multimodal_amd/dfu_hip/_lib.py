@@ -143,13 +143,14 @@ PROTOTYPES = {
     "dfu_ce_weighted_fwd": [P, P, P, I32, I32, P, P, P],
     "dfu_ce_weighted_bwd": [P, P, I32, I32, P, P],
     "dfu_adamw": [P, P, P, P, P, I32, P, I32, F, F, F, F, F, P, P],
-    "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P, P],
+    "dfu_adamw_flat": [P, P, P, P, I64, F, F, F, F, F, P, P, P, P, I64, I64, P],
     "dfu_step_increment": [P, P],
     "dfu_argmax_rows": [P, I32, I32, P, P],
     "dfu_softmax_rows": [P, I32, I32, P, P],
     "dfu_metrics_accumulate": [P, P, I32, I32, P, P, P, P, P],
     "dfu_split_x3": [P, I64, I32, I32, I32, P, I32, P, I64, P],
     "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, I32, P],
+    "dfu_maxpool_bn_fwd_x3": [P, P, P, P, I32, I32, I32, I32, P, P, P, P, I32, I32, P],
     "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P],
     "dfu_patchify_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
     "dfu_bn_apply_x3": [P, P, P, P, P, P, I32, I32, P, P, P, P, P, I64, I32, P],

@@ -483,7 +483,21 @@ _X3_PAIRS = os.environ.get("DFU_X3_PAIRS", "1") != "0"
 
 def conv_weight_x3(w):
     """fp32 OIHW conv weight -> bf16x3 KRSC' operand: C' = 2C interleaved pairs (_X3_PAIRS) or
-    C' = 3C [hi | hi | lo]; 1x1: the row split."""
+    C' = 3C [hi | hi | lo]; 1x1: the row split.  A FusedAdamW-managed weight reads the pairs
+    from the optimizer's x3 shadow (optim.FlatParams.enable_x3: written by the AdamW kernel, no
+    launch here); re-split only after an edit outside the optimizer (version counter)."""
+    flat = getattr(w, "_dfu_flat", None)
+    if _X3_PAIRS and flat is not None:
+        from .optim import x3_pair_weight
+        if x3_pair_weight(w):
+            if flat.shadow_x3 is None:
+                flat.enable_x3()
+            sh = w._dfu_shadow_x3
+            if w._version != getattr(w, "_dfu_shadow_x3_version", -1):
+                src = w.detach().permute(0, 2, 3, 1).reshape(-1, 32)  # KRSC rows of 32
+                ops.split_x3_into(src.contiguous(), ops.X3_PAIRS, sh.view(-1, 64))
+                w._dfu_shadow_x3_version = w._version
+            return sh
     if _X3_PAIRS:
         if w.shape[2] == 1 and w.shape[3] == 1:
             return ops.split_x3(w.detach().reshape(w.shape[0], -1), ops.X3_PAIRS)
@@ -683,11 +697,10 @@ class StemFn(torch.autograd.Function):
                      ldaux_out=Cout)
             del col_lo
             bns.forward_coeffs(stats)
-            af = _empty((M, Cout), F32, x.device)
-            ops.bn_apply_x3(y, bns.scale, bns.shift, None, 0, True, M, Cout, out_f32=af,
-                            y_lo=y_lo, relu_mask=a)
+            # bn1 + ReLU applied inside the pool, from the pair (no fp32 BN output stored)
+            out_lo, out, am, P2, Q2 = ops.maxpool_bn_fwd_x3(y, y_lo, bns.scale, bns.shift, B, P,
+                                                            Q, Cout, relu_mask=a)
             del y_lo
-            out_lo, out, am, P2, Q2 = ops.maxpool_fwd_x3(af, B, P, Q, Cout)
         else:
             ops.gemm(M, Cout, Kp, col, Kp, wb, Kp, y, Cout, epilogue=L.EPI_BF16_STATS,
                      stats=stats)

@@ -731,10 +731,15 @@ def ce_weighted_bwd(saved, grad_loss):
     return out
 
 
-def adamw_flat(p, g, m, v, lr, b1, b2, eps, wd, step_dev, shadow=None, shadow16=None):
+def adamw_flat(p, g, m, v, lr, b1, b2, eps, wd, step_dev, shadow=None, shadow16=None,
+               shadow_x3=None, x3_begin=0, x3_end=0):
+    """AdamW over the flat range p (dfu_adamw_flat); shadow_x3: the interleaved-pair split of
+    elements [x3_begin, x3_end) of the range (2 (x3_end - x3_begin) bf16)."""
+    if shadow_x3 is not None:
+        assert shadow_x3.numel() >= 2 * (x3_end - x3_begin) and shadow_x3.dtype == BF16
     check(lib().dfu_adamw_flat(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd,
-                               ptr(step_dev), ptr(shadow), ptr(shadow16), stream_ptr()),
-          "dfu_adamw_flat")
+                               ptr(step_dev), ptr(shadow), ptr(shadow16), ptr(shadow_x3),
+                               int(x3_begin), int(x3_end), stream_ptr()), "dfu_adamw_flat")
 
 
 def step_increment(step_dev):
@@ -781,6 +786,17 @@ def split_x3(x, pattern, seg=None, hi_out=None):
     check(lib().dfu_split_x3(ptr(x2), x2.stride(0), rows, cols, seg, ptr(out), int(pattern),
                              ptr(hi_out), seg if hi_out is None else hi_out.stride(0),
                              stream_ptr()), "dfu_split_x3")
+    return out
+
+
+def split_x3_into(x, pattern, out):
+    """split_x3 of fp32 [rows, seg] (contiguous rows, seg % 32 == 0 for pairs) into `out`."""
+    _req(x, F32, "split_x3_into")
+    rows, seg = x.shape
+    assert x.stride(1) == 1 and out.dtype == BF16 and out.is_contiguous()
+    assert out.shape == (rows, (2 if pattern == X3_PAIRS else 3) * seg)
+    check(lib().dfu_split_x3(ptr(x), x.stride(0), rows, seg, seg, ptr(out), int(pattern), None,
+                             seg, stream_ptr()), "dfu_split_x3")
     return out
 
 
@@ -842,6 +858,25 @@ def maxpool_fwd_x3(x, B, H, W, C):
     check(lib().dfu_maxpool_fwd_x3(ptr(x), B, H, W, C, ptr(lo), ptr(y), ptr(am), P, Q,
                                    stream_ptr()), "dfu_maxpool_fwd_x3")
     return lo, y, am, P, Q
+
+
+def maxpool_bn_fwd_x3(y, y_lo, scale, shift, B, H, W, C, relu_mask=None):
+    """bn + ReLU + maxpool 3x3/s2/p1 of the split pair (y, y_lo) [B*H*W, C] (dfu_maxpool_bn_fwd_x3)
+    -> (lo [B*P*Q, C], hi = plain bf16 [B, P, Q, C], argmax, P, Q); relu_mask (uint8
+    [B*H*W*C / 8]) receives the BN output's ReLU bitmask."""
+    _req(y, BF16, "maxpool_bn_fwd_x3")
+    _req(y_lo, BF16, "maxpool_bn_fwd_x3")
+    assert y.is_contiguous() and y_lo.is_contiguous() and y.numel() == B * H * W * C
+    assert relu_mask is None or relu_mask.numel() * 8 == y.numel()
+    P = (H - 1) // 2 + 1
+    Q = (W - 1) // 2 + 1
+    lo = torch.empty((B * P * Q, C), dtype=BF16, device=y.device)
+    out = torch.empty((B, P, Q, C), dtype=BF16, device=y.device)
+    am = torch.empty((B, P, Q, C), dtype=torch.uint8, device=y.device)
+    check(lib().dfu_maxpool_bn_fwd_x3(ptr(y), ptr(y_lo), ptr(scale), ptr(shift), B, H, W, C,
+                                      ptr(lo), ptr(out), ptr(am), ptr(relu_mask), P, Q,
+                                      stream_ptr()), "dfu_maxpool_bn_fwd_x3")
+    return lo, out, am, P, Q
 
 
 def avgpool_fwd_x3(hi, lo, B, HW, C):

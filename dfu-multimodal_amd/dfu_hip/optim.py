@@ -32,7 +32,9 @@ import torch.distributed as dist
 from . import functional as Fn
 from . import ops
 
-_ALIGN = 4  # elements (16 B) so every tensor view starts 16-byte aligned
+# elements: every tensor view starts 128-byte aligned, and a parameter's 32-element blocks are
+# the flat buffer's (the interleaved-pair x3 shadow's blocks, enable_x3)
+_ALIGN = 32
 
 
 def _dp_world():
@@ -48,6 +50,14 @@ def stores_krsc(p):
     """Whether FlatParams stores parameter p channels-last (KRSC): spatial conv weights whose
     channel count the implicit-GEMM conv takes (the stem's 3-channel 7x7 keeps OIHW)."""
     return p.dim() == 4 and p.shape[2] * p.shape[3] > 1 and p.shape[1] % 8 == 0
+
+
+def x3_pair_weight(p):
+    """Whether the bf16x3 ResNet forward reads conv weight p as interleaved pairs from the
+    optimizer's x3 shadow (FlatParams.enable_x3): a 1x1 conv weight, or a channels-last
+    spatial one, of C % 32 == 0 input channels (every ResNet-50 conv but the stem)."""
+    return p.dim() == 4 and p.shape[1] % 32 == 0 and (p.shape[2] * p.shape[3] == 1
+                                                        or stores_krsc(p))
 
 
 def _view(flat, o, p, krsc):
@@ -81,6 +91,8 @@ class FlatParams:
         self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=dev) if dev.type == "cuda" \
             else None
         self.shadow16 = None  # fp16 shadow, from the first fp16-stage forward on (enable_f16)
+        self.shadow_x3 = None  # interleaved-pair bf16x3 conv weights (enable_x3)
+        self.x3_lo = self.x3_hi = 0
         self.gen = 0         # bumped whenever every shadow is rewritten (step, refresh)
         self.t_params = []   # parameters with a transposed (p._dfu_shadow_T) or flipped
         self.t_pairs = []    # (p._dfu_shadow_F) shadow, and their (src, dst) transpose jobs
@@ -108,6 +120,8 @@ class FlatParams:
             p._dfu_shadow_version = p._version
         if self.shadow16 is not None:
             self._cast_f16()
+        if self.shadow_x3 is not None:
+            self._split_x3()
         self.shadows_rewritten()
 
     def _cast_f16(self):
@@ -125,6 +139,45 @@ class FlatParams:
         for p, o in zip(self.params, self.offsets):
             p._dfu_shadow16 = self.shadow16[o:o + p.numel()].view(p.shape[0], -1)
         self._cast_f16()
+
+    def enable_x3(self):
+        """Keep the interleaved-pair split (dfu_gemm_desc.x3_pairs B operand: per 32 elements
+        [hi 32 | lo 32]) of every conv weight x3_pair_weight accepts from now on: split once
+        here, then written by every AdamW step beside the bf16 shadow for the flat span those
+        weights occupy (4 B per element of it; the ResNet's 23.5M), so the bf16x3 forward
+        reads its conv weights as they are instead of ~52 per-layer split / pack launches on
+        its critical stream (functional.conv_weight_x3)."""
+        if self.shadow_x3 is not None or self.shadow is None:
+            return
+        idx = [i for i, p in enumerate(self.params) if x3_pair_weight(p)]
+        if not idx:
+            return
+        self.x3_lo = self.offsets[idx[0]]
+        self.x3_hi = self.offsets[idx[-1]] + _aligned(self.params[idx[-1]].numel())
+        self.shadow_x3 = torch.empty(2 * (self.x3_hi - self.x3_lo), dtype=torch.bfloat16,
+                                     device=self.data.device)
+        for i in idx:
+            p, o = self.params[i], self.offsets[i]
+            a = 2 * (o - self.x3_lo)
+            p._dfu_shadow_x3 = self.shadow_x3[a:a + 2 * p.numel()].view(p.shape[0], -1)
+        self._split_x3()
+
+    def _split_x3(self):
+        ops.split_x3_into(self.data[self.x3_lo:self.x3_hi].view(-1, 32), ops.X3_PAIRS,
+                          self.shadow_x3.view(-1, 64))
+        for p in self.params:
+            if getattr(p, "_dfu_shadow_x3", None) is not None:
+                p._dfu_shadow_x3_version = p._version
+
+    def x3_args(self, lo, hi):
+        """dfu_adamw_flat's shadow_x3 arguments for the AdamW range [lo, hi): (shadow view,
+        begin, end) relative to lo, or (None, 0, 0) when the range holds no x3 weights."""
+        if self.shadow_x3 is None:
+            return None, 0, 0
+        a, b = max(lo, self.x3_lo), min(hi, self.x3_hi)
+        if a >= b:
+            return None, 0, 0
+        return self.shadow_x3[2 * (a - self.x3_lo):], a - lo, b - lo
 
     def add_transposed(self, p):
         """Give parameter p a transposed bf16 shadow, kept current from now on."""
@@ -283,11 +336,13 @@ class FusedAdamW(torch.optim.Optimizer):
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         fp = self.flat
+        x3, x3b, x3e = fp.x3_args(lo, hi)
         ops.adamw_flat(fp.data[lo:hi], fp.grad[lo:hi], self.exp_avg[lo:hi],
                        self.exp_avg_sq[lo:hi], g["lr"], b1, b2, g["eps"], g["weight_decay"],
                        self.step_dev,
                        shadow=None if fp.shadow is None else fp.shadow[lo:hi],
-                       shadow16=None if fp.shadow16 is None else fp.shadow16[lo:hi])
+                       shadow16=None if fp.shadow16 is None else fp.shadow16[lo:hi],
+                       shadow_x3=x3, x3_begin=x3b, x3_end=x3e)
 
     @torch.no_grad()
     def step(self, closure=None):

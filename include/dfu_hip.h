@@ -435,10 +435,17 @@ int dfu_adamw(float* const* params, float* const* grads, float* const* exp_avg,
 /* Flat form: one contiguous buffer of n parameters (the fused flat-parameter layout).
  * shadow_bf16 (optional, n bf16): also receives bf16(updated param) — the GEMM operand copy
  * of every weight, so the forward pass needs no cast kernels; shadow_f16 (optional, n fp16):
- * fp16(updated param), the operands of the "parity" precision mode's fp16 ViT forward. */
+ * fp16(updated param), the operands of the "parity" precision mode's fp16 ViT forward;
+ * shadow_x3 (optional, bf16, 2 (x3_end - x3_begin) elements): elements [x3_begin, x3_end) of
+ * the range split into interleaved pairs, per 32-element block [hi 32 | lo 32] (hi =
+ * bf16(p), lo = bf16(p - hi)) -- for conv weights of C % 32 == 0 channels starting on a
+ * 32-element boundary, exactly the dfu_gemm_desc.x3_pairs B operand (dfu_split_x3 /
+ * dfu_pack_conv_weight_x3 pattern 2), so the bf16x3 ResNet forward needs no per-layer split
+ * launches.  x3_begin % 4 == 0, (x3_end - x3_begin) % 32 == 0, x3_end <= n rounded down to 4. */
 int dfu_adamw_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float lr, float beta1, float beta2, float eps, float weight_decay,
-                   const int64_t* step_dev, void* shadow_bf16, void* shadow_f16, void* stream);
+                   const int64_t* step_dev, void* shadow_bf16, void* shadow_f16, void* shadow_x3,
+                   int64_t x3_begin, int64_t x3_end, void* stream);
 int dfu_step_increment(int64_t* step_dev, void* stream);
 /* argmax over C for each row (torch.max(outputs, 1), :384) -> int64. */
 int dfu_argmax_rows(const float* x, int32_t rows, int32_t C, int64_t* out, void* stream);
@@ -495,6 +502,17 @@ int dfu_bn_apply_x3(const void* y, const void* y_lo, const float* scale, const f
 int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t W, int32_t C, void* y_lo,
                        void* y_bf16, uint8_t* argmax, int32_t P, int32_t Q, void* stream);
 /* AdaptiveAvgPool2d(1) on a split pair (hi, lo: [B*HW][C] bf16 each) -> fp32 [B][C]. */
+/* bn1 + ReLU + maxpool 3x3/s2/p1 of the bf16x3 stem in one pass (bitwise dfu_bn_apply_x3 with
+ * out_f32 then dfu_maxpool_fwd_x3, without the fp32 intermediate): the conv output split pair
+ * y / y_lo (bf16 NHWC [B*H*W][C] each), BN scale / shift (fp32 [C], 16-B aligned) -> pooled
+ * pair out_bf16 / out_lo [B*P*Q][C], argmax (uint8, window index) and optionally the BN
+ * backward's ReLU bitmask (bit k of byte i: element 8i + k > 0), each input element written
+ * once.  P = (H - 1) / 2 + 1, Q = (W - 1) / 2 + 1; C / 8 a power of two.  Replaces the
+ * torchvision stem's bn1 / relu / maxpool (resnet.py _forward_impl) in the parity mode. */
+int dfu_maxpool_bn_fwd_x3(const void* y, const void* y_lo, const float* scale, const float* shift,
+                          int32_t B, int32_t H, int32_t W, int32_t C, void* out_lo,
+                          void* out_bf16, uint8_t* argmax, uint8_t* relu_mask, int32_t P,
+                          int32_t Q, void* stream);
 int dfu_avgpool_fwd_x3(const void* hi, const void* lo, int32_t B, int32_t HW, int32_t C, float* y,
                        void* stream);
 /* timm LayerNorm -> triple [rows][3D] + plain bf16 [rows][D]; mean / rstd per row. */

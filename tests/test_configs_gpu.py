@@ -3,7 +3,7 @@ ViT-B/16, bs=64) on the MI355X path against the CPU oracle, plus the reference's
 (training.loop) with device-side metrics.
 
   * C2: ThermalOnlyModel (train_thermal_only.py:188-205) train step at B=64: the default
-    "parity" mode (every Block bf16x3 when the ViT classifies alone, models/vit.py) within the
+    "parity" mode (Blocks 0-8 bf16x3 when the ViT classifies alone, models/vit.py) within the
     5e-4 margin of the fp32 oracle, bf16x3 within north_star's 1e-3, the fp16-Block variant
     (what "parity" runs inside the fusion model) reported, bf16 within the bf16 oracle's band,
     and after one AdamW step (lr 1e-4, wd 1e-4) every parameter within one Adam step of the
@@ -108,14 +108,14 @@ def test_c2_thermal_only_train_step_b64():
         hip.load_state_dict(ref.state_dict(), strict=True)
         hip = hip.to(DEV)
         if precision == "fp16-blocks":  # the fusion model's ViT assignment, on this model
-            hip.backbone.classifier_parity_precision = "fp16"
+            hip.backbone.classifier_x3_blocks = 0
         opt = FusedAdamW(hip.parameters(), lr=1e-4, weight_decay=1e-4)
         mode = "parity" if precision == "fp16-blocks" else precision
         res[precision] = _hip_step(hip, th.to(DEV), y, w, mode, opt) + (hip,)
     out_p, loss_p = res["parity"][:2]
     d_p = _maxd(out_p, out_f32)
     d_16 = _maxd(res["fp16-blocks"][0], out_f32)
-    print(f"\n[C2 B={B}] parity (default; Blocks bf16x3) vs fp32 oracle {d_p:.3e} (bar 5e-4); "
+    print(f"\n[C2 B={B}] parity (default; Blocks 0-8 bf16x3, 9-11 fp16) vs fp32 oracle {d_p:.3e} (bar 5e-4); "
           f"fp16 Blocks {d_16:.3e}")
     assert d_p <= 5e-4 and abs(loss_p - loss_f32.item()) <= 5e-4
     out_x3, loss_x3, hip_x3 = res["bf16x3"]

@@ -140,11 +140,13 @@ def test_flat_params_layout():
     vals = [p.detach().clone() for p in ps]
     fp = FlatParams(ps)
     for p, v, o in zip(ps, vals, fp.offsets):
-        assert o % 4 == 0  # 16-byte aligned views for the vectorised kernels
+        # 128-byte aligned views: the vectorised kernels, and the x3 pair shadow's 32-element
+        # blocks coincide with every parameter's (FlatParams.enable_x3)
+        assert o % 32 == 0
         assert torch.equal(p.data, v)
         assert p.data.data_ptr() == fp.data.data_ptr() + 4 * o
         assert p.grad.data_ptr() == fp.grad.data_ptr() + 4 * o
-    assert fp.numel == 4 + 8 + 8 + 4
+    assert fp.numel == 4 * 32
 
 
 def test_flat_params_store_spatial_conv_weights_krsc():

@@ -94,3 +94,38 @@ def test_early_adamw_on_side_stream_is_bitwise_equal():
                     opt.step_dev.clone()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_x3_pair_shadow_tracks_conv_weights():
+    """The interleaved-pair bf16x3 shadow the AdamW kernel writes (FlatParams.enable_x3) equals
+    the per-layer split (dfu_split_x3 / dfu_pack_conv_weight_x3 pattern 2) of the updated conv
+    weights bitwise, for 1x1 and channels-last 3x3 weights, after steps and after an edit
+    outside the optimizer; the stem-like 3-channel weight is left out."""
+    from dfu_hip import functional as Fn
+    from dfu_hip import ops
+    from dfu_hip.optim import FusedAdamW
+    torch.manual_seed(7)
+    shapes = [(64, 3, 7, 7), (64,), (256, 64, 1, 1), (64, 64, 3, 3), (64,), (128, 256, 1, 1),
+              (128, 128, 3, 3), (7,)]
+    ps = [torch.nn.Parameter(torch.randn(s, device=DEV) * 0.05) for s in shapes]
+    opt = FusedAdamW(ps, lr=1e-3, weight_decay=1e-2)
+
+    def want(w):
+        if w.shape[2] * w.shape[3] == 1:
+            return ops.split_x3(w.detach().reshape(w.shape[0], -1), ops.X3_PAIRS)
+        return ops.pack_conv_weight_x3(w.detach().contiguous(), ops.X3_PAIRS).view(w.shape[0], -1)
+    convs = [p for p in ps if p.dim() == 4 and p.shape[1] % 32 == 0]
+    for w in convs:  # first use enables the shadow (one split)
+        assert torch.equal(Fn.conv_weight_x3(w), want(w))
+    assert opt.flat.shadow_x3 is not None and ps[0].__dict__.get("_dfu_shadow_x3") is None
+    g = torch.Generator(device="cpu").manual_seed(1)
+    for _ in range(3):
+        opt.zero_grad()
+        for p in ps:
+            p.grad.copy_(torch.randn(p.shape, generator=g).to(DEV))
+        opt.step()
+        for w in convs:
+            assert torch.equal(Fn.conv_weight_x3(w), want(w))
+    with torch.no_grad():  # an edit outside the optimizer bumps the version: re-split
+        convs[1].mul_(0.5)
+    assert torch.equal(Fn.conv_weight_x3(convs[1]), want(convs[1]))

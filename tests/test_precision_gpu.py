@@ -447,3 +447,27 @@ def test_attention_fwd_f32_matches_sdpa(N):
     assert torch.equal(qb, qkv.to(torch.bfloat16))  # the backward's bf16 qkv, written in passing
     lref = torch.logsumexp(s, -1).reshape(B * H, N)
     assert torch.allclose(lse[:, :N].double(), lref, rtol=2.0 ** -14, atol=1e-5)
+
+
+@pytest.mark.parametrize("H,W", [(112, 112), (15, 9)])
+def test_maxpool_bn_fused_x3_equals_apply_then_pool(H, W):
+    """The stem's fused bn1 + ReLU + maxpool over the conv output pair (dfu_maxpool_bn_fwd_x3)
+    is bitwise dfu_bn_apply_x3 (fp32 out, ReLU bitmask) followed by dfu_maxpool_fwd_x3: pooled
+    pair, argmax and the bitmask (each element written once, odd sizes included)."""
+    L, ops = _ops()
+    torch.manual_seed(6)
+    B, C = 2, 64
+    M = B * H * W
+    yf = torch.randn(M, C, device=DEV)
+    hi, lo = _pair(yf)
+    sc = torch.rand(C, device=DEV) + 0.5
+    sh = torch.randn(C, device=DEV) * 0.5
+    af = torch.empty(M, C, device=DEV)
+    mask_ref = torch.empty(M * C // 8, dtype=torch.uint8, device=DEV)
+    ops.bn_apply_x3(hi, sc, sh, None, 0, True, M, C, out_f32=af, y_lo=lo, relu_mask=mask_ref)
+    lo_r, out_r, am_r, P, Q = ops.maxpool_fwd_x3(af, B, H, W, C)
+    mask = torch.full((M * C // 8,), 0xAA, dtype=torch.uint8, device=DEV)
+    lo_f, out_f, am_f, P2, Q2 = ops.maxpool_bn_fwd_x3(hi, lo, sc, sh, B, H, W, C, relu_mask=mask)
+    assert (P, Q) == (P2, Q2)
+    assert torch.equal(out_f, out_r) and torch.equal(lo_f, lo_r) and torch.equal(am_f, am_r)
+    assert torch.equal(mask, mask_ref)

@@ -1,18 +1,15 @@
 #!/bin/bash
-# Quick GEMM iteration pass: bitwise schedule tests + kernel tests, ablations, per-GEMM step profile.
+# One build-measure iteration on the GPU box: the named GPU tests, smoke, then the default bench
+# line (C3, library-default precision).  bash tools/gpu_iter.sh <tag> "<pytest -k expr or files>"
 set -o pipefail
-R=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$R/gpurun_out
-mkdir -p $OUT
-cd $R
-timeout -k 10 600 python -u -m pytest -q --maxfail=10 --timeout 120 --timeout-method thread tests/test_gemm_persistent_gpu.py tests/test_kernels_gpu.py > $OUT/t_iter.log 2>&1
-rc=$?; tail -4 $OUT/t_iter.log
-if [ $rc -gt 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
-for c in ${CASES:-qkv_fwd:5 fc2_fwd:5 l1c3_fwd:5}; do
-  case_=${c%:*}; tile=${c#*:}
-  for d in 0 1; do
-    echo -n "dbg=$d "; DFU_GEMM_DEBUG=$d timeout -k 10 60 python tools/gemm_one.py $case_ --tile $tile --iters 30 2>&1 | grep -v amdgpu.ids || exit 1
-  done
-done
-timeout -k 10 300 python tools/gemm_step_profile.py > $OUT/gemm_step_${TAG:-b}.log 2>&1 || { echo "profile rc=$?"; exit 1; }
-head -${HEADN:-30} $OUT/gemm_step_${TAG:-b}.log
+R=${GRAFT_REPO_ROOT:-/root/repo}; OUT=$R/gpurun_out; TAG=${1:-it}; mkdir -p $OUT; cd $R
+if [ -n "$2" ]; then
+  timeout -k 10 600 python -u -m pytest -x -q -s --timeout 300 --timeout-method thread $2 > $OUT/t_$TAG.log 2>&1 || { echo "tests rc=$?"; tail -40 $OUT/t_$TAG.log; exit 1; }
+  tail -3 $OUT/t_$TAG.log
+fi
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { echo "smoke rc=$?"; tail -20 $OUT/smoke_$TAG.log; exit 1; }
+tail -3 $OUT/smoke_$TAG.log
+timeout -k 10 600 python bench.py ${BENCH_ARGS:---no-cpu-baseline} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { echo "bench rc=$?"; tail -20 $OUT/bench_$TAG.err; exit 1; }
+python -c "
+import json; d=json.load(open('$OUT/bench_$TAG.json'))
+print('value', d['value'], 'ms', d['ms_per_step'], 'gpu median', d['gpu_step_ms']['median'], 'modes', {k: v['value'] for k, v in d['precision_modes'].items()}, 'parity', {k: v['max_abs_logits_vs_fp32_oracle'] for k, v in (d['parity'] or {}).items() if isinstance(v, dict)}, 'gemm', d['roofline']['achieved'], d['roofline']['avg_launch_us'])"
