@@ -35,6 +35,34 @@ def main():
     rgb, th, y = bench.synthetic(64, dev, seed=42)
     names = []
     evs, hs = [], []
+    # per-encoder end-of-backward events (recorded on the stream each backward runs on)
+    ends = {}
+
+    def wrap(fn_cls, key):
+        orig = fn_cls.backward
+
+        def bwd(ctx, *g):
+            r = orig(ctx, *g)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ends.setdefault(key, []).append(e)
+            return r
+        fn_cls.backward = staticmethod(bwd)
+    wrap(Fn.StemFn, "resnet backward end")
+    wrap(Fn.PatchEmbedFn, "vit backward end")
+
+    def wrapf(fn_cls, key):
+        orig = fn_cls.forward
+
+        def fwd_(ctx, *a_):
+            r = orig(ctx, *a_)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ends.setdefault(key, []).append(e)
+            return r
+        fn_cls.forward = staticmethod(fwd_)
+    wrapf(Fn.AvgPoolFn, "resnet forward end")
+    wrapf(Fn.TokenNormFn, "vit forward end")
 
     def mark(name):
         e = torch.cuda.Event(enable_timing=True)
@@ -59,6 +87,7 @@ def main():
         step()
     torch.cuda.synchronize()
     names.clear(), evs.clear(), hs.clear()
+    ends.clear()
     mark("start")
     for _ in range(a.steps):
         step()
@@ -69,6 +98,12 @@ def main():
         g = evs[0].elapsed_time(evs[i])
         h = (hs[i] - h0) * 1e3
         print(f"{n:>20s} {h:9.2f} {g:10.2f} {g - h:19.2f}")
+    for key, es in ends.items():
+        es = es[-a.steps:]
+        ts = [evs[0].elapsed_time(e) for e in es]
+        print(f"{key:>20s} (device ms): " + " ".join(f"{t:.2f}" for t in ts))
+    bw = [evs[0].elapsed_time(evs[i]) for i, n in enumerate(names) if n == "backward enqueued"]
+    print("backward joined (device ms): " + " ".join(f"{t:.2f}" for t in bw))
     k = len(names) - 1
     print(f"per step: host {(hs[k] - h0) * 1e3 / a.steps:.2f} ms, device "
           f"{evs[0].elapsed_time(evs[k]) / a.steps:.2f} ms")
