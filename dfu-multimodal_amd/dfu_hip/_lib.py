@@ -150,6 +150,8 @@ PROTOTYPES = {
     "dfu_metrics_accumulate": [P, P, I32, I32, P, P, P, P, P],
     "dfu_split_x3": [P, I64, I32, I32, I32, P, I32, P, I64, P],
     "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, I32, P],
+    "dfu_stem_conv_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, P, I32, I32, I32, I32, I32,
+                         P, P, P, P, P],
     "dfu_maxpool_bn_fwd_x3": [P, P, P, P, I32, I32, I32, I32, P, P, P, P, I32, I32, P],
     "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P],
     "dfu_patchify_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],

@@ -659,6 +659,9 @@ def _geom(conv, B, H, W):
 
 
 # ------------------------------------------------------------------------------- stem
+_STEM_FUSED = os.environ.get("DFU_STEM_FUSED", "1") != "0"
+
+
 class StemFn(torch.autograd.Function):
     """conv1 7x7/s2/p3 (3->64, explicit bf16 im2col, K padded 147->160) + bn1 + relu +
     maxpool 3x3/s2/p1.  Input fp32 (B,3,H,W) any strides; output bf16 channels_last."""
@@ -676,26 +679,33 @@ class StemFn(torch.autograd.Function):
         wb = weight_bf16_rows(w, ld=Kp)
         Cout = w.shape[0]
         x3 = _x3(mod)
-        if x3:
+        # bf16x3: one implicit-GEMM kernel (dfu_stem_conv_x3: no pair im2col in HBM) where its
+        # geometry allows; DFU_STEM_FUSED=0: the pair im2col + interleaved-pair GEMM (A/B)
+        fused = x3 and _STEM_FUSED and Kp == 160 and ops.stem_conv_x3_ok(xf, w, st, pad)
+        if fused:
+            y, y_lo, stats, col, P, Q = ops.stem_conv_x3(xf, w.detach(), st, pad)
+        elif x3:
             (col, col_lo), P, Q = ops.im2col_f32_x3(xf, R, S, st, pad, Kp)  # split pair
         else:
             col, P, Q = ops.im2col_f32(xf, R, S, st, pad, Kp)
         M = B * P * Q
-        y = _empty((M, Cout), BF16, x.device)
-        stats = _empty((ops.stats_tiles(M), 2, Cout), F32, x.device)
+        if not fused:
+            y = _empty((M, Cout), BF16, x.device)
+            stats = _empty((ops.stats_tiles(M), 2, Cout), F32, x.device)
         bns = _BN(bn, M, Cout, x.device)
         if x3:
             a = _empty((M * Cout // 8,), torch.uint8, x.device)  # bn1's ReLU bitmask
-            y_lo = _empty((M, Cout), BF16, x.device)  # the conv output as a split pair (y, y_lo)
-            if _X3_PAIRS and Kp % 32 == 0:  # interleaved pairs (conv_weight_x3)
-                w3, K3, pairs = ops.split_x3(w.detach().reshape(Cout, -1), ops.X3_PAIRS,
-                                             seg=Kp), 2 * Kp, True
-            else:
-                w3, K3, pairs = weight_x3_rows(w, seg=Kp), 3 * Kp, False
-            ops.gemm(M, Cout, K3, col, Kp, w3, K3, y, Cout, epilogue=L.EPI_F32_STATS,
-                     stats=stats, x3=True, a_lo=col_lo, x3_pairs=pairs, aux_out=y_lo,
-                     ldaux_out=Cout)
-            del col_lo
+            if not fused:
+                y_lo = _empty((M, Cout), BF16, x.device)  # the conv output as a split pair
+                if _X3_PAIRS and Kp % 32 == 0:  # interleaved pairs (conv_weight_x3)
+                    w3, K3, pairs = ops.split_x3(w.detach().reshape(Cout, -1), ops.X3_PAIRS,
+                                                 seg=Kp), 2 * Kp, True
+                else:
+                    w3, K3, pairs = weight_x3_rows(w, seg=Kp), 3 * Kp, False
+                ops.gemm(M, Cout, K3, col, Kp, w3, K3, y, Cout, epilogue=L.EPI_F32_STATS,
+                         stats=stats, x3=True, a_lo=col_lo, x3_pairs=pairs, aux_out=y_lo,
+                         ldaux_out=Cout)
+                del col_lo
             bns.forward_coeffs(stats)
             # bn1 + ReLU applied inside the pool, from the pair (no fp32 BN output stored)
             out_lo, out, am, P2, Q2 = ops.maxpool_bn_fwd_x3(y, y_lo, bns.scale, bns.shift, B, P,

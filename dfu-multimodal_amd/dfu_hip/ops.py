@@ -860,6 +860,39 @@ def maxpool_fwd_x3(x, B, H, W, C):
     return lo, y, am, P, Q
 
 
+def stem_conv_x3(x, w, stride=2, pad=3, want_col=True):
+    """bf16x3 stem conv (dfu_stem_conv_x3): x fp32 (B, 3, H, W) any strides, w fp32 OIHW
+    (64, 3, 7, 7) -> (y, y_lo [M, 64] bf16 split pair, stats [M / 128, 2, 64], col [M, 160] bf16
+    hi im2col rows or None, P, Q)."""
+    _req(x, F32, "stem_conv_x3")
+    _req(w, F32, "stem_conv_x3")
+    B, C, H, W = x.shape
+    K, Cw, R, S = w.shape
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - S) // stride + 1
+    M = B * P * Q
+    y = torch.empty((M, K), dtype=BF16, device=x.device)
+    y_lo = torch.empty((M, K), dtype=BF16, device=x.device)
+    stats = torch.empty((max(1, M // 128), 2, K), dtype=F32, device=x.device)
+    col = torch.empty((M, 160), dtype=BF16, device=x.device) if want_col else None
+    sn, sc, sh, sw = x.stride()
+    check(lib().dfu_stem_conv_x3(ptr(x), sn, sc, sh, sw, B, C, H, W, ptr(w.contiguous()), K, R,
+                                 S, stride, pad, ptr(y), ptr(y_lo), ptr(stats), ptr(col),
+                                 stream_ptr()), "dfu_stem_conv_x3")
+    return y, y_lo, stats, col, P, Q
+
+
+def stem_conv_x3_ok(x, w, stride, pad):
+    """Whether dfu_stem_conv_x3 takes this stem (its geometry checks, host side)."""
+    B, C, H, W = x.shape
+    K, _, R, S = w.shape
+    if (C, K, R, S, stride, pad) != (3, 64, 7, 7, 2, 3) or H < 7 or W < 7 or W > 250:
+        return False
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W + 2 * pad - S) // stride + 1
+    return (P * Q) % 128 == 0 and Q >= 64 and B * P * Q < (1 << 31)
+
+
 def maxpool_bn_fwd_x3(y, y_lo, scale, shift, B, H, W, C, relu_mask=None):
     """bn + ReLU + maxpool 3x3/s2/p1 of the split pair (y, y_lo) [B*H*W, C] (dfu_maxpool_bn_fwd_x3)
     -> (lo [B*P*Q, C], hi = plain bf16 [B, P, Q, C], argmax, P, Q); relu_mask (uint8

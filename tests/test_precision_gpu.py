@@ -471,3 +471,39 @@ def test_maxpool_bn_fused_x3_equals_apply_then_pool(H, W):
     assert (P, Q) == (P2, Q2)
     assert torch.equal(out_f, out_r) and torch.equal(lo_f, lo_r) and torch.equal(am_f, am_r)
     assert torch.equal(mask, mask_ref)
+
+
+@pytest.mark.parametrize("contig", [True, False])
+def test_stem_conv_x3_fused_equals_pair_im2col_gemm(contig):
+    """The fused stem conv (dfu_stem_conv_x3: input rows staged in LDS, A fragments split in
+    registers) against the explicit path it replaces (pair im2col + interleaved-pair GEMM with
+    the F32_STATS epilogue): the conv output pair and the hi im2col rows bitwise, the BN tile
+    statistics to fp32 summation order; and the pair within split-bf16 accuracy of an fp64
+    convolution."""
+    L, ops = _ops()
+    torch.manual_seed(8)
+    B, H, W = 2, 224, 224
+    xs = torch.randn(B, 3, H, W + (0 if contig else 5), device=DEV)
+    x = xs[..., :W] if not contig else xs
+    w = torch.randn(64, 3, 7, 7, device=DEV) * 0.05
+    assert ops.stem_conv_x3_ok(x, w, 2, 3)
+    y, ylo, st, col, P, Q = ops.stem_conv_x3(x, w)
+    M = B * P * Q
+    (chi, clo), P2, Q2 = ops.im2col_f32_x3(x, 7, 7, 2, 3, 160)
+    w3 = ops.split_x3(w.reshape(64, -1), ops.X3_PAIRS, seg=160)
+    y2 = torch.empty(M, 64, dtype=torch.bfloat16, device=DEV)
+    y2lo = torch.empty_like(y2)
+    st2 = torch.empty(M // 128, 2, 64, device=DEV)
+    ops.gemm(M, 64, 320, chi, 160, w3, 320, y2, 64, epilogue=L.EPI_F32_STATS, stats=st2,
+             x3=True, a_lo=clo, x3_pairs=True, aux_out=y2lo, ldaux_out=64)
+    assert (P, Q) == (P2, Q2) == (112, 112)
+    assert torch.equal(col, chi)
+    assert torch.equal(y, y2) and torch.equal(ylo, y2lo)
+    torch.testing.assert_close(st[:, 0], st2[:, 0], rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(st[:, 1], st2[:, 1], rtol=1e-4, atol=1e-3)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), stride=2, padding=3)
+    ref = ref.permute(0, 2, 3, 1).reshape(M, 64)
+    v = y.double() + ylo.double()
+    err = ((v - ref).abs().max() / ref.abs().max()).item()
+    print(f"\n[stem x3 fused] rel err vs fp64 conv {err:.2e}")
+    assert err < 2e-5
