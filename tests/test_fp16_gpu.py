@@ -170,25 +170,28 @@ def test_adamw_keeps_the_fp16_shadow_current():
     assert torch.equal(Fn.weight_f16_rows(lin.weight), lin.weight.detach().to(F16))
 
 
-@pytest.mark.parametrize("gain", [1.0, 8.0, 32.0])
-def test_fp16_vit_forward_finite_at_trained_weight_scales(gain):
-    """the parity mode's fp16 ViT forward saturates to inf above 65504, and the
-    per-stage study that chose it used random-init weights only.  Pretrained ViT-B
-    weights have LayerNorm gains and activations well above the random init's (outlier
-    channels of tens); scaled here by `gain` in every LayerNorm weight and the patch
-    embedding, the fp16 fusion-feature forward must stay finite and within fp16's own error
-    of the bf16x3 forward of the same model."""
+@pytest.mark.parametrize("gain", [1.0, 16.0, 128.0])
+def test_fp16_vit_forward_range_at_trained_weight_scales(gain):
+    """the parity mode's fp16 ViT forward saturates above 65504 (and loses bits
+    below 6.1e-5), and the per-stage study that chose it used random-init weights only (DESIGN
+    §4).  Trained ViT-B LayerNorm gains and activations sit well above the random init's; here
+    every LayerNorm's weight and bias are scaled by `gain` and the qkv / fc1 weights that read
+    its output by 1 / gain -- the same function, with the fp16 LayerNorm outputs `gain` times
+    larger (up to ~1e3) and the fp16 weights `gain` times smaller (down to ~1e-4).  The fp16
+    fusion-feature forward must stay finite and within fp16's own error of the bf16x3 forward.
+    (Scaling the gains alone makes the random-init attention chaotic: every precision then
+    diverges from every other, so that is not a range test.)"""
     from dfu_hip import functional as Fn
     from models.vit import VisionTransformer
     from oracle import torch_ref as R
     torch.manual_seed(2)
     v = VisionTransformer(num_classes=0).to(DEV).train()
     with torch.no_grad():
-        for name, p in v.named_parameters():
-            if name.endswith("norm1.weight") or name.endswith("norm2.weight"):
-                p.mul_(gain)
-            if name.startswith("patch_embed"):
-                p.mul_(gain)
+        for blk in v.blocks:
+            for ln, lin in ((blk.norm1, blk.attn.qkv), (blk.norm2, blk.mlp.fc1)):
+                ln.weight.mul_(gain)
+                ln.bias.add_(0.01).mul_(gain)  # (nonzero biases: timm's are, once trained)
+                lin.weight.div_(gain)
     _, th, _ = R.synthetic_batch(8, seed=3)
     th = th.to(DEV)
     with torch.no_grad():
@@ -198,6 +201,6 @@ def test_fp16_vit_forward_finite_at_trained_weight_scales(gain):
             f32 = v(th).float()
     assert torch.isfinite(f16).all(), f"fp16 forward overflowed at gain {gain}"
     rel = ((f16 - f32).norm() / f32.norm()).item()
-    print(f"\n[fp16 ViT, LN / patch gain {gain}] features rel err vs bf16x3 {rel:.2e}; max |x| "
-          f"{f32.abs().max().item():.1f}")
+    print(f"\n[fp16 ViT, LayerNorm x {gain}, qkv / fc1 weights / {gain}] features rel err vs "
+          f"bf16x3 {rel:.2e}")
     assert rel < 5e-3
