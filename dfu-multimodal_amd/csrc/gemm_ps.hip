@@ -22,7 +22,10 @@ namespace {
 
 // Timing ablations (tools/build_ablate.sh builds a separate library with -DDFU_PS_ABLATE=mask;
 // the product build is 0): 1 no epilogue, 2 no MFMA, 4 no DMA, 8 no fragment reads (zero
-// fragments), 16 no K-step barrier, 32 epilogue accesses out of range (issued, no traffic).  Results are wrong in every ablated build.
+// fragments), 16 no K-step barrier, 32 epilogue accesses out of range (issued, no traffic),
+// 64 / 128 no B DMA / no B fragment reads, 256 / 512 the same for A.  The DMA and read
+// ablations keep the first K-step's (random) data in LDS / in the fragments: MFMAs on zero
+// operands would run at a higher clock (MI355X_MICROARCH.md, DVFS give-back).  Results are wrong in every ablated build.
 #ifndef DFU_PS_ABLATE
 #define DFU_PS_ABLATE 0
 #endif
@@ -378,10 +381,10 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
                                                         p.b_bytes, 0x00020000);
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto issue_a = [&](int k0_, int h, char* img) {
-    if constexpr (!(kAbl & 4)) ps_issue<AK_, TMt / 64>(sa, ra_, p.lda, k0_, p.K, h, img, tid, wave_u);
+    ps_issue<AK_, TMt / 64>(sa, ra_, p.lda, k0_, p.K, h, img, tid, wave_u);
   };
   auto issue_b = [&](int k0_, int h, char* img) {
-    if constexpr (!(kAbl & 4)) ps_issue<BK_>(sb, rb_, p.ldb, k0_, p.K, h, img, tid, wave_u);
+    ps_issue<BK_>(sb, rb_, p.ldb, k0_, p.K, h, img, tid, wave_u);
   };
 
   // issue cursor (the K-step whose DMA goes out next) and compute cursor
@@ -414,8 +417,16 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     issue_b(k0, 0, smem + PS_IMG);
     issue_b(k0, 1, smem + PS_IMG);
     issue_a(k0, 1, smem);
+    if constexpr ((kAbl & (4 | 64 | 256)) != 0) {  // ablated DMA: both buffers hold K-step 0
+      issue_a(k0, 0, smem + PS_BUF);
+      issue_b(k0, 0, smem + PS_BUF + PS_IMG);
+      issue_b(k0, 1, smem + PS_BUF + PS_IMG);
+      issue_a(k0, 1, smem + PS_BUF);
+    }
     advance_issue();
   }
+  constexpr bool kDmaA = (kAbl & (4 | 256)) == 0, kDmaB = (kAbl & (4 | 64)) == 0;
+  bool rd_on = true;  // read ablations: fragments read in K-step 0 only
   const int E = (kAbl & 1) ? 0 : ps_epi_stores<EPI, FMH>(p);
   bool epi_last = false;  // an epilogue ran at the end of the previous K-step
   // Fragment registers hold one A half (fa) and one B half (fb); each phase's MFMAs run one
@@ -427,21 +438,20 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   // (Measured and dropped, round 3: both B halves kept in registers, the next K-step's barrier
   // moved in front of the last MFMA group, the DMA spread over all four groups, the two wave rows
   // issuing their DMA at different points, s_setprio around the groups, per-XCD runs for the
-  // partial round -- all within noise.)
+  // partial round -- all within noise.  Round 5: the operand tiles through VGPRs
+  // (buffer_load_dwordx4, then ds_write_b128 two phases later, same LDS images) instead of
+  // LDS-DMA: 10-13 % slower on 4096^3 and the ViT shapes, same box.)
   bf16x8 fa[FMH][2], fb[2][2];
-  if constexpr ((kAbl & 8) != 0) {
-#pragma unroll
-    for (int i = 0; i < FMH; ++i) fa[i][0] = fa[i][1] = (bf16x8){};
-    fb[0][0] = fb[0][1] = fb[1][0] = fb[1][1] = (bf16x8){};
-  }
   auto rd_a = [&](const char* la, int h, int ks) {
-    if constexpr ((kAbl & 8) != 0) return;
+    if constexpr ((kAbl & (8 | 512)) != 0)
+      if (!rd_on) return;
 #pragma unroll
     for (int i = 0; i < FMH; ++i)
       fa[i][ks] = read_frag<AK_>(la, h * TMH + wr * (TMH / 2) + i * 16, ks, lane);
   };
   auto rd_b = [&](const char* lb, int h, int ks) {
-    if constexpr ((kAbl & 8) != 0) return;
+    if constexpr ((kAbl & (8 | 128)) != 0)
+      if (!rd_on) return;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       fb[j][ks] = read_frag<BK_>(lb, h * 128 + wc * 32 + j * 16, ks, lane);
@@ -491,10 +501,11 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     else
       wait_vmcnt<0>();
     if constexpr (!(kAbl & 16)) __builtin_amdgcn_s_barrier();
+    if constexpr ((kAbl & (8 | 128 | 512)) != 0) rd_on = g == 0;
     rd_first(la);
     if (nxt) {
-      issue_a(k1, 0, na);
-      issue_b(k1, 0, nb);
+      if (kDmaA) issue_a(k1, 0, na);
+      if (kDmaB) issue_b(k1, 0, nb);
     }
     __builtin_amdgcn_sched_barrier(0);
     mf(0, 0, 0);   // A-top x B-left
@@ -502,8 +513,8 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
     mf(0, 0, 1);
     rd_b(lb, 1, 1);
     if (nxt) {
-      issue_b(k1, 1, nb);
-      issue_a(k1, 1, na);
+      if (kDmaB) issue_b(k1, 1, nb);
+      if (kDmaA) issue_a(k1, 1, na);
       advance_issue();
     }
     __builtin_amdgcn_sched_barrier(0);
