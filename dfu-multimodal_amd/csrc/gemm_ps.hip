@@ -440,7 +440,10 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   // issuing their DMA at different points, s_setprio around the groups, per-XCD runs for the
   // partial round -- all within noise.  Round 5: the operand tiles through VGPRs
   // (buffer_load_dwordx4, then ds_write_b128 two phases later, same LDS images) instead of
-  // LDS-DMA: 10-13 % slower on 4096^3 and the ViT shapes, same box.)
+  // LDS-DMA: 10-13 % slower on 4096^3 and the ViT shapes, same box.  And the ping-pong schedule
+  // of cdna_hip_programming.md's 256^2 template on this tile (wave row 1 one barrier behind row
+  // 0, two barriers per quadrant phase, MFMAs at priority 1, both B halves in registers, one
+  // half-tile of DMA per phase): level at 4096^3 and fc2, 4-7 % slower at K = 768.)
   bf16x8 fa[FMH][2], fb[2][2];
   auto rd_a = [&](const char* la, int h, int ks) {
     if constexpr ((kAbl & (8 | 512)) != 0)

@@ -6,10 +6,11 @@ import csv
 import re
 import sys
 
+STEP_MARK = re.compile(r"k_im2col_lds|k_stem_conv_x3")  # the stem: one launch per step
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 top = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 50
 by_q = "--queues" in sys.argv
-idx = [i for i, r in enumerate(rows) if "k_im2col_lds" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if STEP_MARK.search(r["Kernel_Name"])]
 steps = list(zip(idx[2:-1], idx[3:]))
 agg, cnt = collections.defaultdict(float), collections.defaultdict(int)
 for a, b in steps:

@@ -3,11 +3,13 @@ per phase (forward, head, backward, optimizer tail), the time with no kernel run
 only kernels of < 64 workgroups running (latency-bound: a few CUs busy), and the histogram of
 idle gaps.  Usage: python tools/trace_fill.py <kernel_trace.csv> [step index]"""
 import csv
+import re
 import sys
 
+STEP_MARK = re.compile(r"k_im2col_lds|k_stem_conv_x3")  # the stem: one launch per step
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 si = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-idx = [i for i, r in enumerate(rows) if "k_im2col_lds" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if STEP_MARK.search(r["Kernel_Name"])]
 seg = rows[idx[si]:idx[si + 1]]
 t0 = int(seg[0]["Start_Timestamp"])
 ev = []

@@ -2,12 +2,14 @@
 launch) in which no kernel runs on any queue, with the kernels on each side.
 Usage: python tools/trace_gaps.py <kernel_trace.csv> [step index] [min gap us]"""
 import csv
+import re
 import sys
 
+STEP_MARK = re.compile(r"k_im2col_lds|k_stem_conv_x3")  # the stem: one launch per step
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 si = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 mg = float(sys.argv[3]) if len(sys.argv) > 3 else 20.0
-idx = [i for i, r in enumerate(rows) if "k_im2col_lds" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if STEP_MARK.search(r["Kernel_Name"])]
 seg = rows[idx[si]:idx[si + 1]]
 t0 = int(seg[0]["Start_Timestamp"])
 end, last = int(seg[0]["End_Timestamp"]), seg[0]

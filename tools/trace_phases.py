@@ -4,10 +4,12 @@ before the head's first launch), when the head starts and ends (k_ce_bwd), when 
 backward ends and when AdamW starts.  Times in us from the step's first launch.
 Usage: python tools/trace_phases.py <kernel_trace.csv>"""
 import csv
+import re
 import sys
 
+STEP_MARK = re.compile(r"k_im2col_lds|k_stem_conv_x3")  # the stem: one launch per step
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_im2col_lds" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if STEP_MARK.search(r["Kernel_Name"])]
 for a, b in zip(idx, idx[1:]):
     seg = rows[a:b]
     t0 = int(seg[0]["Start_Timestamp"])

@@ -4,12 +4,14 @@ what the critical stream of that phase spends its time on.
 Usage: python tools/trace_stream_mix.py <kernel_trace.csv> [step index] [forward|backward]"""
 import collections
 import csv
+import re
 import sys
 
+STEP_MARK = re.compile(r"k_im2col_lds|k_stem_conv_x3")  # the stem: one launch per step
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 si = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 phase = sys.argv[3] if len(sys.argv) > 3 else "forward"
-idx = [i for i, r in enumerate(rows) if "k_im2col_lds" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if STEP_MARK.search(r["Kernel_Name"])]
 seg = rows[idx[si]:idx[si + 1]]
 t0 = int(seg[0]["Start_Timestamp"])
 pool = min(int(r["End_Timestamp"]) for r in seg if "k_avgpool_fwd" in r["Kernel_Name"])

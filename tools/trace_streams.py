@@ -7,7 +7,7 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-mark = sys.argv[2] if len(sys.argv) > 2 else "k_im2col_lds"
+mark = sys.argv[2] if len(sys.argv) > 2 else "k_stem_conv_x3"
 idx = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
 
 
