@@ -4,7 +4,8 @@
   cases: fc1_fwd (12608x3072x768, KM x KM, BF16), fc1_gelu (same, GELU epilogue),
          fc2_dgrad (12608x3072x768, KM x MN, DGELU), fc1_wgrad (3072x768x12608, MN x MN, F32_ACC),
          l1c3_fwd (200704x256x64 1x1 conv, STATS), fc2_fwd_resid (12608x768x3072, F32_RESID),
-         fc2_wgrad / qkv_wgrad / proj_wgrad (768x3072 / 2304x768 / 768x768 x 12608, F32_ACC)
+         fc2_wgrad / qkv_wgrad / proj_wgrad (768x3072 / 2304x768 / 768x768 x 12608, F32_ACC),
+         l1c3x3_fwd / l1c1x3_fwd / l3c2x3_fwd (bf16x3 pair convs; FLOPs: the MFMA work, 3 products)
 """
 import argparse
 import os
@@ -104,6 +105,28 @@ def build(case, tile):
         return 2 * M * N * K, lambda: ops.gemm(M, N, K, A, M, B, N, C, N, a_mode=L.OPND_MNMAJOR,
                                                b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC,
                                                tile=tile)
+    if case in ("l1c3x3_fwd", "l1c1x3_fwd", "l3c2x3_fwd"):
+        # the parity mode's bf16x3 ResNet convs on interleaved hi/lo pairs (functional.conv_fwd_x3):
+        # layer-1 conv3 (1x1, 64 -> 256) and conv1 (1x1, 256 -> 64), layer-3 conv2 (3x3, 256)
+        n, h, w, c, k, r = {"l1c3x3_fwd": (64, 56, 56, 64, 256, 1),
+                            "l1c1x3_fwd": (64, 56, 56, 256, 64, 1),
+                            "l3c2x3_fwd": (64, 14, 14, 256, 256, 3)}[case]
+        M = n * h * w
+        hi, lo = T(M, c), T(M, c)
+        w3 = T(k, r * r * 2 * c)
+        y, y_lo = T(M, k), T(M, k)
+        st = torch.empty(ops.stats_tiles(M), 2, k, device="cuda")
+        xk = dict(x3=True, a_lo=lo, x3_pairs=True, aux_out=y_lo, ldaux_out=k)
+        if r == 1:
+            return 2 * M * k * c * 3, lambda: ops.gemm(M, k, 2 * c, hi, c, w3, 2 * c, y, k,
+                                                       epilogue=L.EPI_F32_STATS, stats=st,
+                                                       tile=tile, **xk)
+        g3 = ops.ConvGeom(n, h, w, 2 * c, k, r, r, 1, 1)
+        K3 = r * r * 2 * c
+        return 2 * M * k * r * r * c * 3, lambda: ops.gemm(M, k, K3, hi, 0, w3, K3, y, k,
+                                                           a_mode=L.OPND_CONV_FWD,
+                                                           epilogue=L.EPI_F32_STATS, stats=st,
+                                                           conv=g3, tile=tile, **xk)
     if case == "l1c3_fwd":
         M, N, K = 200704, 256, 64
         A, B, C = T(M, K), T(N, K), T(M, N)
