@@ -6,6 +6,7 @@ keeping the fastest.  The generated table is compiled into libdfu_hip.so and tak
 over the analytic cost model (csrc/gemm.hip), so plans are deterministic (no runtime tuning).
 
   python tools/gemm_tune.py [--batch 64] [--config fusion] [--out PATH] [--iters 10]
+      [--only-wgrad --all-splits]  (the weight gradients over every split 1..32 too)
 """
 import argparse
 import ctypes
@@ -80,6 +81,11 @@ def main():
                     help="tune only the interleaved-pair bf16x3 GEMMs (dfu_gemm_desc.x3_pairs)")
     ap.add_argument("--only-f16", action="store_true",
                     help="tune only the fp16-operand GEMMs (dfu_gemm_desc.operand_type 1)")
+    ap.add_argument("--only-wgrad", action="store_true",
+                    help="tune only the split-K weight gradients (epilogue F32_ACC)")
+    ap.add_argument("--all-splits", action="store_true",
+                    help="weight gradients: every split 1..32 besides SPLITS (splits that fill the "
+                         "CUs exactly, e.g. 36 tiles x 7 = 252 units)")
     ap.add_argument("--dump", default=None,
                     help="also write every timing (shape -> {tile/split: us}) to this JSON")
     a = ap.parse_args()
@@ -109,6 +115,8 @@ def main():
             continue
         if a.only_f16 and d.operand_type != 1:
             continue
+        if a.only_wgrad and d.epilogue != L.EPI_F32_ACC:
+            continue
         uniq.setdefault(key(d), (d, flops, refs, []))[3].append(1)
     print(f"{len(rec)} launches, {len(uniq)} distinct GEMMs", flush=True)
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
@@ -122,7 +130,8 @@ def main():
         t_auto, ws = time_desc(d, a.iters, ws)
         best = (t_auto, 0, 0)
         ktiles = (d0.K + 63) // 64
-        splits = [s for s in SPLITS if s <= ktiles] if d0.epilogue == L.EPI_F32_ACC else [1]
+        cand = sorted(set(SPLITS) | set(range(1, 33))) if a.all_splits else SPLITS
+        splits = [s for s in cand if s <= ktiles] if d0.epilogue == L.EPI_F32_ACC else [1]
         for tile in tiles:
             for sk in splits:
                 d = copy_desc(d0)
