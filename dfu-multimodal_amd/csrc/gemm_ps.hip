@@ -443,7 +443,9 @@ __global__ __launch_bounds__(512) void gemm_ps(const GemmArgs p) {
   // LDS-DMA: 10-13 % slower on 4096^3 and the ViT shapes, same box.  And the ping-pong schedule
   // of cdna_hip_programming.md's 256^2 template on this tile (wave row 1 one barrier behind row
   // 0, two barriers per quadrant phase, MFMAs at priority 1, both B halves in registers, one
-  // half-tile of DMA per phase): level at 4096^3 and fc2, 4-7 % slower at K = 768.)
+  // half-tile of DMA per phase): level at 4096^3 and fc2, 4-7 % slower at K = 768.  And the
+  // DMA issued by wave row 0 alone (its pieces and row 1's, so one wave per SIMD keeps issuing
+  // MFMAs): level everywhere.)
   bf16x8 fa[FMH][2], fb[2][2];
   auto rd_a = [&](const char* la, int h, int ks) {
     if constexpr ((kAbl & (8 | 512)) != 0)
