@@ -7,6 +7,7 @@ kernel's own duration says little about what it costs the step (the other encode
 it leaves idle); this measures the step instead.
 
   python tools/step_ablate.py [--steps 10] [--rounds 3] [--variants bn_fin,attn_bwd,...]
+      [--config rgb]
 """
 import argparse
 import os
@@ -40,6 +41,9 @@ VARIANTS = {
     "gemm_wgrad_vit": ("gemm", lambda d: d.epilogue == EPI_F32_ACC and d.K == 12608),
     "gemm_wgrad_resnet": ("gemm", lambda d: d.epilogue == EPI_F32_ACC and d.K != 12608),
     "gemm_x3pairs": ("gemm", lambda d: bool(d.x3_pairs)),
+    "gemm_dgrad_strided": ("gemm", lambda d: d.a_mode == 3),  # OPND_CONV_DGRAD (stride 2)
+    "gemm_resnet_dgrad": ("gemm", lambda d: d.M != 12608 and not d.x3_pairs and
+                          d.epilogue in (EPI_BF16, 6)),  # BF16 / BF16_ADD input gradients
     "gemm_x3_layer1": ("gemm", lambda d: bool(d.x3_pairs) and d.M == 200704),
     "gemm_x3_deep": ("gemm", lambda d: bool(d.x3_pairs) and d.M < 200704),
     "gemm_f16_gelu": ("gemm", lambda d: d.operand_type == 1 and d.epilogue == EPI_F16_GELU),
@@ -76,12 +80,13 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--config", default="fusion", help="fusion | rgb | thermal (bench.build)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     proxy = _Proxy(L.load())
     L._lib = proxy  # every L.load() / ops.lib() from here on returns the proxy
     torch.manual_seed(42)
-    model, fwd = bench.build("fusion", dev)
+    model, fwd = bench.build(a.config, dev)
     opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
     crit = hnn.CrossEntropyLoss(weight=torch.tensor([2.0, 2.0], device=dev))
     rgb, th, y = bench.synthetic(64, dev, seed=42)
