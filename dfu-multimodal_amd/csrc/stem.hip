@@ -248,7 +248,199 @@ __global__ __launch_bounds__(SNT, 2) void k_stem_conv_x3(
   }
 }
 
+// ---------------------------------------------------------------- weight gradient
+// dW[n][k] += sum_m dy[m][n] * bf16(x at tap k of output pixel m): the stem's weight gradient
+// straight from the fp32 image (the bf16 backward's operand is bf16(x), the hi rows the
+// explicit path's im2col held), so no im2col rows are written in the forward or read here.
+// A persistent workgroup walks 128-pixel tiles (as k_stem_conv_x3): it stages the tile's input
+// rows (fp32, <= 11 rows x 3 channels) and its dy rows ([128][64] bf16, row stride 72) in LDS,
+// and per 32-pixel step builds
+//   Y fragments (the dy side: 16 channels x 8 consecutive pixels per lane) by two
+//     ds_read_b64_tr_b16 each -- the compiler's builtin: no LDS-DMA here, so its waits are exact;
+//   X fragments (the im2col side: 16 taps x the same 8 pixels) by eight LDS reads of x at
+//     base(pixel) + koff(tap) (8 consecutive pixels lie in one output row: Q % 8 == 0),
+// and accumulates D[n][k] over all its tiles in registers: wave w owns the tap fragments
+// w, w + 4, w + 8 (< 10) x all four channel fragments.  Its partial D goes to slab[blockIdx]
+// ([64][147] fp32); k_stem_wgrad_reduce adds the slabs into dW in slab order (deterministic).
+constexpr int SDYS = 72;  // dy LDS row stride (bf16): 144-B rows
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+DFU_DEV bf16x4 tr16_b64(const bf16_t* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+__global__ __launch_bounds__(SNT, 2) void k_stem_wgrad(
+    const float* __restrict__ x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int H, int W,
+    int P, int Q, int tiles, const bf16_t* __restrict__ dy, float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int WP = W + 6;
+  float* xin = (float*)smem;                                     // [SC][SRR][WP]
+  const int xin_bytes = (SC * SRR * WP * 4 + 4 + 15) / 16 * 16;  // + the zero slot
+  bf16_t* dys = (bf16_t*)(smem + xin_bytes);                     // [STM][SDYS]
+  int* koff = (int*)(dys + STM * SDYS);                          // [SKP]
+  const int ZERO = SC * SRR * WP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lrow = lane & 15, kc = lane >> 4;
+  if (tid < SKP) {
+    const unsigned k = tid, c = k / 49u, rem = k - 49u * c, r = rem / 7u, s_ = rem - 7u * r;
+    koff[k] = k < (unsigned)SKR ? (int)((c * SRR + r) * WP + s_) : (1 << 24);
+  }
+  if (tid == 0) xin[ZERO] = 0.f;
+
+  const int PQ = P * Q;
+  const int cc = tid;  // staged input column of this thread (W + 6 <= 256: host-checked)
+  float v[SC * SRR];
+  u32x4 dv[4];
+  auto load_tile = [&](int t) {  // into registers: the tile's input rows and dy rows
+    const int m0 = t * STM;
+    const int b = m0 / PQ;
+    const int pa = (m0 - b * PQ) / Q;
+    const float* xb = x + b * sn;
+    const int iw = cc - 3;
+    const bool okw = cc < WP && (unsigned)iw < (unsigned)W;
+    const int iwc = min(max(iw, 0), W - 1);
+#pragma unroll
+    for (int cr = 0; cr < SC * SRR; ++cr) {
+      const int c = cr / SRR, rr = cr - c * SRR;
+      const int ihc = min(max(2 * pa - 3 + rr, 0), H - 1);
+      v[cr] = xb[c * sc + (int64_t)ihc * sh + (int64_t)iwc * sw];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dv[i] = *(const u32x4*)(dy + (int64_t)(m0 + (tid >> 3) + 32 * i) * SK + 8 * (tid & 7));
+#pragma unroll
+    for (int cr = 0; cr < SC * SRR; ++cr) {
+      const int ih = 2 * pa - 3 + cr % SRR;
+      v[cr] = okw && (unsigned)ih < (unsigned)H ? v[cr] : 0.f;
+    }
+  };
+  f32x4 acc[4][3];
+#pragma unroll
+  for (int rf = 0; rf < 4; ++rf)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[rf][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // koff
+  int ko[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int cf = wave + 4 * j;
+    ko[j] = koff[min(16 * cf + lrow, SKP - 1)];
+  }
+  const int tq = lane & 15, tp = tq & 3, tr = tq >> 2;  // transposed-read lane roles
+  if ((int)blockIdx.x < tiles) load_tile(blockIdx.x);
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int m0 = t * STM;
+    const int b = m0 / PQ;
+    const int pq0 = m0 - b * PQ;
+    const int pa = pq0 / Q;
+    __syncthreads();  // the previous tile's reads of xin / dys are done
+    if (cc < WP) {
+#pragma unroll
+      for (int cr = 0; cr < SC * SRR; ++cr) xin[cr * WP + cc] = v[cr];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *(u32x4*)(dys + ((tid >> 3) + 32 * i) * SDYS + 8 * (tid & 7)) = dv[i];
+    __syncthreads();
+    if (t + (int)gridDim.x < tiles) load_tile(t + gridDim.x);
+#pragma unroll
+    for (int ks = 0; ks < STM / 32; ++ks) {
+      // this lane's 8 pixels: 32 ks + 8 kc + 0..7 (one output row)
+      const int pq = pq0 + 32 * ks + 8 * kc;
+      const int p = pq / Q, q = pq - p * Q;
+      const int base = 2 * (p - pa) * WP + 2 * q;
+      bf16x8 yf[4];
+#pragma unroll
+      for (int rf = 0; rf < 4; ++rf) {
+        const bf16_t* a0 = dys + (32 * ks + 8 * kc + tr) * SDYS + 16 * rf + 4 * tp;
+        const bf16x4 lo4 = tr16_b64(a0), hi4 = tr16_b64(a0 + 4 * SDYS);
+        yf[rf] = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if (wave + 4 * j >= SKP / 16) continue;  // (wave-uniform)
+        float h[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = bf2f(f2bf(xin[min(base + 2 * e + ko[j], ZERO)]));
+        const bf16x8 xf = __builtin_bit_cast(bf16x8, pack8(h));
+#pragma unroll
+        for (int rf = 0; rf < 4; ++rf)
+          acc[rf][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, yf[rf], acc[rf][j], 0, 0, 0);
+      }
+    }
+  }
+  // lane holds D[n = 16 rf + lrow][k = 16 cf + 4 kc + r]
+  float* sl = slab + (int64_t)blockIdx.x * SK * SKR;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int cf = wave + 4 * j;
+    if (cf >= SKP / 16) continue;
+#pragma unroll
+    for (int rf = 0; rf < 4; ++rf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * cf + 4 * kc + r;
+        if (k < SKR) sl[(16 * rf + lrow) * SKR + k] = acc[rf][j][r];
+      }
+  }
+}
+
+// dW[i] += sum over the G slabs of slab[g][i], i < 64 x 147, in slab order: 4 slices of the
+// slabs per element (threads), merged in slice order.
+__global__ __launch_bounds__(256) void k_stem_wgrad_reduce(const float* __restrict__ slab, int G,
+                                                           float* __restrict__ dw) {
+  __shared__ float part[4][64];
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6;
+  constexpr int NE = SK * SKR;
+  float s = 0.f;
+  if (i < NE) {
+    for (int g = sl; g < G; g += 4) s += slab[(int64_t)g * NE + i];
+  }
+  part[sl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sl == 0 && i < NE) {
+    const int l = threadIdx.x & 63;
+    dw[i] += ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+  }
+}
+
 }  // namespace
+
+extern "C" int64_t dfu_stem_wgrad_ws_bytes(int32_t B, int32_t H, int32_t W) {
+  const int P = (H + 6 - 7) / 2 + 1, Q = (W + 6 - 7) / 2 + 1;
+  const int64_t tiles = (int64_t)B * P * Q / STM;
+  const int64_t g = tiles < 512 ? tiles : 512;
+  return g * SK * SKR * 4;
+}
+
+extern "C" int dfu_stem_wgrad_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
+                                 int32_t B, int32_t C, int32_t H, int32_t W, const void* dy,
+                                 int32_t K, int32_t R, int32_t S, int32_t stride, int32_t pad,
+                                 float* dw, float* slab, int64_t slab_bytes, void* stream) {
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  DFU_CHECK_ARG(x && dy && dw && slab && C == SC && K == SK && R == SR && S == SR &&
+                    stride == 2 && pad == 3 && B > 0 && H >= SR && W >= SR,
+                "dfu_stem_wgrad_x3: the 7x7/s2/p3 3->64 stem only");
+  DFU_CHECK_ARG((P * Q) % STM == 0 && Q >= 64 && Q % 8 == 0 && W + 6 <= SNT &&
+                    (int64_t)B * P * Q < (1LL << 31),
+                "dfu_stem_wgrad_x3: needs P*Q %% 128 == 0, Q >= 64, Q %% 8 == 0, W <= 250");
+  DFU_CHECK_ARG((((uintptr_t)dy) & 15) == 0, "dfu_stem_wgrad_x3: dy must be 16-byte aligned");
+  const int tiles = B * P * Q / STM;
+  const int grid = tiles < 512 ? tiles : 512;
+  DFU_CHECK_ARG(slab_bytes >= (int64_t)grid * SK * SKR * 4,
+                "dfu_stem_wgrad_x3: slab needs dfu_stem_wgrad_ws_bytes bytes");
+  const int xin_bytes = (SC * SRR * (W + 6) * 4 + 4 + 15) / 16 * 16;
+  const size_t lds = xin_bytes + STM * SDYS * 2 + SKP * 4;
+  hipLaunchKernelGGL(k_stem_wgrad, dim3(grid), dim3(SNT), lds, (hipStream_t)stream, x, sn, sc, sh,
+                     sw, H, W, P, Q, tiles, (const bf16_t*)dy, slab);
+  DFU_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_stem_wgrad_reduce, dim3((SK * SKR + 63) / 64), dim3(256), 0,
+                     (hipStream_t)stream, slab, grid, dw);
+  DFU_LAUNCH_CHECK();
+  return DFU_OK;
+}
 
 extern "C" int dfu_stem_conv_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
                                 int32_t B, int32_t C, int32_t H, int32_t W, const float* w,

@@ -152,6 +152,9 @@ PROTOTYPES = {
     "dfu_pack_conv_weight_x3": [P, P, I32, I32, I32, I32, I32, P],
     "dfu_stem_conv_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, P, I32, I32, I32, I32, I32,
                          P, P, P, P, P],
+    "dfu_stem_wgrad_ws_bytes": [I32, I32, I32],
+    "dfu_stem_wgrad_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, P, I32, I32, I32, I32, I32,
+                          P, P, I64, P],
     "dfu_maxpool_bn_fwd_x3": [P, P, P, P, I32, I32, I32, I32, P, P, P, P, I32, I32, P],
     "dfu_im2col_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, P, I32, P],
     "dfu_patchify_f32_x3": [P, I64, I64, I64, I64, I32, I32, I32, I32, I32, P, P],
@@ -169,7 +172,7 @@ PROTOTYPES = {
 }
 _RESTYPE = {"dfu_last_error_string": c_char_p, "dfu_gemm_workspace_bytes": c_int64,
             "dfu_gemm_f32_workspace_bytes": c_int64, "dfu_bn_finalize_ws_bytes": c_int64,
-            "dfu_bn_bwd_finalize_ws_bytes": c_int64}
+            "dfu_bn_bwd_finalize_ws_bytes": c_int64, "dfu_stem_wgrad_ws_bytes": c_int64}
 
 
 def header_symbols(path=HEADER_PATH):

@@ -682,8 +682,8 @@ class StemFn(torch.autograd.Function):
         # bf16x3: one implicit-GEMM kernel (dfu_stem_conv_x3: no pair im2col in HBM) where its
         # geometry allows; DFU_STEM_FUSED=0: the pair im2col + interleaved-pair GEMM (A/B)
         fused = x3 and _STEM_FUSED and Kp == 160 and ops.stem_conv_x3_ok(xf, w, st, pad)
-        if fused:
-            y, y_lo, stats, col, P, Q = ops.stem_conv_x3(xf, w.detach(), st, pad)
+        if fused:  # no im2col rows: the backward's weight gradient reads x (dfu_stem_wgrad_x3)
+            y, y_lo, stats, col, P, Q = ops.stem_conv_x3(xf, w.detach(), st, pad, want_col=False)
         elif x3:
             (col, col_lo), P, Q = ops.im2col_f32_x3(xf, R, S, st, pad, Kp)  # split pair
         else:
@@ -725,7 +725,8 @@ class StemFn(torch.autograd.Function):
         ctx.x3 = x3
         ctx.dims = (B, C, H, W, P, Q, P2, Q2, Cout, Kp, R, S, st, pad)
         ctx.x_requires_grad = x.requires_grad
-        ctx.save_for_backward(col, y, a, am, wb)
+        ctx.fused = fused
+        ctx.save_for_backward(xf if fused else col, y, a, am, wb)
         res = out.permute(0, 3, 1, 2)
         if x3:
             res._dfu_lo = out_lo
@@ -748,9 +749,12 @@ class StemFn(torch.autograd.Function):
         if _wants(w):
             dw = grad_buffer(w).view(Cout, -1)
             K = C * R * S
-            # bf16 im2col rows: the col itself, or the hi rows of the bf16x3 split pair
-            ops.gemm(Cout, K, M, dy, Cout, col, col.stride(0), dw, K, a_mode=L.OPND_MNMAJOR,
-                     b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+            if ctx.fused:  # from x itself (the saved tensor is xf): no im2col rows
+                ops.stem_wgrad_x3(col, dy, dw, st, pad)
+            else:
+                # bf16 im2col rows: the col itself, or the hi rows of the bf16x3 split pair
+                ops.gemm(Cout, K, M, dy, Cout, col, col.stride(0), dw, K, a_mode=L.OPND_MNMAJOR,
+                         b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
             grads_done(w)
         dx = None
         if ctx.x_requires_grad:

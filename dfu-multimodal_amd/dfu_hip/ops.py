@@ -882,6 +882,23 @@ def stem_conv_x3(x, w, stride=2, pad=3, want_col=True):
     return y, y_lo, stats, col, P, Q
 
 
+def stem_wgrad_x3(x, dy, dw, stride=2, pad=3):
+    """dw [64][147] fp32 += the stem's weight gradient from x fp32 (B, 3, H, W) any strides and
+    dy bf16 [B*P*Q, 64] (dfu_stem_wgrad_x3: no im2col rows)."""
+    _req(x, F32, "stem_wgrad_x3")
+    _req(dy, BF16, "stem_wgrad_x3")
+    _req(dw, F32, "stem_wgrad_x3")
+    B, C, H, W = x.shape
+    if not (dw.is_contiguous() and dw.numel() == 64 * C * 49 and dy.is_contiguous()):
+        raise ValueError("stem_wgrad_x3: dw [64][3*7*7] and dy [M][64] contiguous")
+    nbytes = int(lib().dfu_stem_wgrad_ws_bytes(B, H, W))
+    slab = torch.empty((max(1, nbytes // 4),), dtype=F32, device=x.device)
+    sn, sc, sh, sw = x.stride()
+    check(lib().dfu_stem_wgrad_x3(ptr(x), sn, sc, sh, sw, B, C, H, W, ptr(dy), 64, 7, 7, stride,
+                                  pad, ptr(dw), ptr(slab), nbytes, stream_ptr()),
+          "dfu_stem_wgrad_x3")
+
+
 def stem_conv_x3_ok(x, w, stride, pad):
     """Whether dfu_stem_conv_x3 takes this stem (its geometry checks, host side)."""
     B, C, H, W = x.shape
@@ -890,7 +907,7 @@ def stem_conv_x3_ok(x, w, stride, pad):
         return False
     P = (H + 2 * pad - R) // stride + 1
     Q = (W + 2 * pad - S) // stride + 1
-    return (P * Q) % 128 == 0 and Q >= 64 and B * P * Q < (1 << 31)
+    return (P * Q) % 128 == 0 and Q >= 64 and Q % 8 == 0 and B * P * Q < (1 << 31)
 
 
 def maxpool_bn_fwd_x3(y, y_lo, scale, shift, B, H, W, C, relu_mask=None):

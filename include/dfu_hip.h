@@ -507,13 +507,25 @@ int dfu_maxpool_fwd_x3(const float* x, int32_t B, int32_t H, int32_t W, int32_t 
  * sw), w fp32 OIHW [64][3][7][7] -> the conv output as a split pair y / y_lo (bf16 [B*P*Q][64]
  * each: hi = bf16(v), lo = bf16(v - hi)), the BN tile statistics stats [B*P*Q / 128][2][64]
  * (sum, M2 of each 128-row block, as the F32_STATS epilogue) and optionally col, the hi
- * im2col rows [B*P*Q][160] bf16 (taps 147.. zero) the weight gradient reads.  The same fp32
+ * im2col rows [B*P*Q][160] bf16 (taps 147.. zero; the library's own backward reads x instead:
+ * dfu_stem_wgrad_x3).  The same fp32
  * values as dfu_im2col_f32_x3 + the interleaved-pair dfu_gemm, without the pair im2col in
  * HBM.  Needs P*Q % 128 == 0, Q >= 64, W <= 250. */
 int dfu_stem_conv_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
                      int32_t C, int32_t H, int32_t W, const float* w, int32_t K, int32_t R,
                      int32_t S, int32_t stride, int32_t pad, void* y, void* y_lo, float* stats,
                      void* col, void* stream);
+/* The bf16x3 stem's weight gradient without im2col rows (replaces the MN x MN F32_ACC dfu_gemm
+ * over col in StemFn.backward, resnet50 conv1 weight.grad): dw [64][147] fp32 (OIHW order,
+ * contiguous) += sum over the B*P*Q output pixels m of dy[m][n] * bf16(x at tap k of m), from
+ * x fp32 NCHW with element strides (sn, sc, sh, sw) and dy bf16 [B*P*Q][64] (16-B aligned).
+ * Deterministic: per-workgroup partials into slab (dfu_stem_wgrad_ws_bytes bytes), summed in a
+ * fixed order.  The 7x7/s2/p3 3 -> 64 stem with P*Q % 128 == 0, Q >= 64, Q % 8 == 0, W <= 250. */
+int64_t dfu_stem_wgrad_ws_bytes(int32_t B, int32_t H, int32_t W);
+int dfu_stem_wgrad_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
+                      int32_t C, int32_t H, int32_t W, const void* dy, int32_t K, int32_t R,
+                      int32_t S, int32_t stride, int32_t pad, float* dw, float* slab,
+                      int64_t slab_bytes, void* stream);
 /* bn1 + ReLU + maxpool 3x3/s2/p1 of the bf16x3 stem in one pass (bitwise dfu_bn_apply_x3 with
  * out_f32 then dfu_maxpool_fwd_x3, without the fp32 intermediate): the conv output split pair
  * y / y_lo (bf16 NHWC [B*H*W][C] each), BN scale / shift (fp32 [C], 16-B aligned) -> pooled

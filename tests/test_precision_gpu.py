@@ -507,3 +507,32 @@ def test_stem_conv_x3_fused_equals_pair_im2col_gemm(contig):
     err = ((v - ref).abs().max() / ref.abs().max()).item()
     print(f"\n[stem x3 fused] rel err vs fp64 conv {err:.2e}")
     assert err < 2e-5
+
+
+@pytest.mark.parametrize("contig", [True, False])
+def test_stem_wgrad_x3_from_x_equals_im2col_gemm(contig):
+    """The stem weight gradient straight from x (dfu_stem_wgrad_x3: no im2col rows) against the
+    explicit MN x MN F32_ACC GEMM over the hi im2col rows it replaces: equal to fp32 summation
+    order, accumulated onto what dw held, and within bf16-operand accuracy of an fp64 sum."""
+    L, ops = _ops()
+    torch.manual_seed(11)
+    B, H, W = 2, 224, 224
+    xs = torch.randn(B, 3, H, W + (0 if contig else 5), device=DEV)
+    x = xs[..., :W] if not contig else xs
+    M = B * 112 * 112
+    dy = (torch.randn(M, 64, device=DEV) * 0.1).to(torch.bfloat16)
+    col, P, Q = ops.im2col_f32(x, 7, 7, 2, 3, 160)
+    d0 = torch.randn(64, 147, device=DEV)
+    ref = d0.clone()
+    ops.gemm(64, 147, M, dy, 64, col, 160, ref, 147, a_mode=L.OPND_MNMAJOR,
+             b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+    dw = d0.clone()
+    ops.stem_wgrad_x3(x, dy, dw)
+    torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-3)
+    exact = d0.double() + dy.double().t() @ col[:, :147].double()
+    err = ((dw.double() - exact).abs().max() / (exact - d0.double()).abs().max()).item()
+    print(f"\n[stem wgrad from x] rel err vs fp64 sum {err:.2e}")
+    assert err < 1e-5
+    dw2 = d0.clone()
+    ops.stem_wgrad_x3(x, dy, dw2)
+    assert torch.equal(dw, dw2)  # deterministic
