@@ -355,44 +355,53 @@ __global__ __launch_bounds__(256) void k_maxpool_rows(const bf16_t* __restrict__
   *(uint64_t*)(am + o) = packed;
 }
 
-// Backward, one input row per blockIdx.y = (b, h): every input pixel gathers dy of the (at most
-// 2 x 2) windows whose argmax it is (deterministic: the windows in row-major order).
-__global__ __launch_bounds__(256) void k_maxpool_bwd_rows(const bf16_t* __restrict__ dy,
-                                                          const uint8_t* __restrict__ am, int H,
-                                                          int W, int C, int P, int Q,
-                                                          bf16_t* __restrict__ dx) {
+// Backward, one input row pair per blockIdx.y = (b, h / 2): a thread owns the 2 x 2 input
+// pixels (2i .. 2i+1, 2j .. 2j+1) of one 8-channel group.  Every one of them can only be the
+// argmax of the windows (p, q) in {i, i+1} x {j, j+1} (window p covers rows 2p-1 .. 2p+1), so
+// the thread loads those four windows' dy and argmax once (not once per pixel) and each pixel
+// sums the windows whose argmax it is in row-major window order (deterministic; the same
+// order and values as a per-pixel gather).
+__global__ __launch_bounds__(256) void k_maxpool_bwd_2x2(const bf16_t* __restrict__ dy,
+                                                         const uint8_t* __restrict__ am, int H,
+                                                         int W, int C, int P, int Q,
+                                                         bf16_t* __restrict__ dx) {
   const int cv = C / 8;
+  const int W2 = (W + 1) / 2, H2 = (H + 1) / 2;
   const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= W * cv) return;
-  const int b = blockIdx.y / H, h = blockIdx.y - b * H;
-  const int w = t / cv, c8 = t - w * cv;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  // windows p = h/2 + dp (dp = 0, 1) and q = w/2 + dq cover every window holding (h, w); the
-  // four candidates' loads go out together (clamped addresses), invalid ones are skipped, and
-  // the valid ones are summed in row-major window order
-  const int p0 = h / 2, q0 = w / 2;
+  if (t >= W2 * cv) return;
+  const int b = blockIdx.y / H2, i = blockIdx.y - b * H2;
+  const int j = t / cv, c8 = t - j * cv;
   uint64_t a4[4];
   u32x4 g4[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int p = min(p0 + (k >> 1), P - 1), q = min(q0 + (k & 1), Q - 1);
+  for (int k = 0; k < 4; ++k) {  // every load from a clamped address; invalid windows skipped
+    const int p = min(i + (k >> 1), P - 1), q = min(j + (k & 1), Q - 1);
     const int64_t o = (((int64_t)b * P + p) * Q + q) * C + c8 * 8;
     a4[k] = *(const uint64_t*)(am + o);
     g4[k] = *(const u32x4*)(dy + o);
   }
+  float f4[4][8];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int p = p0 + (k >> 1), q = q0 + (k & 1);
-    const int wi = h - (2 * p - 1), wj = w - (2 * q - 1);
-    if (p >= P || q >= Q || wi < 0 || wi > 2 || wj < 0 || wj > 2) continue;
-    float f[8];
-    unpack8(g4[k], f);
-    const int want = wi * 3 + wj;
+  for (int k = 0; k < 4; ++k) unpack8(g4[k], f4[k]);
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      if ((int)((a4[k] >> (8 * e)) & 0xff) == want) acc[e] += f[e];
-  }
-  *(u32x4*)(dx + ((int64_t)blockIdx.y * W + w) * C + c8 * 8) = pack8(acc);
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const int h = 2 * i + dh, w = 2 * j + dw;
+      if (h >= H || w >= W) continue;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int p = i + (k >> 1), q = j + (k & 1);
+        const int wi = h - (2 * p - 1), wj = w - (2 * q - 1);
+        if (p >= P || q >= Q || wi < 0 || wi > 2 || wj < 0 || wj > 2) continue;
+        const int want = wi * 3 + wj;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((int)((a4[k] >> (8 * e)) & 0xff) == want) acc[e] += f4[k][e];
+      }
+      *(u32x4*)(dx + (((int64_t)b * H + h) * W + w) * C + c8 * 8) = pack8(acc);
+    }
 }
 
 __global__ void k_avgpool_fwd(const bf16_t* __restrict__ x, int B, int HW, int C,
@@ -1013,9 +1022,10 @@ extern "C" int dfu_maxpool_bwd(const void* dy, const uint8_t* argmax, int32_t B,
                                int32_t W, int32_t C, int32_t P, int32_t Q, void* dx,
                                void* stream) {
   DFU_CHECK_ARG(dy && dx && argmax && C % 8 == 0, "dfu_maxpool_bwd: C %% 8 != 0");
-  DFU_CHECK_ARG((int64_t)B * H < 65536 && W * (C / 8) < (1 << 24), "dfu_maxpool_bwd: size");
-  const dim3 grid((W * (C / 8) + 255) / 256, B * H);
-  hipLaunchKernelGGL(k_maxpool_bwd_rows, grid, dim3(256), 0, (hipStream_t)stream,
+  DFU_CHECK_ARG((int64_t)B * ((H + 1) / 2) < 65536 && W * (C / 8) < (1 << 24),
+                "dfu_maxpool_bwd: size");
+  const dim3 grid(((W + 1) / 2 * (C / 8) + 255) / 256, B * ((H + 1) / 2));
+  hipLaunchKernelGGL(k_maxpool_bwd_2x2, grid, dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)dy, argmax, H, W, C, P, Q, (bf16_t*)dx);
   DFU_LAUNCH_CHECK();
   return DFU_OK;
