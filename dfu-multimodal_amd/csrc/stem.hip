@@ -252,17 +252,21 @@ __global__ __launch_bounds__(SNT, 2) void k_stem_conv_x3(
 // dW[n][k] += sum_m dy[m][n] * bf16(x at tap k of output pixel m): the stem's weight gradient
 // straight from the fp32 image (the bf16 backward's operand is bf16(x), the hi rows the
 // explicit path's im2col held), so no im2col rows are written in the forward or read here.
-// A persistent workgroup walks 128-pixel tiles (as k_stem_conv_x3): it stages the tile's input
-// rows (fp32, <= 11 rows x 3 channels) and its dy rows ([128][64] bf16, row stride 72) in LDS,
-// and per 32-pixel step builds
+// A persistent workgroup walks tiles of TWO output rows (2Q pixels of one image: the 9 input
+// rows they touch are staged once, where 128-pixel tiles restaged 11 rows per 1.14 output rows)
+// and stages the tile's input rows (fp32, 3 channels) and dy rows ([2Q][64] bf16, row stride
+// 72) in LDS; per 32-pixel step it builds
 //   Y fragments (the dy side: 16 channels x 8 consecutive pixels per lane) by two
 //     ds_read_b64_tr_b16 each -- the compiler's builtin: no LDS-DMA here, so its waits are exact;
-//   X fragments (the im2col side: 16 taps x the same 8 pixels) by eight LDS reads of x at
-//     base(pixel) + koff(tap) (8 consecutive pixels lie in one output row: Q % 8 == 0),
+//   X fragments (the im2col side: 16 taps x the same 8 pixels) by reads of x at
+//     base(pixel) + koff(tap) + 2e (8 consecutive pixels lie in one output row: Q % 16 == 0;
+//     one address per fragment, so the reads pair into ds_read2_b32),
 // and accumulates D[n][k] over all its tiles in registers: wave w owns the tap fragments
 // w, w + 4, w + 8 (< 10) x all four channel fragments.  Its partial D goes to slab[blockIdx]
-// ([64][147] fp32); k_stem_wgrad_reduce adds the slabs into dW in slab order (deterministic).
-constexpr int SDYS = 72;  // dy LDS row stride (bf16): 144-B rows
+// ([64][147] fp32); k_stem_wgrad_reduce adds the slabs into dW in a fixed order.
+constexpr int SDYS = 72;       // dy LDS row stride (bf16): 144-B rows
+constexpr int WRR = 9;         // staged input rows per two-output-row tile
+constexpr int WDV = 7;         // dy 16-B loads per thread per tile: 2Q <= 224 rows
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 DFU_DEV bf16x4 tr16_b64(const bf16_t* p) {
@@ -276,43 +280,46 @@ __global__ __launch_bounds__(SNT, 2) void k_stem_wgrad(
     int P, int Q, int tiles, const bf16_t* __restrict__ dy, float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int WP = W + 6;
-  float* xin = (float*)smem;                                     // [SC][SRR][WP]
-  const int xin_bytes = (SC * SRR * WP * 4 + 4 + 15) / 16 * 16;  // + the zero slot
-  bf16_t* dys = (bf16_t*)(smem + xin_bytes);                     // [STM][SDYS]
-  int* koff = (int*)(dys + STM * SDYS);                          // [SKP]
-  const int ZERO = SC * SRR * WP;
+  const int TP = 2 * Q;  // pixels per tile
+  float* xin = (float*)smem;                                       // [SC][WRR][WP]
+  const int xin_bytes = (SC * WRR * WP * 4 + 64 + 15) / 16 * 16;   // + 16 zeros
+  bf16_t* dys = (bf16_t*)(smem + xin_bytes);                       // [TP][SDYS]
+  int* koff = (int*)(dys + TP * SDYS);                             // [SKP]
+  const int ZERO = SC * WRR * WP;  // 16 zero floats: a padded tap's 8 pixel reads land there
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lrow = lane & 15, kc = lane >> 4;
   if (tid < SKP) {
     const unsigned k = tid, c = k / 49u, rem = k - 49u * c, r = rem / 7u, s_ = rem - 7u * r;
-    koff[k] = k < (unsigned)SKR ? (int)((c * SRR + r) * WP + s_) : (1 << 24);
+    koff[k] = k < (unsigned)SKR ? (int)((c * WRR + r) * WP + s_) : (1 << 24);
   }
-  if (tid == 0) xin[ZERO] = 0.f;
+  if (tid < 16) xin[ZERO + tid] = 0.f;
 
-  const int PQ = P * Q;
+  const int P2 = P / 2;
   const int cc = tid;  // staged input column of this thread (W + 6 <= 256: host-checked)
-  float v[SC * SRR];
-  u32x4 dv[4];
+  float v[SC * WRR];
+  u32x4 dv[WDV];
   auto load_tile = [&](int t) {  // into registers: the tile's input rows and dy rows
-    const int m0 = t * STM;
-    const int b = m0 / PQ;
-    const int pa = (m0 - b * PQ) / Q;
+    const int b = t / P2;
+    const int pa = 2 * (t - b * P2);
     const float* xb = x + b * sn;
     const int iw = cc - 3;
     const bool okw = cc < WP && (unsigned)iw < (unsigned)W;
     const int iwc = min(max(iw, 0), W - 1);
 #pragma unroll
-    for (int cr = 0; cr < SC * SRR; ++cr) {
-      const int c = cr / SRR, rr = cr - c * SRR;
+    for (int cr = 0; cr < SC * WRR; ++cr) {
+      const int c = cr / WRR, rr = cr - c * WRR;
       const int ihc = min(max(2 * pa - 3 + rr, 0), H - 1);
       v[cr] = xb[c * sc + (int64_t)ihc * sh + (int64_t)iwc * sw];
     }
+    const int64_t m0 = ((int64_t)b * P + pa) * Q;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dv[i] = *(const u32x4*)(dy + (int64_t)(m0 + (tid >> 3) + 32 * i) * SK + 8 * (tid & 7));
+    for (int i = 0; i < WDV; ++i) {  // rows past the tile (2Q < 224) reload its last row
+      const int row = min((tid >> 3) + 32 * i, TP - 1);
+      dv[i] = *(const u32x4*)(dy + (m0 + row) * SK + 8 * (tid & 7));
+    }
 #pragma unroll
-    for (int cr = 0; cr < SC * SRR; ++cr) {
-      const int ih = 2 * pa - 3 + cr % SRR;
+    for (int cr = 0; cr < SC * WRR; ++cr) {
+      const int ih = 2 * pa - 3 + cr % WRR;
       v[cr] = okw && (unsigned)ih < (unsigned)H ? v[cr] : 0.f;
     }
   };
@@ -329,28 +336,26 @@ __global__ __launch_bounds__(SNT, 2) void k_stem_wgrad(
     ko[j] = koff[min(16 * cf + lrow, SKP - 1)];
   }
   const int tq = lane & 15, tp = tq & 3, tr = tq >> 2;  // transposed-read lane roles
+  const int ksteps = TP / 32;
   if ((int)blockIdx.x < tiles) load_tile(blockIdx.x);
   for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
-    const int m0 = t * STM;
-    const int b = m0 / PQ;
-    const int pq0 = m0 - b * PQ;
-    const int pa = pq0 / Q;
     __syncthreads();  // the previous tile's reads of xin / dys are done
     if (cc < WP) {
 #pragma unroll
-      for (int cr = 0; cr < SC * SRR; ++cr) xin[cr * WP + cc] = v[cr];
+      for (int cr = 0; cr < SC * WRR; ++cr) xin[cr * WP + cc] = v[cr];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *(u32x4*)(dys + ((tid >> 3) + 32 * i) * SDYS + 8 * (tid & 7)) = dv[i];
+    for (int i = 0; i < WDV; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      if (row < TP) *(u32x4*)(dys + row * SDYS + 8 * (tid & 7)) = dv[i];
+    }
     __syncthreads();
     if (t + (int)gridDim.x < tiles) load_tile(t + gridDim.x);
-#pragma unroll
-    for (int ks = 0; ks < STM / 32; ++ks) {
-      // this lane's 8 pixels: 32 ks + 8 kc + 0..7 (one output row)
-      const int pq = pq0 + 32 * ks + 8 * kc;
-      const int p = pq / Q, q = pq - p * Q;
-      const int base = 2 * (p - pa) * WP + 2 * q;
+    for (int ks = 0; ks < ksteps; ++ks) {
+      // this lane's 8 pixels: tile pixels 32 ks + 8 kc + 0..7 (one output row)
+      const int lp = 32 * ks + 8 * kc;
+      const int pr = lp >= Q ? 1 : 0, q = lp - pr * Q;
+      const int base = 2 * pr * WP + 2 * q;
       bf16x8 yf[4];
 #pragma unroll
       for (int rf = 0; rf < 4; ++rf) {
@@ -361,10 +366,11 @@ __global__ __launch_bounds__(SNT, 2) void k_stem_wgrad(
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         if (wave + 4 * j >= SKP / 16) continue;  // (wave-uniform)
+        const float* xp = xin + (ko[j] < (1 << 24) ? base + ko[j] : ZERO);
         float h[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) h[e] = bf2f(f2bf(xin[min(base + 2 * e + ko[j], ZERO)]));
-        const bf16x8 xf = __builtin_bit_cast(bf16x8, pack8(h));
+        for (int e = 0; e < 8; ++e) h[e] = xp[2 * e];
+        const bf16x8 xf = __builtin_bit_cast(bf16x8, pack8(h));  // bf16(x): the hi rows
 #pragma unroll
         for (int rf = 0; rf < 4; ++rf)
           acc[rf][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, yf[rf], acc[rf][j], 0, 0, 0);
@@ -387,32 +393,40 @@ __global__ __launch_bounds__(SNT, 2) void k_stem_wgrad(
   }
 }
 
-// dW[i] += sum over the G slabs of slab[g][i], i < 64 x 147, in slab order: 4 slices of the
-// slabs per element (threads), merged in slice order.
-__global__ __launch_bounds__(256) void k_stem_wgrad_reduce(const float* __restrict__ slab, int G,
-                                                           float* __restrict__ dw) {
-  __shared__ float part[4][64];
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6;
+// dW[i] += sum over the G slabs of slab[g][i], i < 64 x 147, in a fixed order: 16 slices of
+// the slabs per element (waves), each slice's loads all in flight (four running sums), then the
+// slices merged in order.
+__global__ __launch_bounds__(1024) void k_stem_wgrad_reduce(const float* __restrict__ slab,
+                                                            int G, float* __restrict__ dw) {
+  __shared__ float part[16][64];
+  const int l = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + l;
   constexpr int NE = SK * SKR;
-  float s = 0.f;
-  if (i < NE) {
-    for (int g = sl; g < G; g += 4) s += slab[(int64_t)g * NE + i];
+  const int ic = min(i, NE - 1);
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  int g = sl;
+  for (; g + 48 < G; g += 64) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s4[u] += slab[(int64_t)(g + 16 * u) * NE + ic];
   }
-  part[sl][threadIdx.x & 63] = s;
+  for (; g < G; g += 16) s4[0] += slab[(int64_t)g * NE + ic];
+  part[sl][l] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   __syncthreads();
   if (sl == 0 && i < NE) {
-    const int l = threadIdx.x & 63;
-    dw[i] += ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += part[k][l];
+    dw[i] += t;
   }
 }
 
 }  // namespace
 
 extern "C" int64_t dfu_stem_wgrad_ws_bytes(int32_t B, int32_t H, int32_t W) {
-  const int P = (H + 6 - 7) / 2 + 1, Q = (W + 6 - 7) / 2 + 1;
-  const int64_t tiles = (int64_t)B * P * Q / STM;
+  const int P = (H + 6 - 7) / 2 + 1;
+  const int64_t tiles = (int64_t)B * (P / 2);
   const int64_t g = tiles < 512 ? tiles : 512;
-  return g * SK * SKR * 4;
+  return (g > 0 ? g : 1) * SK * SKR * 4;
 }
 
 extern "C" int dfu_stem_wgrad_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw,
@@ -423,20 +437,21 @@ extern "C" int dfu_stem_wgrad_x3(const float* x, int64_t sn, int64_t sc, int64_t
   DFU_CHECK_ARG(x && dy && dw && slab && C == SC && K == SK && R == SR && S == SR &&
                     stride == 2 && pad == 3 && B > 0 && H >= SR && W >= SR,
                 "dfu_stem_wgrad_x3: the 7x7/s2/p3 3->64 stem only");
-  DFU_CHECK_ARG((P * Q) % STM == 0 && Q >= 64 && Q % 8 == 0 && W + 6 <= SNT &&
+  DFU_CHECK_ARG(P % 2 == 0 && Q % 16 == 0 && 2 * Q <= 32 * WDV && W + 6 <= SNT &&
                     (int64_t)B * P * Q < (1LL << 31),
-                "dfu_stem_wgrad_x3: needs P*Q %% 128 == 0, Q >= 64, Q %% 8 == 0, W <= 250");
+                "dfu_stem_wgrad_x3: needs P even, Q %% 16 == 0, Q <= 112, W <= 250 (P=%d Q=%d)",
+                P, Q);
   DFU_CHECK_ARG((((uintptr_t)dy) & 15) == 0, "dfu_stem_wgrad_x3: dy must be 16-byte aligned");
-  const int tiles = B * P * Q / STM;
+  const int tiles = B * (P / 2);
   const int grid = tiles < 512 ? tiles : 512;
   DFU_CHECK_ARG(slab_bytes >= (int64_t)grid * SK * SKR * 4,
                 "dfu_stem_wgrad_x3: slab needs dfu_stem_wgrad_ws_bytes bytes");
-  const int xin_bytes = (SC * SRR * (W + 6) * 4 + 4 + 15) / 16 * 16;
-  const size_t lds = xin_bytes + STM * SDYS * 2 + SKP * 4;
+  const int xin_bytes = (SC * WRR * (W + 6) * 4 + 64 + 15) / 16 * 16;
+  const size_t lds = xin_bytes + 2 * Q * SDYS * 2 + SKP * 4;
   hipLaunchKernelGGL(k_stem_wgrad, dim3(grid), dim3(SNT), lds, (hipStream_t)stream, x, sn, sc, sh,
                      sw, H, W, P, Q, tiles, (const bf16_t*)dy, slab);
   DFU_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_stem_wgrad_reduce, dim3((SK * SKR + 63) / 64), dim3(256), 0,
+  hipLaunchKernelGGL(k_stem_wgrad_reduce, dim3((SK * SKR + 63) / 64), dim3(1024), 0,
                      (hipStream_t)stream, slab, grid, dw);
   DFU_LAUNCH_CHECK();
   return DFU_OK;

@@ -907,7 +907,8 @@ def stem_conv_x3_ok(x, w, stride, pad):
         return False
     P = (H + 2 * pad - R) // stride + 1
     Q = (W + 2 * pad - S) // stride + 1
-    return (P * Q) % 128 == 0 and Q >= 64 and Q % 8 == 0 and B * P * Q < (1 << 31)
+    return ((P * Q) % 128 == 0 and Q >= 64 and Q % 16 == 0 and Q <= 112 and P % 2 == 0 and
+            B * P * Q < (1 << 31))
 
 
 def maxpool_bn_fwd_x3(y, y_lo, scale, shift, B, H, W, C, relu_mask=None):

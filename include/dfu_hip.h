@@ -520,7 +520,7 @@ int dfu_stem_conv_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t
  * contiguous) += sum over the B*P*Q output pixels m of dy[m][n] * bf16(x at tap k of m), from
  * x fp32 NCHW with element strides (sn, sc, sh, sw) and dy bf16 [B*P*Q][64] (16-B aligned).
  * Deterministic: per-workgroup partials into slab (dfu_stem_wgrad_ws_bytes bytes), summed in a
- * fixed order.  The 7x7/s2/p3 3 -> 64 stem with P*Q % 128 == 0, Q >= 64, Q % 8 == 0, W <= 250. */
+ * fixed order.  The 7x7/s2/p3 3 -> 64 stem with P even, Q % 16 == 0, Q <= 112, W <= 250. */
 int64_t dfu_stem_wgrad_ws_bytes(int32_t B, int32_t H, int32_t W);
 int dfu_stem_wgrad_x3(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int32_t B,
                       int32_t C, int32_t H, int32_t W, const void* dy, int32_t K, int32_t R,

@@ -1,6 +1,7 @@
 """Time the parity mode's stem conv at B = 64: the fused implicit-GEMM kernel
 (dfu_stem_conv_x3) against the pair im2col + split weights + interleaved-pair GEMM it
-replaces.  python tools/stem_time.py"""
+replaces; and its weight gradient from x (dfu_stem_wgrad_x3) against the MN x MN GEMM over the
+hi im2col rows.  python tools/stem_time.py"""
 import os
 import sys
 
@@ -35,8 +36,23 @@ def new_nocol():
     ops.stem_conv_x3(x, w, want_col=False)
 
 
+dy = (torch.randn(M, 64, device="cuda") * 0.1).to(torch.bfloat16)
+col = ops.im2col_f32(x, 7, 7, 2, 3, 160)[0]
+dw = torch.zeros(64, 147, device="cuda")
+
+
+def wgrad_gemm():
+    ops.gemm(64, 147, M, dy, 64, col, 160, dw, 147, a_mode=L.OPND_MNMAJOR,
+             b_mode=L.OPND_MNMAJOR, epilogue=L.EPI_F32_ACC)
+
+
+def wgrad_x():
+    ops.stem_wgrad_x3(x, dy, dw)
+
+
 for name, fn in (("pair im2col + GEMM", old), ("fused stem kernel", new),
-                 ("fused, no col rows", new_nocol)):
+                 ("fused, no col rows", new_nocol), ("wgrad: GEMM over col", wgrad_gemm),
+                 ("wgrad: from x", wgrad_x)):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
