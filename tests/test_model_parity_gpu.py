@@ -197,12 +197,13 @@ def _grad_errors(grads, ref_m, other_m=None):
 
 
 # fixed gradient bars (the backward is bf16): every parameter, and the median
-GRAD_REL_MAX, GRAD_COS_MIN, GRAD_REL_MEDIAN = 0.3, 0.95, 0.03
+# (round 5: tightened from 0.3 / 0.95; measured worst 0.186 / 0.983 bf16x3, 0.159 / 0.987 parity)
+GRAD_REL_MAX, GRAD_COS_MIN, GRAD_REL_MEDIAN = 0.25, 0.975, 0.03
 
 
 def test_c3_grads_bf16x3_vs_fp32_oracle(c3):
     """Parameter gradients of the bf16x3 step against the fp32 oracle at C3 (default init),
-    FIXED bars: rel L2 <= 0.3 and cosine >= 0.95 for every parameter, median rel <= 0.03.
+    FIXED bars: rel L2 <= 0.25 and cosine >= 0.975 for every parameter, median rel <= 0.03.
     (The bf16-rounded oracle itself misses these by far on the early BN parameters -- rel
     1.2-1.6: its forward is chaotic at this init -- which is why the forward is bf16x3 here.)"""
     f32, emu, h = c3["f32"], c3["emu"], c3["x3"]
