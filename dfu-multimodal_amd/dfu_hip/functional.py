@@ -44,11 +44,14 @@ F32 = torch.float32
 # "fp16" (a ViT Block stage only): the block's four Linears and its attention on fp16 MFMA
 #   operands (11-bit significands, fp32 accumulate; fp32 residual stream, LayerNorm statistics
 #   and softmax), writing the same bf16 tensors for the bf16 backward.
-# "parity": the headline mode -- per stage the precision its module class names in
-#   ``dfu_parity_precision``: every ResNet stage bf16x3, every ViT Block fp16 (the cheapest
-#   assignment measured to keep the fusion logits within north_star's 1e-3 of the fp32 oracle
-#   with margin: profiles/r16a_precision_grid.json, profiles/r19_precision_study.json).  A
-#   model may override a stage's class default on the instance (models.single.ThermalOnlyModel).
+# "parity": the headline mode -- per stage the precision named by its ``dfu_parity_precision``
+#   (bf16x3 where unset): every ResNet stage bf16x3; ViT Blocks as their VisionTransformer
+#   assigns them per role (models/vit.py ``_parity_policy``): every Block fp16 in a ViT a
+#   fusion model marks as its feature extractor, Blocks 0-8 bf16x3 and 9-11 fp16 otherwise --
+#   the cheapest assignments measured to keep the logits within north_star's 1e-3 of the fp32
+#   oracle with margin (profiles/r16a_precision_grid.json, profiles/r19_precision_study.json,
+#   profiles/r20_c2_precision_study.txt).  A user may set ``dfu_parity_precision`` on a stage
+#   instance; the ViT's policy leaves such an override alone.
 # "mixed": per stage -- a ResNet Bottleneck / ViT Block (or the ResNet module itself, for the
 #   stem) runs its ``dfu_precision`` attribute's mode ("bf16", "bf16x3", ViT Blocks also
 #   "fp16"), bf16x3 where unset (models.precision.apply_policy sets the attributes).  A bf16 or
@@ -249,6 +252,9 @@ def new_stream(idx, priority=0):
     Never returned to torch's stream pool: a stream a failed graph capture left capturing is
     retired (dfu_hip.graphs) and this makes a fresh one."""
     import ctypes
+    # hipStreamCreate is not a capturable call: under a global-mode capture it invalidates the
+    # capture of every stream forked into it (dfu_hip.graphs)
+    ops.refuse_in_capture("a new library stream")
     h = ctypes.c_void_p(0)
     with torch.cuda.device(idx):
         L.check(L.load().dfu_stream_create(int(priority), ctypes.byref(h)), "dfu_stream_create")

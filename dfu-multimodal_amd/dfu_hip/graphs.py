@@ -18,13 +18,26 @@ import torch
 
 from . import _lib as L
 from . import functional as Fn
+from . import ops
+
+
+def _seen_streams():
+    """The streams library launches went to during the capture being recorded (ops.stream_ptr),
+    as torch streams -- user streams the step forked onto included."""
+    seen = ops._capture_seen
+    if not seen:
+        return []
+    return [torch.cuda.ExternalStream(raw, device=torch.device("cuda", dev))
+            for dev, raw in sorted(seen)]
 
 
 def step_streams(device=None, extra=()):
     """Every stream a DFU step may enqueue on: the current one, the encoder side streams, the
-    ViT weight-gradient streams, and `extra`."""
+    ViT weight-gradient streams, the streams library launches went to during the capture in
+    progress, and `extra`."""
     out = [torch.cuda.current_stream(device)]
     out += list(Fn._side_streams.values()) + list(Fn._wgrad_streams.values()) + list(extra)
+    out += _seen_streams()
     seen, uniq = set(), []
     for s in out:
         if s.cuda_stream not in seen:
@@ -46,7 +59,11 @@ def join_forked(origin, extra=()):
     fork of this capture), so work left on a side stream joins the graph instead of failing
     the capture as unjoined -- which HIP cannot undo: the origin's hipStreamEndCapture then
     returns hipErrorStreamCaptureUnjoined and leaves the origin and its forks capturing for
-    good (a second end returns hipErrorStreamCaptureWrongThread; tools/diag)."""
+    good (a second end returns hipErrorStreamCaptureWrongThread; tools/diag).  The step streams
+    include every stream a library launch went to during this capture, so a fork onto a plain
+    torch stream that the step did not join back (the C5 split-graph
+    attempt's crash at hipStreamEndCapture) is joined here too; only non-library work on a
+    stream the library never saw can still leave a fork unjoined."""
     for s in step_streams(extra=extra):
         if s.cuda_stream != origin.cuda_stream and capture_status(s) == 1:
             origin.wait_stream(s)
@@ -115,11 +132,21 @@ def try_capture(step, log=None, pool=None):
     if cap is None:
         cap = _capture_streams[prev.device_index] = Fn.new_stream(prev.device_index)
     cap.wait_stream(prev)
+    # the capture stream's split-K tile counters exist before the capture: created inside it,
+    # their zero-fill would be recorded into this graph and run only at its replays
+    with torch.cuda.stream(cap):
+        ops.tile_counters(cap.device)
     g = torch.cuda.CUDAGraph()
+    ops._capture_seen = set()
     try:
         with torch.cuda.graph(g, pool=pool, stream=cap):
-            step()
-            join_forked(cap)
+            try:
+                step()
+            finally:
+                # also when step() raised (a DfuError refusing a non-capturable call): joined
+                # forks let torch.cuda.graph's hipStreamEndCapture succeed, so the failure is a
+                # Python exception and the streams are clean for the eager fallback
+                join_forked(cap)
         return g
     except Exception as e:  # noqa: BLE001 -- any capture failure falls back to eager
         # torch.cuda.graph.__exit__ leaves its capture stream current when capture_end raises
@@ -135,3 +162,5 @@ def try_capture(step, log=None, pool=None):
             log(msg)
         del g
         return None
+    finally:
+        ops._capture_seen = None

@@ -24,14 +24,37 @@ _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 _cur_device = getattr(torch._C, "_cuda_getDevice", None)
 
 
+# (device, raw stream) of every launch while dfu_hip.graphs.try_capture records a graph (None
+# otherwise): the capture joins each of these streams that is still capturing into its origin
+# before hipStreamEndCapture, so library work a step left on a stream it forked -- a plain torch
+# stream included -- becomes part of the graph instead of failing the capture as unjoined.
+_capture_seen = None
+
+
 def stream_ptr():
     """The current HIP stream of the current device (the raw-pointer query: torch.cuda.
     current_stream() builds a Stream object per call, ~8 us of host time x ~260 calls a step).
     Pointers go to the C ABI as plain ints (ctypes converts them for c_void_p parameters:
     0.4 us per argument less than a c_void_p object, ~2000 arguments a step)."""
     if _raw_stream is not None and _cur_device is not None:
-        return _raw_stream(_cur_device())
-    return torch.cuda.current_stream().cuda_stream
+        dev = _cur_device()
+        s = _raw_stream(dev)
+    else:
+        st = torch.cuda.current_stream()
+        dev, s = st.device_index, st.cuda_stream
+    if _capture_seen is not None:
+        _capture_seen.add((dev, s))
+    return s
+
+
+def refuse_in_capture(what):
+    """Raise DfuError when the current stream is recording a graph: `what` would either
+    invalidate the capture (a stream creation is not a capturable call) or leave state that
+    only a replay initialises (a zero-fill recorded into the graph)."""
+    if torch.cuda.is_current_stream_capturing():
+        stream_ptr()  # a fork with no library launch yet: join_forked must still see it
+        raise L.DfuError(f"{what} requested inside a HIP-graph capture: run the step once "
+                         f"eagerly on the same streams before capturing it")
 
 
 def ptr(t):
@@ -160,17 +183,31 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, a_mode=L.OPND_KMAJOR, b_mode=L.OPND_KM
 
 
 _COUNTERS = {}
+_COUNTER_POOLS = {}  # device index -> [zeroed pool, next free slot]
 TILE_COUNTERS = 1 << 16
+COUNTER_SLOTS = 64  # streams per pool (64 x 256 KiB)
 
 
 def tile_counters(device):
     """Per-stream zeroed int32 tile counters for the in-kernel split-K reduction (every launch
-    returns them zeroed; launches on one stream never overlap)."""
+    returns them zeroed; launches on one stream never overlap).  A stream's counters are a slot
+    of a per-device pool zeroed when the pool is made, so a stream first seen inside a graph
+    capture takes a slot by host bookkeeping alone (a zero-fill made inside the capture would be
+    recorded into the graph and run only at its replays: eager launches on that stream before
+    the first replay would read uninitialised counters)."""
     st = torch.cuda.current_stream(device)
     key = (st.device_index, st.cuda_stream)
     t = _COUNTERS.get(key)
     if t is None:
-        t = _COUNTERS[key] = torch.zeros(TILE_COUNTERS, dtype=torch.int32, device=device)
+        pool = _COUNTER_POOLS.get(st.device_index)
+        if pool is None or pool[1] == COUNTER_SLOTS:
+            refuse_in_capture(f"a fresh pool of split-K tile counters (stream "
+                              f"{st.cuda_stream:#x})")
+            pool = _COUNTER_POOLS[st.device_index] = [
+                torch.zeros(COUNTER_SLOTS * TILE_COUNTERS, dtype=torch.int32, device=device), 0]
+        i = pool[1]
+        pool[1] += 1
+        t = _COUNTERS[key] = pool[0][i * TILE_COUNTERS:(i + 1) * TILE_COUNTERS]
     return t
 
 

@@ -24,6 +24,7 @@ view) and ``p.grad`` into a matching flat gradient buffer, so:
     ``FlatParams.refresh_shadow()`` after those.
 """
 import os
+import warnings
 import weakref
 
 import torch
@@ -154,7 +155,16 @@ class FlatParams:
             return
         self.x3_lo = self.offsets[idx[0]]
         self.x3_hi = self.offsets[idx[-1]] + _aligned(self.params[idx[-1]].numel())
-        self.shadow_x3 = torch.empty(2 * (self.x3_hi - self.x3_lo), dtype=torch.bfloat16,
+        # the span also covers any parameter registered between the first and last x3 weight
+        # (contiguous in the reference ResNet: BN vectors only); report a model whose span
+        # carries much more than its conv weights
+        covered = sum(_aligned(self.params[i].numel()) for i in idx)
+        self.x3_extra = (self.x3_hi - self.x3_lo) - covered
+        if self.x3_extra > max(1 << 20, covered // 10):
+            warnings.warn(f"FusedAdamW x3 shadow: the conv-weight span holds {self.x3_extra} "
+                          f"elements of other parameters beside {covered} conv-weight "
+                          f"elements (4 B of memory and AdamW writes each per step)")
+        self.shadow_x3 =torch.empty(2 * (self.x3_hi - self.x3_lo), dtype=torch.bfloat16,
                                      device=self.data.device)
         for i in idx:
             p, o = self.params[i], self.offsets[i]

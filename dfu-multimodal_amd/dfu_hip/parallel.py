@@ -118,12 +118,14 @@ class GradAllReducer:
                 cur, lo, hi = set(), None, None
         if cur:
             self.buckets.append((lo, hi, cur))
+        self._bucket_of = {pid: k for k, b in enumerate(self.buckets) for pid in b[2]}
+        self._views = None  # (flat.grad, bucket views), built on first launch
         self._pending = None
         self._issued = None
         self._hook = None
         self._works = []
         self.issue_log = []  # bucket indices in launch order (ranks must agree: RCCL pairs them)
-        self.carriers = {}  # id(stream) -> stream: the streams collectives were issued from
+        self.carriers = {}  # stream handle -> stream: the streams this step's collectives used
         if self.overlap:
             self._hook = Fn.register_grad_ready_hook(self._on_ready)
 
@@ -135,7 +137,11 @@ class GradAllReducer:
         # streams it drew gradients from (event recorded when the producer switched away)
         self._last = [None] * len(self.buckets)
         self._marks = [{} for _ in self.buckets]
+        # per bucket: some gradient came from several or unknown streams (its
+        # producers have no event in _marks, so the bucket must join every gradient stream)
+        self._unknown = [False] * len(self.buckets)
         self._works = []
+        self.carriers = {}
 
     def _producer(self, p):
         if not self.cuda:
@@ -144,6 +150,8 @@ class GradAllReducer:
         return st if st else False  # False: several (or unknown) producer streams
 
     def _note(self, k, st):
+        if st is False:
+            self._unknown[k] = True
         prev = self._last[k]
         if prev is not None and prev is not st and prev is not False:
             ev = torch.cuda.Event()
@@ -151,18 +159,28 @@ class GradAllReducer:
             self._marks[k][id(prev)] = (prev, ev)
         self._last[k] = st
 
+    def _carrier(self, k, carrier):
+        """The stream bucket k's collective is issued from, or None when every gradient
+        stream must join the caller's stream first: the last producer is unknown, or an
+        earlier gradient of the bucket had several / unknown producers."""
+        if carrier is None or carrier is False or self._unknown[k]:
+            return None
+        return carrier
+
     def _launch(self, k, carrier=None):
-        lo, hi, _ = self.buckets[k]
-        view = self.flat.grad[lo:hi]
+        g = self.flat.grad
+        if self._views is None or self._views[0] is not g:
+            self._views = (g, [g[lo:hi] for lo, hi, _ in self.buckets])
+        view = self._views[1][k]
         if self.cuda:
-            if carrier is None or carrier is False:
-                # unknown producers: every gradient stream joins the caller's stream first
+            carrier = self._carrier(k, carrier)
+            if carrier is None:
                 carrier = torch.cuda.current_stream()
                 Fn.join_grad_streams(carrier, clear=False)
             for sid, (st, ev) in self._marks[k].items():
                 if st is not carrier:
                     carrier.wait_event(ev)
-            self.carriers[id(carrier)] = carrier
+            self.carriers[carrier.cuda_stream] = carrier
             with torch.cuda.stream(carrier):
                 self._works.append(self._reduce(view))
         else:
@@ -175,18 +193,20 @@ class GradAllReducer:
         return dist.all_reduce(view, op=op, group=self.group, async_op=True)
 
     def _on_ready(self, p):
-        if self._pending is None:
+        pending = self._pending
+        if pending is None:
             return
         pid = id(p)
-        for k, pend in enumerate(self._pending):
-            if pid in pend:
-                pend.discard(pid)
-                st = self._producer(p)
-                if st is not None:
-                    self._note(k, st)
-                if not pend and not self._issued[k]:
-                    self._launch(k, st)
-                break
+        k = self._bucket_of.get(pid)
+        if k is None or pid not in pending[k]:
+            return
+        pend = pending[k]
+        pend.discard(pid)
+        st = self._producer(p) if self.cuda else None
+        if st is not None:
+            self._note(k, st)
+        if not pend and not self._issued[k]:
+            self._launch(k, st)
 
     def finish(self):
         Fn.join_grad_streams()

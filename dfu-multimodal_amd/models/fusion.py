@@ -103,6 +103,9 @@ class MultimodalFusionModel(tnn.Module):
         rgb = resnet50(pretrained=pretrained)
         rgb.fc = tnn.Identity()
         th = vit_base_patch16_224(pretrained=pretrained, num_classes=0)
+        # the ViT's 768 features reach the logits only through the 2816-wide fusion head, whose
+        # dilution keeps fp16 Blocks inside the parity margin (models/vit.py _parity_policy)
+        th.dfu_feature_extractor = True
         if layout == "eval":
             self.resnet = rgb
             self.vit = th

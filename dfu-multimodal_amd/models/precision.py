@@ -7,8 +7,10 @@ operands and activations), "bf16x3" (fp32-accurate split-bf16 operands) or, for 
 mode.
 
   * functional.precision("parity") -- the headline mode and the library default -- runs each
-    stage at its ``dfu_parity_precision``: ResNet stages bf16x3, ViT Blocks fp16.  It is the
-    cheapest assignment the per-stage study found to keep the fusion logits within half of
+    stage at its ``dfu_parity_precision``: ResNet stages bf16x3; ViT Blocks fp16 when a fusion
+    model marks the ViT as its feature extractor (mark_feature_extractor), Blocks 0-8 bf16x3
+    and 9-11 fp16 otherwise (models/vit.py _parity_policy).  The fusion assignment is the
+    cheapest the per-stage study found to keep the fusion logits within half of
     north_star's 1e-3 of the fp32 oracle on every seed (profiles/r16a_precision_grid.json,
     profiles/r16b_precision_study.json, profiles/r19_precision_study.json,
     tools/precision_policy_study.py): the random-init ResNet amplifies rounding ~30x more than
@@ -82,6 +84,22 @@ def parity_policy(model, vit_x3_blocks=0):
     return {n: ("bf16x3" if k < vit_x3_blocks else "fp16") for k, n in enumerate(names)}
 
 
+def mark_feature_extractor(model, on=True):
+    """Mark the ViT inside `model` (or `model` itself) as a fusion feature extractor: its
+    features reach the logits only through a late-fusion head beside the ResNet's 2048
+    (train_multimodal_fusion.py:305-313, grad_cam_visualization.py:289-302), so the "parity"
+    mode runs every Block fp16 (models/vit.py _parity_policy).  Unmarked, a ViT runs Blocks 0-8
+    bf16x3 -- the safe assignment for a ViT whose features feed a head directly.
+    models.fusion.MultimodalFusionModel marks its own ViT; a script that builds the fusion from
+    models.encoders.create_model(num_classes=0) and torch.cat may call this.  Returns the
+    model."""
+    _, v = encoders(model)
+    if v is None:
+        raise ValueError("mark_feature_extractor: no VisionTransformer in the model")
+    v.dfu_feature_extractor = bool(on)
+    return model
+
+
 def clear_policy(model):
     for m in stages(model).values():
         if "dfu_precision" in m.__dict__:
@@ -89,4 +107,5 @@ def clear_policy(model):
     return model
 
 
-__all__ = ["apply_policy", "clear_policy", "encoders", "parity_policy", "stages", "suffix"]
+__all__ = ["apply_policy", "clear_policy", "encoders", "mark_feature_extractor", "parity_policy",
+           "stages", "suffix"]

@@ -63,8 +63,9 @@ class Mlp(tnn.Module):
 
 
 class Block(tnn.Module):
-    # forward precision under functional.precision("parity") (models/precision.py)
-    dfu_parity_precision = "fp16"
+    # No class-level parity precision: a Block outside a VisionTransformer runs bf16x3 in the
+    # "parity" mode (functional.stage_mode's default); its VisionTransformer assigns the mode
+    # per role (VisionTransformer._parity_policy).
 
     def __init__(self, dim, num_heads, mlp_ratio=4.0, qkv_bias=True):
         super().__init__()
@@ -134,29 +135,38 @@ class VisionTransformer(tnn.Module):
     def get_classifier(self):
         return self.head
 
-    # The "parity" mode's Block precisions when this ViT classifies by itself (its head is not
-    # Identity: train_thermal_only.py:188-205, C2).  Its logits see the Blocks' rounding
-    # undiluted by a fusion head: with fp16 Blocks the thermal-only logits sit 1.0-1.6e-3 from
-    # the fp32 oracle (HIP 1.612e-3).  tools/c2_precision_study.py (CPU emulation of the fp16
-    # sites, five seeds; profiles/r20_c2_precision_study.txt): the first 1-3 Blocks bf16x3
-    # 6.6e-4-1.2e-3, the first 6 6.6e-4, the first 9 <= 3.7e-4, the first 11 <= 2.1e-4 --
-    # earlier Blocks' rounding is amplified by every later one -- and exact weights or
-    # LayerNorm outputs in the fp16 Blocks 5.5e-4-9.5e-4.  So the first 9 Blocks run bf16x3
-    # and the last 3 fp16: the cheapest assignment measured inside the 5e-4 margin.  As a
-    # fusion feature extractor (num_classes=0, head Identity) every Block keeps the class
-    # default, fp16 (fusion logits within 5e-4).
+    # The "parity" mode's Block precisions.  Safe by construction:
+    # unless a fusion model marks this ViT as a feature extractor whose 768 features are
+    # diluted by its 2816-wide head (``dfu_feature_extractor``, set by
+    # models.fusion.MultimodalFusionModel or models.precision.mark_feature_extractor), the
+    # ViT's output is assumed to reach logits undiluted -- its own head (C2,
+    # train_thermal_only.py:188-205) or a caller's head on ``num_classes=0`` features
+    # (notebooks/test_time_augmentation.py:99-104, models/models.py:15-22 + a Linear).  There
+    # every Block fp16 puts the logits 1.0-1.6e-3 from the fp32 oracle (HIP 1.612e-3);
+    # tools/c2_precision_study.py (CPU emulation of the fp16 sites, five seeds;
+    # profiles/r20_c2_precision_study.txt): the first 1-3 Blocks bf16x3 6.6e-4-1.2e-3, the
+    # first 6 6.6e-4, the first 9 <= 3.7e-4, the first 11 <= 2.1e-4 -- earlier Blocks'
+    # rounding is amplified by every later one.  So the first 9 Blocks run bf16x3 and the last
+    # 3 fp16: the cheapest assignment measured inside the 5e-4 margin.  A marked feature
+    # extractor runs every Block fp16 (fusion logits within 5e-4).
     classifier_x3_blocks = 9
+    dfu_feature_extractor = False
 
     def _parity_policy(self):
         """Set every Block's parity-mode precision for this ViT's role (see above); called at
-        the top of each forward, since the reference scripts replace ``head`` after
-        construction (train_thermal_only.py:188-205)."""
-        alone = not isinstance(self.head, tnn.Identity)
+        the top of each forward, since the reference scripts replace ``head`` or mark the ViT
+        after construction.  Only attributes this method wrote are replaced: a
+        ``dfu_parity_precision`` a user set on a Block instance is left alone."""
         for k, blk in enumerate(self.blocks):
-            if alone:
-                blk.dfu_parity_precision = "bf16x3" if k < self.classifier_x3_blocks else "fp16"
-            elif "dfu_parity_precision" in blk.__dict__:
-                del blk.dfu_parity_precision
+            mine = blk.__dict__.get("_dfu_policy_precision")
+            if blk.__dict__.get("dfu_parity_precision", mine) != mine:
+                continue  # the user's per-instance override
+            if self.dfu_feature_extractor:
+                mode = "fp16"
+            else:
+                mode = "bf16x3" if k < self.classifier_x3_blocks else "fp16"
+            blk.dfu_parity_precision = mode
+            blk._dfu_policy_precision = mode
 
     def _embed(self, x):
         pe = self.patch_embed

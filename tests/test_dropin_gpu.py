@@ -139,6 +139,92 @@ def test_c3_fusion_construct_default_precision_b64():
              steps_after=1, bar=5e-4)
 
 
+class _EncoderHead(nn.Module):
+    """A caller's own head on an encoder with no classifier: models/models.py:15-22's
+    ThermalViTEncoder + a Linear, or notebooks/test_time_augmentation.py:99-104's
+    ThermalOnlyModel (timm ViT with num_classes=0, then nn.Linear(768, 1))."""
+
+    def __init__(self, vit, out):
+        super().__init__()
+        self.vit = vit
+        self.classifier = nn.Linear(768, out)
+
+    def forward(self, x):
+        return self.classifier(self.vit(x))
+
+
+class _RefViTEncoder(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.vit = R.VisionTransformer(num_classes=0)
+
+    def forward(self, x):
+        return self.vit(x)
+
+
+def test_thermal_vit_encoder_with_caller_head_b64():
+    """ThermalViTEncoder() (head = Identity) followed by a caller's
+    nn.Linear(768, 2) is NOT a diluted fusion feature extractor: the default parity mode must
+    hold the 5e-4 margin at B = 64 (fp16 Blocks here gave 1.6e-3 before the policy inversion)."""
+    from models import models as M
+    torch.manual_seed(0)
+    ref = _EncoderHead(_RefViTEncoder(), 2)
+    hip = _EncoderHead(M.ThermalViTEncoder(pretrained=False), 2)
+    assert not hip.vit.vit.dfu_feature_extractor
+    _compare("ThermalViTEncoder + Linear(768, 2)", hip, ref, lambda r, t: (t,), B=64,
+             steps_after=1, bar=5e-4)
+    assert [b.dfu_parity_precision for b in hip.vit.vit.blocks] == ["bf16x3"] * 9 + ["fp16"] * 3
+
+
+def test_tta_create_model_num_classes0_linear1_b64():
+    """notebooks/test_time_augmentation.py:99-104: create_model(num_classes=0) then
+    nn.Linear(768, 1), run in eval mode as the TTA script does; logits within the 5e-4 margin
+    of the fp32 oracle at B = 64, no precision call."""
+    from dfu_hip import functional as Fn
+    from models import encoders
+    assert Fn.get_precision() == "parity"
+    torch.manual_seed(1)
+    ref = _EncoderHead(R.VisionTransformer(num_classes=0), 1).eval()
+    hip = _EncoderHead(encoders.create_model("vit_base_patch16_224", pretrained=False,
+                                             num_classes=0), 1)
+    hip.load_state_dict(ref.state_dict(), strict=True)
+    hip = hip.to(DEV).eval()
+    _, th, _ = R.synthetic_batch(64, seed=6)
+    with torch.no_grad():
+        out_r = ref(th)
+        out_h = hip(th.to(DEV))
+    torch.cuda.synchronize()
+    d = _maxd(out_h, out_r)
+    print(f"\n[TTA ViT num_classes=0 + Linear(768, 1), B=64] default-mode logits vs fp32 oracle "
+          f"{d:.3e} (bar 5e-4)")
+    assert d <= 5e-4
+
+
+def test_feature_extractor_mark_and_user_override():
+    """The fusion model marks its ViT (every Block fp16); the mark is an explicit opt-in for
+    script-built fusions (models.precision.mark_feature_extractor); a per-Block override set
+    by the user survives the policy."""
+    from models import encoders
+    from models import precision as P
+    from models.fusion import MultimodalFusionModel
+    m = MultimodalFusionModel(num_classes=2, dropout=0.0).to(DEV).train()
+    assert m.vit.dfu_feature_extractor
+    rgb, th, _ = R.synthetic_batch(2, seed=2)
+    m(rgb.to(DEV), th.to(DEV))
+    assert [b.dfu_parity_precision for b in m.vit.blocks] == ["fp16"] * 12
+    v = encoders.create_model("vit_base_patch16_224", num_classes=0).to(DEV)
+    v.blocks[10].dfu_parity_precision = "bf16x3"
+    P.mark_feature_extractor(v)
+    v(th.to(DEV))
+    got = [b.dfu_parity_precision for b in v.blocks]
+    assert got == ["fp16"] * 10 + ["bf16x3", "fp16"]
+    P.mark_feature_extractor(v, on=False)
+    v(th.to(DEV))
+    assert [b.dfu_parity_precision for b in v.blocks] == ["bf16x3"] * 9 + ["fp16", "bf16x3",
+                                                                          "fp16"]
+    torch.cuda.synchronize()
+
+
 def _fusion_step(clip, early):
     from dfu_hip import nn as hnn
     from dfu_hip.optim import FusedAdamW

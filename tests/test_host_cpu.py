@@ -223,3 +223,39 @@ def test_default_precision_is_the_parity_mode():
     with Fn.precision("bf16"):
         assert Fn.get_precision() == "bf16"
     assert Fn.get_precision() == "parity"
+
+
+def test_vit_parity_policy_safe_by_construction():
+    """a ViT runs Blocks 0-8 bf16x3 in the parity mode unless a fusion
+    model marks it as its feature extractor -- whichever object holds the head (ViT head,
+    Identity head + a caller's Linear, ThermalViTEncoder).  Only the policy's own attributes
+    are rewritten."""
+    from dfu_hip import functional as Fn
+    from models import encoders
+    from models import models as M
+    from models import precision as P
+    from models.fusion import MultimodalFusionModel
+    safe = ["bf16x3"] * 9 + ["fp16"] * 3
+
+    def modes(v):
+        v._parity_policy()
+        return [Fn.stage_mode(b) for b in v.blocks]
+
+    assert modes(encoders.create_model("vit_base_patch16_224", num_classes=2)) == safe
+    assert modes(encoders.create_model("vit_base_patch16_224", num_classes=0)) == safe
+    assert modes(M.ThermalViTEncoder().vit) == safe
+    for layout in ("eval", "train"):
+        m = MultimodalFusionModel(layout=layout)
+        _, v = P.encoders(m)
+        assert v.dfu_feature_extractor and modes(v) == ["fp16"] * 12
+    v = encoders.create_model("vit_base_patch16_224", num_classes=0)
+    P.mark_feature_extractor(v)
+    assert modes(v) == ["fp16"] * 12
+    v.blocks[3].dfu_parity_precision = "bf16x3"  # a user's per-instance override
+    P.mark_feature_extractor(v, on=False)
+    assert modes(v) == safe
+    P.mark_feature_extractor(v)
+    assert modes(v)[3] == "bf16x3" and modes(v).count("fp16") == 11
+    from models.resnet import ResNet
+    with pytest.raises(ValueError):
+        P.mark_feature_extractor(ResNet())

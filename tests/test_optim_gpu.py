@@ -129,3 +129,26 @@ def test_x3_pair_shadow_tracks_conv_weights():
     with torch.no_grad():  # an edit outside the optimizer bumps the version: re-split
         convs[1].mul_(0.5)
     assert torch.equal(Fn.conv_weight_x3(convs[1]), want(convs[1]))
+
+
+def test_x3_span_holds_only_conv_weights_in_the_fusion_model():
+    """the x3 shadow covers the flat span from the first to the last x3 conv
+    weight.  In the fusion model that span holds the ResNet's BN vectors only (a few 10^4
+    elements beside 23.5M); a model that registers a large parameter between its convs is
+    reported."""
+    import warnings
+    from dfu_hip.optim import FusedAdamW
+    from models.fusion import MultimodalFusionModel
+    model = MultimodalFusionModel(num_classes=2, dropout=0.0).to(DEV)
+    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        opt.flat.enable_x3()
+    span = opt.flat.x3_hi - opt.flat.x3_lo
+    print(f"\n[x3 span] {span} elements, {opt.flat.x3_extra} of them not x3 conv weights")
+    assert 23_000_000 < span < 24_000_000 and opt.flat.x3_extra < 100_000
+    ps = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in
+          [(64, 64, 1, 1), (4096, 1024), (64, 64, 1, 1)]]
+    opt2 = FusedAdamW(ps, lr=1e-4)
+    with pytest.warns(UserWarning, match="x3 shadow"):
+        opt2.flat.enable_x3()

@@ -71,7 +71,7 @@ def test_bucket_ready_points_are_final():
         Fn.remove_grad_ready_hook(hook)
 
 
-def _dp_worker(rank, port, q):
+def _dp_worker(rank, port, overlap, q):
     """One rank of a world-2 data-parallel step on the real fusion model, both ranks on cuda:0
     over gloo (CUDA tensors; RCCL needs one GPU per rank).  The GPU is touched only here, after
     the spawn."""
@@ -117,8 +117,10 @@ def _dp_worker(rank, port, q):
 
         step()  # this rank's own gradient (no exchange)
         local = opt.flat.grad.clone()
-        red = parallel.GradAllReducer(opt.flat, overlap=True)
-        step(red)  # overlapped bucketed all-reduce launched from the grad-ready hooks
+        red = parallel.GradAllReducer(opt.flat, overlap=overlap)
+        # overlap: bucketed all-reduce launched from the grad-ready hooks; otherwise every
+        # bucket from finish() (bench's graph mode at world > 1)
+        step(red)
         nstreams = len({s.cuda_stream for s in streams.values()})
         ncarriers = len(red.carriers)
         got = opt.flat.grad.clone()
@@ -142,7 +144,8 @@ def _dp_worker(rank, port, q):
             dist.destroy_process_group()
 
 
-def test_fusion_dp_world2_overlapped_reducer():
+@pytest.mark.parametrize("overlap", [True, False])
+def test_fusion_dp_world2_overlapped_reducer(overlap):
     """SURVEY §8e check on the real fusion model with overlap=True: the
     averaged gradients equal the mean of the per-rank gradients, both ranks issue the buckets
     in the same order (every one from the hooks), and hold identical averaged gradients.  The
@@ -157,7 +160,7 @@ def test_fusion_dp_world2_overlapped_reducer():
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_worker, args=(r, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, port, overlap, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -169,7 +172,7 @@ def test_fusion_dp_world2_overlapped_reducer():
         p.join(timeout=60)
         assert p.exitcode == 0
     a, b = res[0], res[1]
-    print(f"\n[DP world 2] buckets {a['nbuckets']}, issue order r0 {a['log']} r1 {b['log']}; "
+    print(f"\n[DP world 2, overlap={overlap}] buckets {a['nbuckets']}, issue order r0 {a['log']} r1 {b['log']}; "
           f"max |avg - mean(local)| {a['diff']:.2e} / {b['diff']:.2e} (scale {a['scale']:.2e})")
     print(f"  streams used (grad producers + collective carriers): {a['nstreams']} / "
           f"{b['nstreams']}; carriers {a['ncarriers']}")
