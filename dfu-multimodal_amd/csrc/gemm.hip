@@ -40,9 +40,6 @@ int g_persistent = getenv("DFU_GEMM_PERSISTENT") ? atoi(getenv("DFU_GEMM_PERSIST
 int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
 const int g_wide_reduce = getenv("DFU_GEMM_WIDE_REDUCE") ? atoi(getenv("DFU_GEMM_WIDE_REDUCE")) : 1;
-// A/B (env): pad the persistent 256x256 / 192x256 launches' LDS to the CU's 160 KiB, so no other
-// kernel's workgroup co-resides on their CUs -- 1: the fp16 (forward) launches, 2: all of them
-const int g_ps_pad = getenv("DFU_PS_PAD") ? atoi(getenv("DFU_PS_PAD")) : 0;
 int g_tail_split = 1;       // dfu_gemm_set_tail_split
 
 const Entry* find_entry(int a, int b, int e, int tile) {
@@ -646,10 +643,7 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   const int units = a.tail_r ? a.tail_full + a.tail_r * a.tail_s : a.tiles_m * a.tiles_n * splits;
   const bool atomics = acc_epi && splits > 1 && a.slab == nullptr;
   const int nwg = (g_persistent && !atomics && units > slots) ? slots : units;
-  const bool ps = pl.tile == T256x256ps || pl.tile == T192x256ps;
-  const unsigned pad = ps && (g_ps_pad == 2 || (g_ps_pad == 1 && d->operand_type == 1))
-                           ? 163840u - (unsigned)pl.entry->lds_bytes : 0u;
-  hipLaunchKernelGGL(pl.entry->fn, dim3(nwg), dim3(pl.entry->threads), pad, s, a);
+  hipLaunchKernelGGL(pl.entry->fn, dim3(nwg), dim3(pl.entry->threads), 0, s, a);
   DFU_LAUNCH_CHECK();
   if (a.slab != nullptr && a.counters == nullptr) {
     const int64_t n = (int64_t)d->M * d->N;
