@@ -88,13 +88,20 @@ def profile(steps=5):
     for _ in range(3):
         step()
     torch.cuda.synchronize()
+    # the autograd engine runs CUDA backward nodes on its own device thread, which cProfile
+    # (per thread) does not see: run them on this thread for the profile
+    torch.autograd.set_multithreading_enabled(False)
+    step()
+    torch.cuda.synchronize()
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(steps):
         step()
     pr.disable()
     torch.cuda.synchronize()
-    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(45)
+    st.sort_stats("cumulative").print_stats(45)
 
 
 if __name__ == "__main__":
