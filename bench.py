@@ -28,6 +28,7 @@ import torch.distributed as dist  # noqa: E402
 # Algorithmic GEMM/conv FLOPs per unit of work (fwd + dgrad + wgrad), SURVEY.md §8(d)
 FLOPS_PER_UNIT = {"fusion": 129.44e9, "thermal": 105.15e9, "rgb": 24.29e9, "gradcam": 173.20e9}
 PEAK_BF16_TFLOPS = 2500.0
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 PRECISION_NOTE = {
     "parity": "the library default.  forward: ResNet50 bf16x3 (split-bf16 MFMA, fp32-accurate), "
               "ViT-B/16 Blocks fp16 MFMA inside the fusion model (fp32 accumulate / residual / "
@@ -312,7 +313,23 @@ def gemm_roofline(fwd_bwd, tail, replays=3):
     executed = sum(r[4] for r in rec)
     nbytes = sum(r[2] for r in rec)
     n = len(rec)
+    # each launch priced at its OWN bound: the MFMA time of the work it executes at the dense
+    # peak, or the HBM time of its compulsory bytes at 8 TB/s, whichever is longer (the layer-1
+    # convolutions and the split-K weight gradients of small planes are HBM-bound, the ViT
+    # linears MFMA-bound); their sum over the measured replay time is the family's fraction of
+    # its per-launch roofline
+    t_mfma = [r[4] / (PEAK_BF16_TFLOPS * 1e12) for r in rec]
+    t_hbm = [r[2] / (PEAK_HBM_GBS * 1e9) for r in rec]
+    bound_us = sum(max(a, b) for a, b in zip(t_mfma, t_hbm)) * 1e6
+    per_launch = {"frac": round(bound_us / us, 4), "bound_us_per_step": round(bound_us, 1),
+                  "measured_us_per_step": round(us, 1),
+                  "mfma_bound_launches": sum(1 for a, b in zip(t_mfma, t_hbm) if a >= b),
+                  "hbm_bound_launches": sum(1 for a, b in zip(t_mfma, t_hbm) if a < b),
+                  "basis": f"sum over the step's launches of max(executed MFMA FLOPs / "
+                           f"{PEAK_BF16_TFLOPS:.0f} TFLOP/s, algorithmic bytes / "
+                           f"{PEAK_HBM_GBS:.0f} GB/s) / replay time"}
     return {"launches_per_step": n, "avg_launch_us": us / n, "flops_per_launch": flops / n,
+            "per_launch_roofline": per_launch,
             "bytes_per_launch": nbytes / n, "gemm_ms_per_step": us / 1e3,
             "achieved": flops / (us * 1e-6) / 1e12,
             "mfma_executed": executed / (us * 1e-6) / 1e12,
@@ -552,8 +569,8 @@ def main_pipeline(args, rank, world, dev):
                        "per_gpu_batch": args.batch, "source": f"{W0}x{H0}",
                        "parallelism": f"replicas{args.gpus}", "dist": args.dist},
             "pcie_inclusive_pairs_per_sec": round(incl, 1),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0,
-                         "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
                          "kernel": "augment pipeline (8 launches per step: 2 resize passes, "
                                    "contrast statistics, gather/normalise, per modality)",
                          "algorithmic_bytes_per_pair": per_pair},
@@ -882,6 +899,7 @@ def main():
                          "mfma_executed_tflops": round(gr["mfma_executed"], 1),
                          "x3_launches_per_step": gr["x3_launches"],
                          "gemm_ms_per_step": round(gr["gemm_ms_per_step"], 3),
+                         "per_launch_roofline": gr["per_launch_roofline"],
                          "step": {"achieved": round(achieved, 1),
                                   "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                                   "basis": f"{FLOPS_PER_UNIT[args.config] / 1e9:.2f} GFLOP per "
