@@ -181,3 +181,100 @@ def test_fusion_dp_world2_overlapped_reducer(overlap):
     for d in (a, b):
         assert d["diff"] <= 1e-6 * max(d["scale"], 1e-30)
     assert a["sum"] == b["sum"] and a["sq"] == b["sq"] and (a["sample"] == b["sample"]).all()
+
+
+def _dp_oracle_worker(rank, port, q, B):
+    """One rank of a world-2 data-parallel step (gloo, both ranks on cuda:0): the HIP fusion
+    model in the library default precision on this rank's batch, gradients averaged by the
+    overlapped reducer; beside it the fp32 CPU oracle on the same batch and weights, its
+    gradients averaged over the ranks too ("compare against N independent
+    per-rank CPU computations averaged")."""
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE="2", LOCAL_RANK=str(rank))
+    try:
+        import copy
+        from dfu_hip import functional as Fn
+        from dfu_hip import nn as hnn
+        from dfu_hip.optim import FusedAdamW
+        from models.fusion import MultimodalFusionModel
+        from oracle import torch_ref as R
+        parallel.init_from_env(backend="gloo")
+        torch.set_num_threads(8)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        torch.manual_seed(0)  # the same initial replica on both ranks
+        ref = R.MultimodalFusionModel(num_classes=2, dropout=0.0)
+        hip = MultimodalFusionModel(num_classes=2, dropout=0.0)
+        hip.load_state_dict(ref.state_dict(), strict=True)
+        hip = hip.to(dev).train()
+        rgb, th, y = R.synthetic_batch(B, seed=42 + rank)  # each rank its own batch
+        w = torch.tensor([2.0, 2.0])
+        opt = FusedAdamW(hip.parameters(), lr=1e-4, weight_decay=1e-4)
+        red = parallel.GradAllReducer(opt.flat, overlap=True)
+        opt.zero_grad()
+        red.start()
+        loss = hnn.CrossEntropyLoss(weight=w.to(dev))(hip(rgb.to(dev), th.to(dev)), y.to(dev))
+        loss.backward()
+        Fn.join_grad_streams()
+        red.finish()
+        torch.cuda.synchronize()
+        got = {n: p.grad.detach().float().cpu().clone() for n, p in hip.named_parameters()}
+        red.close()
+        # the oracle on this rank's batch, then the mean over the ranks
+        m = copy.deepcopy(ref).train()
+        out = m(rgb, th)
+        torch.nn.functional.cross_entropy(out, y, weight=w).backward()
+        errs = []
+        for n, p in m.named_parameters():
+            g = p.grad.detach().clone()
+            dist.all_reduce(g)
+            g /= 2
+            if g.norm().item() == 0.0:
+                continue
+            h = got[n]
+            cos = torch.nn.functional.cosine_similarity(h.flatten().double(),
+                                                        g.flatten().double(), dim=0).item()
+            errs.append((((h - g).norm() / g.norm()).item(), cos, n))
+        errs.sort(reverse=True)
+        q.put((rank, dict(worst=errs[:5], median=errs[len(errs) // 2][0],
+                          min_cos=min(e[1] for e in errs), n=len(errs),
+                          checksum=float(sum(v.double().sum() for v in got.values()))), None))
+    except Exception as e:
+        import traceback
+        q.put((rank, None, traceback.format_exc() + repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_fusion_dp_world2_vs_mean_of_rank_oracles():
+    """VERDICT round 5 weak item 6 / SURVEY §8e: the averaged gradients of a world-2 step (two
+    ranks, own batches of 16, overlapped bucketed all-reduce) against the MEAN OF THE TWO RANKS'
+    fp32 CPU ORACLE gradients, under the single-rank parity test's fixed bars (rel L2 <= 0.25
+    and cosine >= 0.975 per parameter, median rel <= 0.03); both ranks hold the same average."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_oracle_worker, args=(r, port, q, 16)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, d, err = q.get(timeout=280)
+        assert err is None, f"rank {rank}: {err}"
+        res[rank] = d
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, d in sorted(res.items()):
+        print(f"\n[DP world 2 vs mean of rank oracles, rank {r}] {d['n']} params, median rel "
+              f"{d['median']:.3e}, min cos {d['min_cos']:.5f}, worst {d['worst'][:3]}")
+        assert d["median"] <= 0.03 and d["min_cos"] >= 0.975
+        assert all(e <= 0.25 for e, _, _ in d["worst"]), d["worst"]
+    assert res[0]["checksum"] == res[1]["checksum"]
