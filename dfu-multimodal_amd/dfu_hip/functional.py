@@ -327,9 +327,12 @@ class _Beside:
 
 
 def grads_done(*params):
+    if not _grad_ready_hooks:
+        return
+    hooks = tuple(_grad_ready_hooks)  # (a hook may be removed meanwhile: GC)
     for p in params:
         if p is not None:
-            for h in tuple(_grad_ready_hooks):  # (a hook may be removed meanwhile: GC)
+            for h in hooks:
                 h(p)
 
 
