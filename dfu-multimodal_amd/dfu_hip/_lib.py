@@ -81,6 +81,7 @@ PROTOTYPES = {
     "dfu_stream_capture_status": [P, P],
     "dfu_stream_create": [I32, P],
     "dfu_stream_destroy": [P],
+    "dfu_stream_wait": [P, P],
     "dfu_gemm": [ctypes.POINTER(GemmDesc), P],
     "dfu_gemm_stats_tiles": [I32],
     "dfu_gemm_workspace_bytes": [ctypes.POINTER(GemmDesc)],

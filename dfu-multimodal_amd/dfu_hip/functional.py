@@ -155,23 +155,10 @@ def grad_buffer(p):
     return g
 
 
-_stream_objs = {}
-_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
-
-
 def _current_stream_obj(t):
-    """The current stream of t's device as one cached torch Stream per (device, raw HIP stream)
-    (the per-call torch.cuda.current_stream() object costs ~8 us of host time; this is called
-    for every parameter gradient of the step).  A cached object is re-validated against the
-    raw handle, so a destroyed user stream whose address is reused gets a fresh object."""
-    if _raw_stream is None:
-        return torch.cuda.current_stream(t.device)
-    idx = t.get_device()
-    raw = _raw_stream(idx)
-    st = _stream_objs.get((idx, raw))
-    if st is None or st.cuda_stream != raw:
-        st = _stream_objs[(idx, raw)] = torch.cuda.current_stream(t.device)
-    return st
+    """The current stream of t's device as one cached torch Stream object (ops.current_stream;
+    called for every parameter gradient of the step)."""
+    return ops.current_stream(t.get_device())
 
 
 def join_grad_streams(stream=None, clear=True):
@@ -179,10 +166,10 @@ def join_grad_streams(stream=None, clear=True):
     gradients since the last clearing join."""
     if not _grad_streams:
         return
-    cur = stream if stream is not None else torch.cuda.current_stream()
+    cur = stream if stream is not None else ops.current_stream()
     for st in _grad_streams.values():
         if st != cur:
-            cur.wait_stream(st)
+            ops.stream_wait(cur, st)
     if clear:
         _grad_streams.clear()
 
@@ -215,7 +202,7 @@ def remove_backward_end_hook(fn):
 def arm_backward_join():
     if _join_armed[0] or not torch.cuda.is_available():
         return
-    target = torch.cuda.current_stream()
+    target = ops.current_stream()
     _join_armed[0] = True
 
     def _join():
@@ -314,13 +301,13 @@ class _Beside:
 
     def __init__(self, stream):
         self.ws = stream
-        self.cur = torch.cuda.current_stream() if stream is not None else None
+        self.cur = ops.current_stream() if stream is not None else None
 
     def run(self, fn, *tensors):
         if self.ws is None:
             return fn()
-        self.ws.wait_stream(self.cur)
-        with torch.cuda.stream(self.ws):
+        ops.stream_wait(self.ws, self.cur)
+        with ops.on_stream(self.ws):
             for t in tensors:
                 t.record_stream(self.ws)
             return fn()
@@ -334,6 +321,13 @@ def grads_done(*params):
         if p is not None:
             for h in hooks:
                 h(p)
+
+
+def module_param(mod, name):
+    """mod.<name> for a registered parameter by its dict (nn.Module.__getattr__, the slow path
+    for parameters, costs ~0.25 us an attribute); anything else by getattr."""
+    p = mod._parameters
+    return p[name] if name in p else getattr(mod, name)
 
 
 def _wants(p):
@@ -1433,7 +1427,7 @@ class TokenNormFn(torch.autograd.Function):
     def backward(ctx, g):
         if g.is_cuda:  # produced on the fusion head's stream; the ViT may run on a side stream
             arm_backward_join()
-            g.record_stream(torch.cuda.current_stream())
+            g.record_stream(ops.current_stream())
         x, mean, rstd = ctx.saved_tensors
         norm = ctx.norm
         B, T, D = x.shape

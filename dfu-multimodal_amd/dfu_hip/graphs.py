@@ -102,7 +102,7 @@ def reset_after_failed_capture(extra=()):
         raise RuntimeError("dfu: the caller's stream is still capturing after a failed capture")
     Fn._grad_streams.clear()
     Fn._join_armed[0] = False
-    Fn._stream_objs.clear()
+    ops._stream_objs.clear()
     try:  # can the process run eager work again?  (an allocation + a kernel + a host sync)
         torch.empty(1024, device=cur.device).fill_(0.0)
         torch.cuda.synchronize()

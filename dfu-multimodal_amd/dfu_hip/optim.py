@@ -372,11 +372,11 @@ class FusedAdamW(torch.optim.Optimizer):
         touched = fp.grad._version != self._grad_version
         if (self.early_update and fp.data.is_cuda and not _dp_world() and not rebind
                 and not touched):
-            early = self._early_range(torch.cuda.current_stream(fp.data.device))
-        cur = torch.cuda.current_stream(fp.data.device) if fp.data.is_cuda else None
+            early = self._early_range(ops.current_stream(fp.data.get_device()))
+        cur = ops.current_stream(fp.data.get_device()) if fp.data.is_cuda else None
         if early is not None:
             lo, hi, st = early
-            with torch.cuda.stream(st):
+            with ops.on_stream(st):
                 ops.step_increment(self.step_dev)  # the rest runs after the join: sees it
                 self._adamw(lo, hi)
                 # the block's transposed shadows right behind its update, beside the other
@@ -384,7 +384,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 inside = fp.range_jobs(lo, hi)[0] if fp.t_jobs is not None and _EARLY_T else None
                 if inside is not None:
                     inside.launch()
-            cur.wait_stream(st)  # the rest, the step counter and the shadow transposes after it
+            ops.stream_wait(cur, st)  # the rest, the step counter and the shadow transposes after it
         Fn.join_grad_streams()
         if rebind:
             fp.rebind_grads()

@@ -15,6 +15,7 @@ import torch
 import torch.distributed as dist
 
 from . import functional as Fn
+from . import ops
 
 
 def init_from_env(backend=None):
@@ -175,13 +176,13 @@ class GradAllReducer:
         if self.cuda:
             carrier = self._carrier(k, carrier)
             if carrier is None:
-                carrier = torch.cuda.current_stream()
+                carrier = ops.current_stream()
                 Fn.join_grad_streams(carrier, clear=False)
             for sid, (st, ev) in self._marks[k].items():
                 if st is not carrier:
                     carrier.wait_event(ev)
             self.carriers[carrier.cuda_stream] = carrier
-            with torch.cuda.stream(carrier):
+            with ops.on_stream(carrier):
                 self._works.append(self._reduce(view))
         else:
             self._works.append(self._reduce(view))

@@ -11,6 +11,7 @@ import torch.nn as tnn
 
 from dfu_hip import functional as Fn
 from dfu_hip import nn as hnn
+from dfu_hip import ops
 
 from .encoders import resnet50, vit_base_patch16_224
 
@@ -68,7 +69,7 @@ def _interleave(rgen, vgen, side):
             if i == 0:
                 next(rgen)
             else:
-                with torch.cuda.stream(side):
+                with ops.on_stream(side):
                     next(vgen)
         except StopIteration as e:
             out[i] = e.value
@@ -126,19 +127,19 @@ class MultimodalFusionModel(tnn.Module):
         joined by FusedAdamW.step / GradAllReducer.finish (functional.join_grad_streams)."""
         if not (self.concurrent_branches and rgb.is_cuda):
             return rgb_net(rgb), th_net(thermal)
-        main = torch.cuda.current_stream()
+        main = ops.current_stream()
         side = Fn.side_stream(rgb.device)
-        side.wait_stream(main)
+        ops.stream_wait(side, main)
         with Fn.concurrent_encoders():
             thermal.record_stream(side)
             if _INTERLEAVE and _stageable(rgb_net) and _stageable(th_net):
                 rgb_feat, th_feat = _interleave(rgb_net.forward_stages(rgb),
                                                 th_net.forward_stages(thermal), side)
             else:
-                with torch.cuda.stream(side):
+                with ops.on_stream(side):
                     th_feat = th_net(thermal)
                 rgb_feat = rgb_net(rgb)
-        main.wait_stream(side)
+        ops.stream_wait(main, side)
         th_feat.record_stream(main)
         return rgb_feat, th_feat
 

@@ -15,6 +15,7 @@ import torch.nn as tnn
 
 from dfu_hip import functional as Fn
 from dfu_hip import nn as hnn
+from dfu_hip.functional import module_param
 
 
 def _trunc_normal_(t, std=0.02):
@@ -79,10 +80,14 @@ class Block(tnn.Module):
         self.drop_path2 = tnn.Identity()
 
     def _params(self):
-        a, m = self.attn, self.mlp
-        return [self.norm1.weight, self.norm1.bias, a.qkv.weight, a.qkv.bias, a.proj.weight,
-                a.proj.bias, self.norm2.weight, self.norm2.bias, m.fc1.weight, m.fc1.bias,
-                m.fc2.weight, m.fc2.bias]
+        # through the modules' dicts: nn.Module.__getattr__ is the slow path (~0.25 us an
+        # attribute, 26 a block a step)
+        d = self._modules
+        am, mm = d["attn"]._modules, d["mlp"]._modules
+        ps = []
+        for mod in (d["norm1"], am["qkv"], am["proj"], d["norm2"], mm["fc1"], mm["fc2"]):
+            ps += (module_param(mod, "weight"), module_param(mod, "bias"))
+        return ps
 
     def forward(self, x):
         x = Fn.ViTBlockFn.apply(x, *self._params(), self)

@@ -37,6 +37,10 @@ int dfu_zero(void* ptr, int64_t bytes, void* stream);
 /* Library-owned non-blocking HIP streams at a HIP priority (lower = higher; 0 default). */
 int dfu_stream_create(int32_t priority, void** stream);
 int dfu_stream_destroy(void* stream);
+/* `waiter` waits for the work enqueued on `producer` so far (torch Stream.wait_stream without an
+ * Event object per call: one of a per-device ring of events, recorded on `producer` and waited
+ * on by `waiter`; capturable).  Both streams belong to the current device. */
+int dfu_stream_wait(void* waiter, void* producer);
 /* Capture status of `stream`: 0 none, 1 active, 2 invalidated (hipStreamCaptureStatus). */
 int dfu_stream_capture_status(void* stream, int32_t* status);
 /* End a HIP stream capture left active on any of `streams` (n <= 64) after a failed capture
