@@ -114,6 +114,8 @@ PROTOTYPES = {
     "dfu_bn_bwd_reduce": [P, P, P, I32, P, P, P, P, I64, I32, P, P],
     "dfu_bn_bwd_finalize": [P, I32, I64, I32, P, P, I32, P, P, P, P, P, I32, P],
     "dfu_bn_bwd_apply": [P, P, P, I32, P, P, P, P, P, I64, I32, P, P, P],
+    "dfu_bn_bwd_ws_bytes": [I64, I32],
+    "dfu_bn_bwd": [P, P, P, I32, P, P, P, P, P, I64, I32, I32, P, P, P, P, P, I64, P, I32, P],
     "dfu_maxpool_fwd": [P, I32, I32, I32, I32, P, P, I32, I32, P],
     "dfu_maxpool_bn_fwd": [P, P, P, I32, I32, I32, I32, P, P, I32, I32, P],
     "dfu_maxpool_bwd": [P, P, I32, I32, I32, I32, I32, I32, P, P],
@@ -173,7 +175,8 @@ PROTOTYPES = {
 }
 _RESTYPE = {"dfu_last_error_string": c_char_p, "dfu_gemm_workspace_bytes": c_int64,
             "dfu_gemm_f32_workspace_bytes": c_int64, "dfu_bn_finalize_ws_bytes": c_int64,
-            "dfu_bn_bwd_finalize_ws_bytes": c_int64, "dfu_stem_wgrad_ws_bytes": c_int64}
+            "dfu_bn_bwd_finalize_ws_bytes": c_int64, "dfu_stem_wgrad_ws_bytes": c_int64,
+            "dfu_bn_bwd_ws_bytes": c_int64}
 
 
 def header_symbols(path=HEADER_PATH):

@@ -558,39 +558,31 @@ def bn_apply(y, scale, shift, residual, relu, out, M, C, mask=None):
               "dfu_bn_apply_mask")
 
 
-def bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres,
-                  dgamma, dbeta, batch_stats=True, scale=None, shift=None):
-    """BN backward after the reduction: finalize the [blocks][2][C] partial sums of
-    dfu_bn_bwd_reduce -> apply."""
-    relu = int(relu)
-    coef = torch.empty((C, 3), dtype=F32, device=y.device)
-    s = stream_ptr()
-    ws, cnt = _slice_ws(lib().dfu_bn_bwd_finalize_ws_bytes(blocks, C), y.device)
-    check(lib().dfu_bn_bwd_finalize(ptr(partial), blocks, M, C, ptr(gamma), ptr(invstd),
-                                    int(batch_stats), ptr(dgamma), ptr(dbeta), ptr(coef),
-                                    ptr(ws), ptr(cnt), 0 if cnt is None else cnt.numel(), s),
-          "dfu_bn_bwd_finalize")
-    check(lib().dfu_bn_bwd_apply(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
-                                 ptr(mean), ptr(invstd), ptr(coef), M, C, ptr(dy), ptr(dres), s),
-          "dfu_bn_bwd_apply")
+_BN_BWD_WS = {}  # (M, C) -> dfu_bn_bwd_ws_bytes
 
 
 def bn_bwd(dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres, dgamma, dbeta,
            batch_stats=True, scale=None, shift=None):
-    """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply.  relu: False/0 none;
-    True/1 mask from the stored output `out`; 2 mask recomputed from y with the forward's
-    scale/shift (BN + ReLU without residual; `out` is not read); 3 mask from the bitmask
-    bn_apply(mask=) wrote, passed as `out`."""
+    """Full BN(+residual)(+ReLU) backward: reduce -> finalize -> apply, one C call (dfu_bn_bwd)
+    on one workspace.  relu: False/0 none; True/1 mask from the stored output `out`; 2 mask
+    recomputed from y with the forward's scale/shift (BN + ReLU without residual; `out` is not
+    read); 3 mask from the bitmask bn_apply(mask=) wrote, passed as `out`."""
     relu = int(relu)
     if relu == 2 and (scale is None or shift is None):
         raise ValueError("bn_bwd: relu=2 needs the forward scale/shift")
-    blocks = lib().dfu_bn_bwd_blocks(M, C)
-    partial = torch.empty((blocks, 2, C), dtype=F32, device=y.device)
-    check(lib().dfu_bn_bwd_reduce(ptr(dout), ptr(y), ptr(out), relu, ptr(scale), ptr(shift),
-                                  ptr(mean), ptr(invstd), M, C, ptr(partial), stream_ptr()),
-          "dfu_bn_bwd_reduce")
-    bn_bwd_finish(partial, blocks, dout, y, out, relu, mean, invstd, gamma, M, C, dy, dres,
-                  dgamma, dbeta, batch_stats, scale, shift)
+    lb = lib()
+    nb = _BN_BWD_WS.get((M, C))
+    if nb is None:
+        nb = _BN_BWD_WS[(M, C)] = int(lb.dfu_bn_bwd_ws_bytes(M, C))
+    dev = y.device
+    ws = torch.empty((nb + 7) // 8, dtype=torch.float64, device=dev)
+    cnt = tile_counters(dev)
+    rc = lb.dfu_bn_bwd(ptr(dout), y.data_ptr(), ptr(out), relu, ptr(scale), ptr(shift),
+                       mean.data_ptr(), invstd.data_ptr(), ptr(gamma), M, C, int(batch_stats),
+                       ptr(dgamma), ptr(dbeta), dy.data_ptr(), ptr(dres), ws.data_ptr(), nb,
+                       cnt.data_ptr(), cnt.numel(), stream_ptr())
+    if rc:
+        check(rc, "dfu_bn_bwd")
 
 
 # ------------------------------------------------------------------------------- pooling

@@ -312,6 +312,15 @@ int dfu_bn_bwd_apply(const void* dout, const void* y, const void* out, int32_t r
                      const float* scale, const float* shift, const float* mean,
                      const float* invstd, const float* coef, int64_t M, int32_t C, void* dy,
                      void* dres, void* stream);
+/* The three above in one call (the same launches, bitwise the same results) on one workspace of
+ * dfu_bn_bwd_ws_bytes(M, C) bytes, 16-B aligned: finalize slices, the partial sums and coef;
+ * counters: zeroed per-stream tile counters (zero in, zero out) for the sliced finalize. */
+int64_t dfu_bn_bwd_ws_bytes(int64_t M, int32_t C);
+int dfu_bn_bwd(const void* dout, const void* y, const void* out, int32_t relu, const float* scale,
+               const float* shift, const float* mean, const float* invstd, const float* gamma,
+               int64_t M, int32_t C, int32_t batch_stats, float* dgamma, float* dbeta, void* dy,
+               void* dres, void* ws, int64_t ws_bytes, int32_t* counters, int32_t ncounters,
+               void* stream);
 
 /* ---------------------------------------------------------------- pooling ----------- */
 /* resnet maxpool 3x3/s2/p1 on NHWC bf16; argmax (0..8 window index) saved as uint8. */

@@ -16,6 +16,8 @@ def test_stream_wait_orders_a_consumer_after_a_producer():
     out = []
     torch.cuda.synchronize()
     for it in range(300):  # more joins than the event ring holds (256): re-recorded events
+        # both directions: the producer's next fill must also wait for the consumer's read
+        ops.stream_wait(prod, cons)
         with torch.cuda.stream(prod):
             x.fill_(float(it))
             for _ in range(3):  # keep the producer busy so an unordered read would see old data

@@ -25,8 +25,15 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--profile", action="store_true", help="cProfile the host side instead")
     ap.add_argument("--precision", default="parity")
+    ap.add_argument("--pin", action="store_true", help="pin the process to four cores")
     a = ap.parse_args()
     Fn.set_precision(a.precision)
+    if a.pin and hasattr(os, "sched_setaffinity"):
+        # four fixed cores (the calling thread, autograd's device thread, the runtime's): the
+        # box's scheduler otherwise moves the process between cores of different speed mid-run
+        cores = sorted(os.sched_getaffinity(0))[:4]
+        os.sched_setaffinity(0, cores)
+        print("pinned to cores", cores)
     if a.profile:
         return profile()
     dev = torch.device("cuda", 0)
@@ -65,6 +72,10 @@ def main():
     print("host enqueue ms per phase (median):",
           ", ".join(f"{k} {med(acc[k]):.3f}" for k in phases))
     print(f"host total {host:.3f} ms, GPU step {med(gpu):.3f} ms (synchronised each step)")
+    # the fastest step: the enqueue's own cost without the host's noise (other processes on the
+    # box's cores, frequency changes) -- which moves the medians by several ms between runs
+    tot = [sum(acc[k][j] for k in phases) for j in range(len(gpu))]
+    print(f"host fastest step {min(tot):.3f} ms, lower quartile {sorted(tot)[len(tot) // 4]:.3f} ms")
 
 
 

@@ -28,7 +28,7 @@ EPI_BF16, EPI_F32_RESID, EPI_BF16_DGELU, EPI_F32_ACC, EPI_F16_GELU = 0, 4, 5, 7,
 VARIANTS = {
     "bn_fin": ["dfu_bn_finalize", "dfu_bn_bwd_finalize"],
     "bn_apply_x3": ["dfu_bn_apply_x3"],
-    "bn_bwd": ["dfu_bn_bwd_reduce", "dfu_bn_bwd_finalize", "dfu_bn_bwd_apply"],
+    "bn_bwd": ["dfu_bn_bwd", "dfu_bn_bwd_reduce", "dfu_bn_bwd_finalize", "dfu_bn_bwd_apply"],
     "attn_bwd": ["dfu_attention_bwd", "dfu_attention_bwd_qkv16"],
     "attn": ["dfu_attention_fwd", "dfu_attention_fwd_f16", "dfu_attention_bwd",
              "dfu_attention_bwd_qkv16"],
