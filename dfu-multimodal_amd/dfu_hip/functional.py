@@ -324,10 +324,13 @@ def grads_done(*params):
 
 
 def module_param(mod, name):
-    """mod.<name> for a registered parameter by its dict (nn.Module.__getattr__, the slow path
-    for parameters, costs ~0.25 us an attribute); anything else by getattr."""
+    """mod.<name> for a registered parameter or buffer by its dict (nn.Module.__getattr__, the
+    slow path for both, costs ~0.25 us an attribute); anything else by getattr."""
     p = mod._parameters
-    return p[name] if name in p else getattr(mod, name)
+    if name in p:
+        return p[name]
+    b = mod._buffers
+    return b[name] if name in b else getattr(mod, name)
 
 
 def _wants(p):
@@ -542,10 +545,11 @@ class _BN:
         if self.training:
             track = bn.track_running_stats and bn.training
             mom = bn.momentum if bn.momentum is not None else 0.1
-            ops.bn_finalize(stats, self.M, self.C, bn.weight, bn.bias, bn.eps, mom,
-                            bn.running_mean if track else None,
-                            bn.running_var if track else None,
-                            bn.num_batches_tracked if track else None,
+            mp = module_param
+            ops.bn_finalize(stats, self.M, self.C, mp(bn, "weight"), mp(bn, "bias"), bn.eps, mom,
+                            mp(bn, "running_mean") if track else None,
+                            mp(bn, "running_var") if track else None,
+                            mp(bn, "num_batches_tracked") if track else None,
                             self.mean, self.invstd, self.scale, self.shift)
         else:
             ops.bn_eval_coeffs(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
@@ -559,12 +563,13 @@ class _BN:
         with no residual: the mask is recomputed from y with the forward's scale/shift, so
         `out` is not read); or 3 (`out` is the forward's ReLU bitmask, ops.bn_apply(mask=))."""
         bn = self.bn
-        dgamma = grad_buffer(bn.weight) if _wants(bn.weight) else None
-        dbeta = grad_buffer(bn.bias) if _wants(bn.bias) else None
-        ops.bn_bwd(dout, y, out, relu, self.mean, self.invstd, bn.weight, self.M, self.C, dy,
+        w, b = module_param(bn, "weight"), module_param(bn, "bias")
+        dgamma = grad_buffer(w) if _wants(w) else None
+        dbeta = grad_buffer(b) if _wants(b) else None
+        ops.bn_bwd(dout, y, out, relu, self.mean, self.invstd, w, self.M, self.C, dy,
                    dres, dgamma, dbeta, batch_stats=self.training, scale=self.scale,
                    shift=self.shift)
-        grads_done(bn.weight, bn.bias)
+        grads_done(w, b)
 
 
 # --------------------------------------------------------------------------- conv helpers
@@ -785,18 +790,19 @@ class BottleneckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, *params_and_mod):
         mod = params_and_mod[-1]
+        mm = mod._modules  # (nn.Module attributes are slow __getattr__ lookups)
         x3mode = _x3(mod)
         xin3 = _take_x3(x) if x3mode else None
         x = nhwc_bf16(x.detach())
         B, Cin, H, W = x.shape
         dev = x.device
         xr = rows_view(x)
-        g1 = _geom(mod.conv1, B, H, W)
-        g2 = _geom(mod.conv2, B, g1.p, g1.q)
-        g3 = _geom(mod.conv3, B, g2.p, g2.q)
-        w1 = conv_weight_bf16(mod.conv1.weight)
-        w2 = conv_weight_bf16(mod.conv2.weight)
-        w3 = conv_weight_bf16(mod.conv3.weight)
+        g1 = _geom(mm["conv1"], B, H, W)
+        g2 = _geom(mm["conv2"], B, g1.p, g1.q)
+        g3 = _geom(mm["conv3"], B, g2.p, g2.q)
+        w1 = conv_weight_bf16(mm["conv1"].weight)
+        w2 = conv_weight_bf16(mm["conv2"].weight)
+        w3 = conv_weight_bf16(mm["conv3"].weight)
         M1 = B * g1.p * g1.q
         M2 = B * g2.p * g2.q
         planes, outc = g1.k, g3.k
@@ -836,17 +842,18 @@ class BottleneckFn(torch.autograd.Function):
         out_lo = None
         masks = None
         if x3mode:
-            y1, a1, a1_lo, _, s1, m1 = conv_bn_x3(xin3, g1, conv_weight_x3(mod.conv1.weight),
-                                                   mod.bn1, True)
+            y1, a1, a1_lo, _, s1, m1 = conv_bn_x3(xin3, g1, conv_weight_x3(mm["conv1"].weight),
+                                                   mm["bn1"], True)
             y2, a2, a2_lo, _, s2, m2 = conv_bn_x3((a1, a1_lo), g2,
-                                                   conv_weight_x3(mod.conv2.weight), mod.bn2, True)
+                                                   conv_weight_x3(mm["conv2"].weight), mm["bn2"],
+                                                   True)
             masks = (m1, m2)  # the BN + ReLU backward's masks (the pre-activations were fp32)
             del a1_lo
         else:
-            y1, a1, s1 = conv_bn(xr, g1, w1, mod.bn1, True)
-            y2, a2, s2 = conv_bn(a1, g2, w2, mod.bn2, True)
-        if mod.downsample is not None:
-            dconv, dbn = mod.downsample[0], mod.downsample[1]
+            y1, a1, s1 = conv_bn(xr, g1, w1, mm["bn1"], True)
+            y2, a2, s2 = conv_bn(a1, g2, w2, mm["bn2"], True)
+        if mm.get("downsample") is not None:
+            dconv, dbn = mm.get("downsample")[0], mm.get("downsample")[1]
             gd = _geom(dconv, B, H, W)
             wd = conv_weight_bf16(dconv.weight)
             if x3mode:
@@ -861,14 +868,15 @@ class BottleneckFn(torch.autograd.Function):
             res, res_mode = xin3, 2
         if x3mode:
             y3, out, out_lo, _, s3, mask3 = conv_bn_x3((a2, a2_lo), g3,
-                                                        conv_weight_x3(mod.conv3.weight), mod.bn3,
-                                                        True, res=res, res_mode=res_mode)
+                                                        conv_weight_x3(mm["conv3"].weight),
+                                                        mm["bn3"], True, res=res,
+                                                        res_mode=res_mode)
             del a2_lo, res, xin3
         else:
             # bn3 + residual + ReLU also writes its ReLU bitmask: the backward reads M*C/8 bytes
             # instead of the block output twice (reduce and apply)
             mask3 = _empty((M2 * outc // 8,), torch.uint8, dev)
-            y3, out, s3 = conv_bn(a2, g3, w3, mod.bn3, True, residual=idn, mask=mask3)
+            y3, out, s3 = conv_bn(a2, g3, w3, mm["bn3"], True, residual=idn, mask=mask3)
         ctx.x3 = x3mode
         ctx.mod = mod
         ctx.geo = (g1, g2, g3, gd)
@@ -897,6 +905,7 @@ class BottleneckFn(torch.autograd.Function):
         xr, y1, a1, y2, a2, y3, out, w1, w2, w3 = saved[:10]
         yd, wd = (saved[10], saved[11]) if len(saved) > 10 else (None, None)
         mod = ctx.mod
+        mm = mod._modules
         g1, g2, g3, gd = ctx.geo
         s1, s2, s3, sd = ctx.bns
         B, Cin, H, W = ctx.shape
@@ -918,13 +927,13 @@ class BottleneckFn(torch.autograd.Function):
         if yd is not None:
             dyd = torch.empty_like(yd)
             sd.backward(dres, yd, None, False, dyd, None)
-            wgrad(mod.downsample[0], dyd, xr, gd)
+            wgrad(mm.get("downsample")[0], dyd, xr, gd)
         # conv3
         da2 = torch.empty_like(a2)
-        conv_dgrad(dy3, g3, w3, da2, w_t=conv1x1_weight_T(mod.conv3, g3))
+        conv_dgrad(dy3, g3, w3, da2, w_t=conv1x1_weight_T(mm["conv3"], g3))
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[1], from_rows(da2, B, g2.p, g2.q, g2.k))
-        wgrad(mod.conv3, dy3, a2, g3)
+        wgrad(mm["conv3"], dy3, a2, g3)
         # bn2 + relu, conv2
         # BN + ReLU masks: recomputed from y (bf16), or in bf16x3 mode (fp32 pre-activations)
         # the bitmasks the forward apply wrote
@@ -933,25 +942,25 @@ class BottleneckFn(torch.autograd.Function):
         s2.backward(da2, y2, m2, 3 if ctx.x3 else 2, dy2, None)
         da1 = torch.empty_like(a1)
         conv_dgrad(dy2, g2, w2, da1, w_flip=None if g2.stride != 1 else
-                   conv_weight_flipped(mod.conv2.weight))
+                   conv_weight_flipped(mm["conv2"].weight))
         if ctx.probes is not None:
             _fire_grad_hooks(ctx.probes[0], from_rows(da1, B, g1.p, g1.q, g1.k))
-        wgrad(mod.conv2, dy2, a1, g2)
+        wgrad(mm["conv2"], dy2, a1, g2)
         # bn1 + relu, conv1 (+ identity gradient fused in the dgrad epilogue)
         dy1 = torch.empty_like(y1)
         s1.backward(da1, y1, m1, 3 if ctx.x3 else 2, dy1, None)
         dx = None
         if ctx.x_requires_grad:
             dxr = _empty((M1, Cin), BF16, dev)
-            w1t = conv1x1_weight_T(mod.conv1, g1)
+            w1t = conv1x1_weight_T(mm["conv1"], g1)
             if dyd is None:  # identity shortcut: its gradient rides in conv1's dgrad epilogue
                 conv_dgrad(dy1, g1, w1, dxr, add=dres, w_t=w1t)
             else:  # downsample: conv1's dgrad, then the (strided) 1x1 dgrad added in place
                 conv_dgrad(dy1, g1, w1, dxr, w_t=w1t)
                 conv_dgrad(dyd, gd, wd, dxr, add=dxr,
-                           w_t=conv1x1_weight_T(mod.downsample[0], gd))
+                           w_t=conv1x1_weight_T(mm.get("downsample")[0], gd))
             dx = from_rows(dxr, B, H, W, Cin)
-        wgrad(mod.conv1, dy1, xr, g1)
+        wgrad(mm["conv1"], dy1, xr, g1)
         n_params = len(ctx.needs_input_grad) - 2
         return (dx,) + (None,) * n_params + (None,)
 
@@ -1132,7 +1141,8 @@ class ViTBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, *params_and_mod):
         blk = params_and_mod[-1]
-        attn, mlp = blk.attn, blk.mlp
+        bm = blk._modules  # (nn.Module attributes are slow __getattr__ lookups)
+        attn, mlp = bm["attn"], bm["mlp"]
         B, T, D = x.shape
         rows = B * T
         H = attn.num_heads
@@ -1140,10 +1150,11 @@ class ViTBlockFn(torch.autograd.Function):
         dev = x.device
         x = x.detach().contiguous()
         x2 = x.view(rows, D)
-        wqkv = weight_bf16_rows(attn.qkv.weight)
-        wproj = weight_bf16_rows(attn.proj.weight)
-        wfc1 = weight_bf16_rows(mlp.fc1.weight)
-        wfc2 = weight_bf16_rows(mlp.fc2.weight)
+        # the Linears' weights: the Function's own inputs (models.vit.Block._params order)
+        wqkv = weight_bf16_rows(params_and_mod[2])
+        wproj = weight_bf16_rows(params_and_mod[4])
+        wfc1 = weight_bf16_rows(params_and_mod[8])
+        wfc2 = weight_bf16_rows(params_and_mod[10])
         Dh = wfc1.shape[0]
         bias = lambda lin: lin.bias.detach() if lin.bias is not None else None  # noqa: E731
         mode = stage_mode(blk)
@@ -1255,7 +1266,9 @@ class ViTBlockFn(torch.autograd.Function):
         256 x 256 tile, 192 x 256 for the N = 768 GEMMs when the ViT runs alone), the fp16
         attention, fp32 residual stream; saves the same bf16 tensors as the bf16 forward (every
         fp16 producer also writes the bf16 copy)."""
-        attn, mlp = blk.attn, blk.mlp
+        bm = blk._modules
+        attn, mlp = bm["attn"], bm["mlp"]
+        am, mm = attn._modules, mlp._modules
         dev = x2.device
         Dh = wfc1.shape[0]
         F16 = torch.float16
@@ -1272,31 +1285,31 @@ class ViTBlockFn(torch.autograd.Function):
         h16 = L.OPERAND_F16
         ctx.t768 = _t768()
         tl_d = ctx.t768 or 8
-        xn1_16, xn1, m1, r1 = ln(x2, blk.norm1)
+        xn1_16, xn1, m1, r1 = ln(x2, bm["norm1"])
         # qkv in fp16 only: the attention backward rounds it to bf16 while staging
         # (same-box A/B: 21.56-21.62 vs 21.72-21.75 ms with the bf16 copy written too)
         qkv = _empty((rows, 3 * D), F16, dev)
-        ops.gemm(rows, 3 * D, D, xn1_16, D, weight_f16_rows(attn.qkv.weight), D, qkv, 3 * D,
-                 epilogue=L.EPI_F16_DUAL, bias=bias(attn.qkv), tile=8, operand_type=h16)
+        ops.gemm(rows, 3 * D, D, xn1_16, D, weight_f16_rows(am["qkv"].weight), D, qkv, 3 * D,
+                 epilogue=L.EPI_F16_DUAL, bias=bias(am["qkv"]), tile=8, operand_type=h16)
         del xn1_16
         o16, o, lse = ops.attention_fwd_f16(qkv, B, T, H, dh, attn.scale)
         xm = _empty((rows, D), F32, dev)
-        ops.gemm(rows, D, D, o16, D, weight_f16_rows(attn.proj.weight), D, xm, D,
-                 epilogue=L.EPI_F32_RESID, bias=bias(attn.proj), aux=x2, ldaux=D, tile=tl_d,
+        ops.gemm(rows, D, D, o16, D, weight_f16_rows(am["proj"].weight), D, xm, D,
+                 epilogue=L.EPI_F32_RESID, bias=bias(am["proj"]), aux=x2, ldaux=D, tile=tl_d,
                  operand_type=h16)
         del o16
-        xn2_16, xn2, m2, r2 = ln(xm, blk.norm2)
+        xn2_16, xn2, m2, r2 = ln(xm, bm["norm2"])
         # fc1 + GELU: [fp16 gelu | bf16 gelu] (fc2's operand, the backward's h) + bf16 gelu'
         h2 = _empty((rows, 2 * Dh), BF16, dev)
         dgl = _empty((rows, Dh), BF16, dev)
-        ops.gemm(rows, Dh, D, xn2_16, D, weight_f16_rows(mlp.fc1.weight), D, h2, 2 * Dh,
-                 epilogue=L.EPI_F16_GELU, bias=bias(mlp.fc1), aux_out=dgl, ldaux_out=Dh, tile=8,
+        ops.gemm(rows, Dh, D, xn2_16, D, weight_f16_rows(mm["fc1"].weight), D, h2, 2 * Dh,
+                 epilogue=L.EPI_F16_GELU, bias=bias(mm["fc1"]), aux_out=dgl, ldaux_out=Dh, tile=8,
                  operand_type=h16)
         del xn2_16
         h = h2[:, Dh:]
         xo = _empty((B, T, D), F32, dev)
-        ops.gemm(rows, D, Dh, h2, 2 * Dh, weight_f16_rows(mlp.fc2.weight), Dh, xo.view(rows, D),
-                 D, epilogue=L.EPI_F32_RESID, bias=bias(mlp.fc2), aux=xm, ldaux=D, tile=tl_d,
+        ops.gemm(rows, D, Dh, h2, 2 * Dh, weight_f16_rows(mm["fc2"].weight), Dh, xo.view(rows, D),
+                 D, epilogue=L.EPI_F32_RESID, bias=bias(mm["fc2"]), aux=xm, ldaux=D, tile=tl_d,
                  operand_type=h16)
         ctx.blk = blk
         ctx.dims = (B, T, D, H, dh, Dh)
@@ -1311,7 +1324,12 @@ class ViTBlockFn(torch.autograd.Function):
         (x2, xn1, m1, r1, qkv, o, lse, xm, xn2, m2, r2, dgl, h, wqkv, wproj, wfc1,
          wfc2) = ctx.saved_tensors
         blk = ctx.blk
-        attn, mlp = blk.attn, blk.mlp
+        # modules resolved once (each nn.Module attribute is a slow __getattr__ lookup)
+        bm = blk._modules
+        attn, mlp = bm["attn"], bm["mlp"]
+        am, mm = attn._modules, mlp._modules
+        qkv_l, proj_l, fc1_l, fc2_l = am["qkv"], am["proj"], mm["fc1"], mm["fc2"]
+        norm1, norm2 = bm["norm1"], bm["norm2"]
         B, T, D, H, dh, Dh = ctx.dims
         rows = B * T
         dev = x2.device
@@ -1337,7 +1355,7 @@ class ViTBlockFn(torch.autograd.Function):
         # through frozen weights -- would leave the stream unjoined, which a graph capture
         # rejects; the streams that wrote gradients are joined by join_grad_streams)
         wants_w = any(_wants(lin.weight) or _wants(lin.bias)
-                      for lin in (mlp.fc1, mlp.fc2, attn.qkv, attn.proj))
+                      for lin in (fc1_l, fc2_l, qkv_l, proj_l))
         bw = _Beside(wgrad_stream(dev) if (ctx.beside and g.is_cuda and wants_w) else None)
         red_w = ops.PartialReductions() if bw.ws is not None else red
 
@@ -1352,7 +1370,7 @@ class ViTBlockFn(torch.autograd.Function):
             bw.run(fn, dy, x, *(() if partial is None else (partial,)))
 
         # ---- MLP branch: x_out = x_mid + fc2(gelu(fc1(norm2(x_mid))))
-        wgrad(mlp.fc2, gb, h)
+        wgrad(fc2_l, gb, h)
         dh_pre = _empty((rows, Dh), BF16, dev)
         # fc1.bias's gradient = column sums of dh_pre: reduced in the dGELU epilogue (per 128-row
         # half of each 256-row tile) where the plan is the persistent 256x256 tile, else a pass
@@ -1360,45 +1378,45 @@ class ViTBlockFn(torch.autograd.Function):
         # the ViT's critical stream measured 0.07 ms slower per step than the separate pass,
         # thermal-only 0.13 ms faster)
         cs1 = None
-        if (_DGELU_COLSUM == 2 or (_DGELU_COLSUM and ctx.beside)) and _wants(mlp.fc1.bias) and \
+        if (_DGELU_COLSUM == 2 or (_DGELU_COLSUM and ctx.beside)) and _wants(fc1_l.bias) and \
                 g.is_cuda:
             cs1 = _empty((2 * ((rows + 255) // 256), Dh), F32, dev)
             try:
-                _linear_dgrad(rows, Dh, D, gb, mlp.fc2.weight, wfc2, dh_pre,
+                _linear_dgrad(rows, Dh, D, gb, fc2_l.weight, wfc2, dh_pre,
                               epilogue=L.EPI_BF16_DGELU, aux=dgl, ldaux=Dh, stats=cs1)
             except L.DfuError as e:
                 if e.code != L.DFU_E_UNSUPPORTED:
                     raise
                 cs1 = None
         if cs1 is None:
-            _linear_dgrad(rows, Dh, D, gb, mlp.fc2.weight, wfc2, dh_pre,
+            _linear_dgrad(rows, Dh, D, gb, fc2_l.weight, wfc2, dh_pre,
                           epilogue=L.EPI_BF16_DGELU, aux=dgl, ldaux=Dh)
-        if _wants(mlp.fc2.bias):
-            _colsum_of_grad(gout if gout.dtype == F32 else g, grad_buffer(mlp.fc2.bias), red)
-        wgrad(mlp.fc1, dh_pre, xn2, Dh, partial=cs1)
+        if _wants(fc2_l.bias):
+            _colsum_of_grad(gout if gout.dtype == F32 else g, grad_buffer(fc2_l.bias), red)
+        wgrad(fc1_l, dh_pre, xn2, Dh, partial=cs1)
         dxn2 = _empty((rows, D), BF16, dev)
-        _linear_dgrad(rows, D, Dh, dh_pre, mlp.fc1.weight, wfc1, dxn2, tile=ctx.t768)
+        _linear_dgrad(rows, D, Dh, dh_pre, fc1_l.weight, wfc1, dxn2, tile=ctx.t768)
         gmb = _empty((rows, D), BF16, dev)
-        gsp = _ln_bwd(dxn2, xm, m2, r2, blk.norm2, rows, D, g2, gmb,
-                      gsum=_wants(attn.proj.bias), batch=red)  # g2 := g_mid (in place)
+        gsp = _ln_bwd(dxn2, xm, m2, r2, norm2, rows, D, g2, gmb,
+                      gsum=_wants(proj_l.bias), batch=red)  # g2 := g_mid (in place)
         # ---- attention branch: x_mid = x_in + proj(attn(norm1(x_in)))
-        wgrad(attn.proj, gmb, o)
+        wgrad(proj_l, gmb, o)
         do = _empty((rows, D), BF16, dev)
-        _linear_dgrad(rows, D, D, gmb, attn.proj.weight, wproj, do, tile=ctx.t768)
-        if _wants(attn.proj.bias):
-            red.add(gsp, grad_buffer(attn.proj.bias), D)
+        _linear_dgrad(rows, D, D, gmb, proj_l.weight, wproj, do, tile=ctx.t768)
+        if _wants(proj_l.bias):
+            red.add(gsp, grad_buffer(proj_l.bias), D)
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, T, H, dh, attn.scale)
-        wgrad(attn.qkv, dqkv, xn1, 3 * D)
+        wgrad(qkv_l, dqkv, xn1, 3 * D)
         dxn1 = _empty((rows, D), BF16, dev)
-        _linear_dgrad(rows, D, 3 * D, dqkv, attn.qkv.weight, wqkv, dxn1, tile=ctx.t768)
+        _linear_dgrad(rows, D, 3 * D, dqkv, qkv_l.weight, wqkv, dxn1, tile=ctx.t768)
         gib = _empty((B, T, D), BF16, dev)
-        gsp = _ln_bwd(dxn1, x2, m1, r1, blk.norm1, rows, D, g2, gib.view(rows, D),
+        gsp = _ln_bwd(dxn1, x2, m1, r1, norm1, rows, D, g2, gib.view(rows, D),
                       gsum=True, batch=red)  # g2 := g_in
         red.flush()
         if red_w is not red:
             bw.run(red_w.flush)
-        grads_done(mlp.fc2.bias, mlp.fc1.bias, blk.norm2.weight, blk.norm2.bias,
-                   attn.proj.bias, attn.qkv.bias, blk.norm1.weight, blk.norm1.bias)
+        grads_done(fc2_l.bias, fc1_l.bias, norm2.weight, norm2.bias,
+                   proj_l.bias, qkv_l.bias, norm1.weight, norm1.bias)
         gin = g.view(B, T, D)
         gin._dfu_bf16 = gib
         gin._dfu_colsum = gsp  # the previous block's fc2.bias gradient, pre-reduced
