@@ -353,6 +353,60 @@ def test_batchnorm_bwd_mask_from_y_is_bitwise(M, C):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("M,C,relu", [(5000, 128, 1), (200704, 64, 3), (3136, 2048, 0)])
+def test_batchnorm_bwd_one_call_equals_three(M, C, relu):
+    """dfu_bn_bwd (the step's path: one C call, one workspace) is bit for bit the three-call
+    sequence reduce -> finalize -> apply it replaces (sliced finalize included: M = 200704)."""
+    lib = L.load()
+    y = rnd(M, C, seed=60, scale=2.0)
+    stats = torch.empty(ops.stats_tiles(M), 2, C, dtype=torch.float32, device=DEV)
+    Y = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(M, C, C, y, C, torch.eye(C, dtype=torch.bfloat16, device=DEV), C, Y, C,
+             epilogue=L.EPI_BF16_STATS, stats=stats)
+    gamma = rnd(C, dtype=torch.float32, seed=61) * 0.5 + 1
+    beta = rnd(C, dtype=torch.float32, seed=62)
+    mean, invstd, scale, shift = (torch.empty(C, device=DEV) for _ in range(4))
+    ops.bn_finalize(stats, M, C, gamma, beta, 1e-5, 0.1, None, None, None, mean, invstd, scale,
+                    shift)
+    out = torch.empty_like(Y)
+    mask = torch.empty(M * C // 8, dtype=torch.uint8, device=DEV)
+    ops.bn_apply(Y, scale, shift, rnd(M, C, seed=63) if relu == 1 else None, relu != 0, out, M,
+                 C, mask=mask)
+    o = {0: None, 1: out, 3: mask}[relu]
+    dout = rnd(M, C, seed=64)
+
+    def grads():
+        return (torch.empty_like(Y), torch.empty_like(Y), torch.full((C,), 0.25, device=DEV),
+                torch.full((C,), -0.5, device=DEV))
+    dy1, dr1, dg1, db1 = grads()
+    ops.bn_bwd(dout, Y, o, relu, mean, invstd, gamma, M, C, dy1, dr1, dg1, db1)
+    dy2, dr2, dg2, db2 = grads()
+    s = ops.stream_ptr()
+    blocks = lib.dfu_bn_bwd_blocks(M, C)
+    partial = torch.empty(blocks, 2, C, dtype=torch.float32, device=DEV)
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    assert lib.dfu_bn_bwd_reduce(P(dout), P(Y), P(o), relu, None, None, P(mean), P(invstd), M, C,
+                                 P(partial), s) == 0
+    nb = lib.dfu_bn_bwd_finalize_ws_bytes(blocks, C)
+    ws = torch.empty(max(nb, 8) // 8, dtype=torch.float64, device=DEV) if nb > 0 else None
+    cnt = ops.tile_counters(torch.device(DEV)) if nb > 0 else None
+    coef = torch.empty(C, 3, dtype=torch.float32, device=DEV)
+    assert lib.dfu_bn_bwd_finalize(P(partial), blocks, M, C, P(gamma), P(invstd), 1, P(dg2),
+                                   P(db2), P(coef), P(ws), P(cnt),
+                                   0 if cnt is None else cnt.numel(), s) == 0
+    assert lib.dfu_bn_bwd_apply(P(dout), P(Y), P(o), relu, None, None, P(mean), P(invstd),
+                                P(coef), M, C, P(dy2), P(dr2), s) == 0
+    torch.cuda.synchronize()
+    for a, b, what in ((dy1, dy2, "dy"), (dr1, dr2, "dres"), (dg1, dg2, "dgamma"),
+                       (db1, db2, "dbeta")):
+        assert torch.equal(a, b), what
+    # a workspace smaller than dfu_bn_bwd_ws_bytes is refused before any launch
+    small = torch.empty(1, dtype=torch.float64, device=DEV)
+    rc = lib.dfu_bn_bwd(P(dout), P(Y), P(o), relu, None, None, P(mean), P(invstd), P(gamma), M,
+                        C, 1, None, None, P(dy1), None, P(small), 8, None, 0, s)
+    assert rc == L.DFU_E_INVALID
+
+
 def test_layernorm_fwd_bwd():
     rows, D = 1000, 768
     x = (torch.randn(rows, D, device=DEV) * 3 + 1).float()
