@@ -36,7 +36,12 @@ constexpr double kReduceLaunchUs = 2.0;
 // Persistent schedule (gemm_kernel.h): a workgroup owning several work units pays one
 // prologue fill for all of them plus, per unit, the epilogue time its MFMAs do not hide.
 constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0, 3.0, 3.0, 3.0, 3.0};
-int g_persistent = getenv("DFU_GEMM_PERSISTENT") ? atoi(getenv("DFU_GEMM_PERSISTENT")) : 1;  // dfu_gemm_set_persistent (env: A/B)
+// Persistent launches (at most one wave of workgroups, each walking its work units) for the
+// generic tiles (g_persistent) and the persistent phased 256-wide tiles (g_persistent_ps);
+// otherwise one workgroup per unit, which the hardware dispatcher hands to CUs as they free up.
+// dfu_gemm_set_persistent sets both; env DFU_GEMM_PERSISTENT / DFU_GEMM_PERSISTENT_PS: A/B.
+int g_persistent = getenv("DFU_GEMM_PERSISTENT") ? atoi(getenv("DFU_GEMM_PERSISTENT")) : 1;
+int g_persistent_ps = getenv("DFU_GEMM_PERSISTENT_PS") ? atoi(getenv("DFU_GEMM_PERSISTENT_PS")) : 1;
 int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
 const int g_wide_reduce = getenv("DFU_GEMM_WIDE_REDUCE") ? atoi(getenv("DFU_GEMM_WIDE_REDUCE")) : 1;
@@ -323,6 +328,7 @@ extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* spl
 extern "C" int dfu_gemm_set_persistent(int32_t enable) {
   const int old = g_persistent;
   g_persistent = enable != 0;
+  g_persistent_ps = enable != 0;
   return old;
 }
 
@@ -642,7 +648,9 @@ int launch(const dfu_gemm_desc* d, const Plan& pl, const Phase* ph, hipStream_t 
   }
   const int units = a.tail_r ? a.tail_full + a.tail_r * a.tail_s : a.tiles_m * a.tiles_n * splits;
   const bool atomics = acc_epi && splits > 1 && a.slab == nullptr;
-  const int nwg = (g_persistent && !atomics && units > slots) ? slots : units;
+  const bool pers = (pl.tile == T256x256ps || pl.tile == T192x256ps) ? g_persistent_ps
+                                                                     : g_persistent;
+  const int nwg = (pers && !atomics && units > slots) ? slots : units;
   hipLaunchKernelGGL(pl.entry->fn, dim3(nwg), dim3(pl.entry->threads), 0, s, a);
   DFU_LAUNCH_CHECK();
   if (a.slab != nullptr && a.counters == nullptr) {

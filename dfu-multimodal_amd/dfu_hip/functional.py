@@ -1130,9 +1130,10 @@ def _t768():
     """Tile hint for a ViT GEMM with N = 768 output columns (0: the tuned plan)."""
     return 9 if _concurrent_encoders[0] == 0 and not _NO_T192 else 0
 
-# fc1.bias gradient from the dGELU epilogue's column sums when the ViT runs alone
-# (DFU_DGELU_COLSUM=0: a colsum pass everywhere; 2: the epilogue's sums in the fusion step too)
-_DGELU_COLSUM = int(os.environ.get("DFU_DGELU_COLSUM", "1"))
+# fc1.bias gradient from the dGELU epilogue's column sums, in the fusion step too (round 6: 0.1 ms
+# faster per step there on the final tree; DFU_DGELU_COLSUM=0: a colsum pass everywhere,
+# 1: the epilogue's sums only when the ViT runs alone, the round-3 setting)
+_DGELU_COLSUM = int(os.environ.get("DFU_DGELU_COLSUM", "2"))
 
 
 class ViTBlockFn(torch.autograd.Function):
@@ -1374,9 +1375,8 @@ class ViTBlockFn(torch.autograd.Function):
         dh_pre = _empty((rows, Dh), BF16, dev)
         # fc1.bias's gradient = column sums of dh_pre: reduced in the dGELU epilogue (per 128-row
         # half of each 256-row tile) where the plan is the persistent 256x256 tile, else a pass
-        # (when the ViT runs alone: inside the two-stream fusion step the longer dGELU GEMM on
-        # the ViT's critical stream measured 0.07 ms slower per step than the separate pass,
-        # thermal-only 0.13 ms faster)
+        # (thermal-only 0.13 ms faster per step; the fusion step 0.07 ms slower in round 3 and
+        # 0.1 ms faster on the round-6 tree: _DGELU_COLSUM)
         cs1 = None
         if (_DGELU_COLSUM == 2 or (_DGELU_COLSUM and ctx.beside)) and _wants(fc1_l.bias) and \
                 g.is_cuda:
