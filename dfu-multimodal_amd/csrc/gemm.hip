@@ -39,8 +39,11 @@ constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0, 3.0, 3.0,
 // Persistent launches (at most one wave of workgroups, each walking its work units) for the
 // generic tiles (g_persistent) and the persistent phased 256-wide tiles (g_persistent_ps);
 // otherwise one workgroup per unit, which the hardware dispatcher hands to CUs as they free up.
-// dfu_gemm_set_persistent sets both; env DFU_GEMM_PERSISTENT / DFU_GEMM_PERSISTENT_PS: A/B.
-int g_persistent = getenv("DFU_GEMM_PERSISTENT") ? atoi(getenv("DFU_GEMM_PERSISTENT")) : 1;
+// Round 6 (final tree, same box, three rounds): the generic tiles one workgroup per unit ran the
+// fusion step 0.4 % faster and the GEMM replay 0.7 %; the phased tiles level either way in the
+// step, persistent faster alone.  dfu_gemm_set_persistent (bit 0 generic, bit 1 phased); env
+// DFU_GEMM_PERSISTENT / DFU_GEMM_PERSISTENT_PS: A/B.
+int g_persistent = getenv("DFU_GEMM_PERSISTENT") ? atoi(getenv("DFU_GEMM_PERSISTENT")) : 0;
 int g_persistent_ps = getenv("DFU_GEMM_PERSISTENT_PS") ? atoi(getenv("DFU_GEMM_PERSISTENT_PS")) : 1;
 int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
@@ -325,10 +328,10 @@ extern "C" int dfu_gemm_plan(const dfu_gemm_desc* d, int32_t* tile, int32_t* spl
   return DFU_OK;
 }
 
-extern "C" int dfu_gemm_set_persistent(int32_t enable) {
-  const int old = g_persistent;
-  g_persistent = enable != 0;
-  g_persistent_ps = enable != 0;
+extern "C" int dfu_gemm_set_persistent(int32_t mode) {
+  const int old = (g_persistent ? 1 : 0) | (g_persistent_ps ? 2 : 0);
+  g_persistent = (mode & 1) != 0;
+  g_persistent_ps = (mode & 2) != 0;
   return old;
 }
 

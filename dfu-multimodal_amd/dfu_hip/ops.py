@@ -321,9 +321,14 @@ def gemm_plan(M, N, K, a_mode, b_mode, epilogue, split_k=0, tile=0):
     return t.value, sk.value
 
 
-def gemm_set_persistent(enable):
-    """Select the GEMM schedule (dfu_gemm_set_persistent); returns the previous setting."""
-    return int(lib().dfu_gemm_set_persistent(int(bool(enable))))
+PERSISTENT_ALL = 3  # dfu_gemm_set_persistent: bit 0 generic tiles, bit 1 phased 256-wide tiles
+
+
+def gemm_set_persistent(mode):
+    """Select the GEMM schedule (dfu_gemm_set_persistent: 0 one workgroup per work unit
+    everywhere, PERSISTENT_ALL persistent everywhere, 2 the default); returns the previous
+    mode, which restores it exactly."""
+    return int(lib().dfu_gemm_set_persistent(int(mode)))
 
 
 def gemm_f32(M, N, K, A, sam, sak, B, sbn, sbk, C, ldc, bias=None, relu=False, accumulate=False):

@@ -10,7 +10,7 @@
  * implicit ATen ops; the comment on each names the reference call site.
  *
  * Conventions:
- *   - the library NEVER allocates; every pointer is caller-owned device memory;
+ *   - the library NEVER allocates device memory; every pointer is caller-owned;
  *   - activations are NHWC (ResNet) / [tokens][features] (ViT), bf16 = raw uint16 bits;
  *   - every call takes the HIP stream to enqueue on and returns 0 on success, otherwise a
  *     hipError_t value or a DFU_E_* code; dfu_last_error_string() gives the message;
@@ -164,10 +164,11 @@ int dfu_gemm_stats_tiles(int32_t M);
 int64_t dfu_gemm_workspace_bytes(const dfu_gemm_desc* desc);
 /* The tile (1..11, as dfu_gemm_desc.tile) and split-K the cost model picks for this descriptor. */
 int dfu_gemm_plan(const dfu_gemm_desc* desc, int32_t* tile, int32_t* split_k);
-/* GEMM schedule switch (tests, A/B timing): 1 (default) = persistent workgroups, each walking
- * several work units as one continuous K-step stream; 0 = one workgroup per work unit.  The
- * two give bitwise-identical results.  Returns the previous setting. */
-int dfu_gemm_set_persistent(int32_t enable);
+/* GEMM schedule switch (tests, A/B timing), a bit mask: bit 0 the generic tiles, bit 1 the
+ * persistent phased 256-wide tiles; set = persistent workgroups, each walking several work units
+ * as one continuous K-step stream; clear = one workgroup per work unit.  Default 2 (round 6).
+ * Every setting gives bitwise-identical results.  Returns the previous mask. */
+int dfu_gemm_set_persistent(int32_t mode);
 /* Split-K reduction switch: 1 = inside the GEMM when the descriptor carries tile
  * counters, 0 (default: measured faster) = the separate reduce kernel.  Bitwise-identical; returns the
  * previous setting. */

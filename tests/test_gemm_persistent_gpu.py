@@ -37,7 +37,7 @@ def gemm_t(*args, tile=0, **kw):
 def both_schedules(run):
     """[outputs under the persistent schedule, outputs with one workgroup per unit]."""
     res = []
-    for pers in (1, 0):
+    for pers in (ops.PERSISTENT_ALL, 0):
         old = ops.gemm_set_persistent(pers)
         try:
             res.append([t.clone() for t in run()])
