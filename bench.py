@@ -268,7 +268,7 @@ def cpu_baseline_gradcam(threads, budget_s=10.0):
 
 # The PMC traffic measurement this tree's bench line cites (tools/prof_summary.py output of the
 # separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; bench.py cannot read counters itself).
-TRAFFIC_FILE = os.path.join("profiles", "r25_gemm_traffic.json")  # parity-mode step (round 6)
+TRAFFIC_FILE = os.path.join("profiles", "r26_gemm_traffic.json")  # parity-mode step (round 6)
 
 
 def gemm_traffic():
