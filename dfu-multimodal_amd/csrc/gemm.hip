@@ -45,10 +45,13 @@ constexpr double kUnitUs[NTILES] = {1.0, 1.8, 1.7, 3.0, 1.2, 1.2, 3.0, 3.0, 3.0,
 // DFU_GEMM_PERSISTENT / DFU_GEMM_PERSISTENT_PS: A/B.
 int g_persistent = getenv("DFU_GEMM_PERSISTENT") ? atoi(getenv("DFU_GEMM_PERSISTENT")) : 0;
 int g_persistent_ps = getenv("DFU_GEMM_PERSISTENT_PS") ? atoi(getenv("DFU_GEMM_PERSISTENT_PS")) : 1;
-int g_inkernel_reduce = 0;  // dfu_gemm_set_inkernel_reduce (measured slower: off)
+// dfu_gemm_set_inkernel_reduce (measured slower: off); env DFU_GEMM_INKERNEL_REDUCE: A/B
+int g_inkernel_reduce =
+    getenv("DFU_GEMM_INKERNEL_REDUCE") ? atoi(getenv("DFU_GEMM_INKERNEL_REDUCE")) : 0;
 // the wave-split reduce for small planes (DFU_GEMM_WIDE_REDUCE=0 disables it: A/B timing)
 const int g_wide_reduce = getenv("DFU_GEMM_WIDE_REDUCE") ? atoi(getenv("DFU_GEMM_WIDE_REDUCE")) : 1;
-int g_tail_split = 1;       // dfu_gemm_set_tail_split
+// dfu_gemm_set_tail_split; env DFU_GEMM_TAIL_SPLIT: A/B
+int g_tail_split = getenv("DFU_GEMM_TAIL_SPLIT") ? atoi(getenv("DFU_GEMM_TAIL_SPLIT")) : 1;
 
 const Entry* find_entry(int a, int b, int e, int tile) {
   const Entry* tabs[NTILES] = {kTable128x128, kTable256x128, kTable128x256, kTable256x256,
